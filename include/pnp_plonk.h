@@ -1,0 +1,298 @@
+/*
+ * pnp_plonk.h — C-ABI boundary of the MI355X gen_proof backend.
+ *
+ * Drop-in replacement for the reference's CUDA library behind the Rust FFI:
+ *   Rust declaration   : plonk-core/src/lib.rs:52-239   (repr(C) structs + extern "C" gen_proof)
+ *   C implementation   : plonk-core/lib/hello.cu:4-6     (gen_proof -> prove)
+ *   C struct mirror    : plonk-core/lib/PLONK/src/structure.cuh:7-329
+ * (paths relative to /root/reference/Prize 1B/).
+ *
+ * Everything in section 1 is layout-identical to lib.rs, so the Rust host
+ * links this library instead of libzprize without source changes
+ * (see INTEGRATION.md).  Sections 2-4 are additive (v2) entry points: explicit
+ * lengths, error codes, resident (HBM) keys and the operator API used by the
+ * parity tests.  No torch or HIP types appear in any signature.
+ *
+ * Field encodings (identical to arkworks 0.3 / the reference):
+ *   Fr  : 4 x u64 little-endian limbs, Montgomery form R = 2^256 mod r
+ *   Fq  : 6 x u64 little-endian limbs, Montgomery form R = 2^384 mod q
+ *   G1 affine point: {Fq x, Fq y} (12 u64), no infinity flag;
+ *   the point at infinity is reported as x = 0, y = Fq::one (Montgomery),
+ *   as the reference's to_affine (PLONK/src/point.cu:29-47).
+ */
+#ifndef PNP_PLONK_H
+#define PNP_PLONK_H
+
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ------------------------------------------------------------------ */
+/* 1. v1 ABI — byte-for-byte the reference FFI (lib.rs:52-239)         */
+/* ------------------------------------------------------------------ */
+
+/* lib.rs:53-59 */
+typedef struct {
+    uint64_t a_eval[4];
+    uint64_t b_eval[4];
+    uint64_t c_eval[4];
+    uint64_t d_eval[4];
+} WireEvaluationsC;
+
+/* lib.rs:61-67 */
+typedef struct {
+    uint64_t left_sigma_eval[4];
+    uint64_t right_sigma_eval[4];
+    uint64_t out_sigma_eval[4];
+    uint64_t permutation_eval[4];
+} PermutationEvaluationsC;
+
+/* lib.rs:69-81 */
+typedef struct {
+    uint64_t q_arith_eval[4];
+    uint64_t q_c_eval[4];
+    uint64_t q_l_eval[4];
+    uint64_t q_r_eval[4];
+    uint64_t q_hl_eval[4];
+    uint64_t q_hr_eval[4];
+    uint64_t q_h4_eval[4];
+    uint64_t a_next_eval[4];
+    uint64_t b_next_eval[4];
+    uint64_t d_next_eval[4];
+} CustomEvaluationsC;
+
+/* lib.rs:101-111 */
+typedef struct {
+    uint64_t q_lookup_eval[4];
+    uint64_t z2_next_eval[4];
+    uint64_t h1_eval[4];
+    uint64_t h1_next_eval[4];
+    uint64_t h2_eval[4];
+    uint64_t f_eval[4];
+    uint64_t table_eval[4];
+    uint64_t table_next_eval[4];
+} LookupEvaluationsC;
+
+/* lib.rs:112-118 */
+typedef struct {
+    WireEvaluationsC wire_evals;
+    PermutationEvaluationsC perm_evals;
+    LookupEvaluationsC lookup_evals;
+    CustomEvaluationsC custom_evals;
+} ProofEvaluationsC;
+
+/* lib.rs:231-235 : affine G1, Montgomery Fq limbs */
+typedef struct {
+    uint64_t x[6];
+    uint64_t y[6];
+} CommitmentC;
+
+/* lib.rs:120-142 */
+typedef struct {
+    CommitmentC a_comm;
+    CommitmentC b_comm;
+    CommitmentC c_comm;
+    CommitmentC d_comm;
+    CommitmentC z_comm;
+    CommitmentC f_comm;
+    CommitmentC h_1_comm;
+    CommitmentC h_2_comm;
+    CommitmentC z_2_comm;
+    CommitmentC t_1_comm;
+    CommitmentC t_2_comm;
+    CommitmentC t_3_comm;
+    CommitmentC t_4_comm;
+    CommitmentC t_5_comm;
+    CommitmentC t_6_comm;
+    CommitmentC t_7_comm;
+    CommitmentC t_8_comm;
+    CommitmentC aw_opening;
+    CommitmentC saw_opening;
+    ProofEvaluationsC evaluations;
+} ProofC;
+
+/* lib.rs:144-155.  n = unpadded gate count; q_lookup/w_* hold n Montgomery Fr;
+ * pi holds ONE Fr in canonical (non-Montgomery) form (prover.rs:717-725). */
+typedef struct {
+    uint64_t n;
+    uint64_t lookup_len;
+    uint64_t intended_pi_pos;
+    uint64_t *q_lookup;
+    uint64_t *pi;
+    uint64_t *w_l;
+    uint64_t *w_r;
+    uint64_t *w_o;
+    uint64_t *w_4;
+} CircuitC;
+
+/* lib.rs:157-223.  With D = next_pow2(max(n, lookup_len)):
+ *   *_coeffs, table1..4 : D Montgomery Fr
+ *   *_evals, linear_evaluations, v_h_coset_8n : 8*D Montgomery Fr
+ * The coeff buffers of q_m, the four custom-gate selectors and q_lookup are
+ * empty Rust Vecs for the Merkle circuit and are never read (gen_proof.cuh:277,
+ * 319-329), exactly as in the reference. */
+typedef struct {
+    uint64_t *q_m_coeffs;
+    uint64_t *q_m_evals;
+    uint64_t *q_l_coeffs;
+    uint64_t *q_l_evals;
+    uint64_t *q_r_coeffs;
+    uint64_t *q_r_evals;
+    uint64_t *q_o_coeffs;
+    uint64_t *q_o_evals;
+    uint64_t *q_4_coeffs;
+    uint64_t *q_4_evals;
+    uint64_t *q_c_coeffs;
+    uint64_t *q_c_evals;
+    uint64_t *q_hl_coeffs;
+    uint64_t *q_hl_evals;
+    uint64_t *q_hr_coeffs;
+    uint64_t *q_hr_evals;
+    uint64_t *q_h4_coeffs;
+    uint64_t *q_h4_evals;
+    uint64_t *q_arith_coeffs;
+    uint64_t *q_arith_evals;
+    uint64_t *range_selector_coeffs;
+    uint64_t *range_selector_evals;
+    uint64_t *logic_selector_coeffs;
+    uint64_t *logic_selector_evals;
+    uint64_t *fixed_group_add_selector_coeffs;
+    uint64_t *fixed_group_add_selector_evals;
+    uint64_t *variable_group_add_selector_coeffs;
+    uint64_t *variable_group_add_selector_evals;
+    uint64_t *q_lookup_coeffs;
+    uint64_t *q_lookup_evals;
+    uint64_t *table1;
+    uint64_t *table2;
+    uint64_t *table3;
+    uint64_t *table4;
+    uint64_t *left_sigma_coeffs;
+    uint64_t *left_sigma_evals;
+    uint64_t *right_sigma_coeffs;
+    uint64_t *right_sigma_evals;
+    uint64_t *out_sigma_coeffs;
+    uint64_t *out_sigma_evals;
+    uint64_t *fourth_sigma_coeffs;
+    uint64_t *fourth_sigma_evals;
+    uint64_t *linear_evaluations;
+    uint64_t *v_h_coset_8n;
+} ProverKeyC;
+
+/* lib.rs:225-229.  powers_of_g: >= D affine points (12 u64 each);
+ * powers_of_gamma_g: 2 affine points (unused: hiding is disabled). */
+typedef struct {
+    const uint64_t *powers_of_g;
+    const uint64_t *powers_of_gamma_g;
+} CommitKeyC;
+
+/* lib.rs:237-239 / hello.cu:4-6.  Structs by value, ProofC returned by value.
+ * Synchronous, device 0.  On any device error it prints and exits, like the
+ * reference's CUDA_CHECK (caffe/common.hpp:23-30). */
+ProofC gen_proof(CircuitC circuit, ProverKeyC pk, CommitKeyC ck);
+
+/* ------------------------------------------------------------------ */
+/* 2. v2 ABI — explicit errors, resident keys (additive)               */
+/* ------------------------------------------------------------------ */
+
+#define PNP_OK              0
+#define PNP_E_ARG          -1   /* bad argument / size                      */
+#define PNP_E_DEVICE       -2   /* HIP runtime error                        */
+#define PNP_E_NOKEY        -3   /* prover / commit key not loaded           */
+#define PNP_E_ENVELOPE     -4   /* input outside the supported circuit class */
+#define PNP_E_NOMEM        -5   /* device allocation failed                 */
+
+typedef struct pnp_ctx pnp_ctx;
+
+/* Human-readable message of the last error on this thread. */
+const char *pnp_last_error(void);
+
+/* One context per GPU; owns the stream, twiddle tables, scratch and keys. */
+int pnp_ctx_create(int device, pnp_ctx **out);
+void pnp_ctx_destroy(pnp_ctx *ctx);
+
+/* Copy (or adopt) the prover key into HBM once; it stays resident for every
+ * later pnp_prove.  domain_size = D (power of two).  If `device_ptrs` is
+ * non-zero the pointers are HBM pointers that the context reads in place
+ * (they must outlive the context) instead of copying. */
+int pnp_load_prover_key(pnp_ctx *ctx, const ProverKeyC *pk, uint64_t domain_size,
+                        int device_ptrs);
+int pnp_load_commit_key(pnp_ctx *ctx, const CommitKeyC *ck, uint64_t n_points,
+                        int device_ptrs);
+
+/* Prove with the resident keys.  `device_ptrs`: the CircuitC witness pointers
+ * (q_lookup, w_*) are HBM pointers; pi is always a host pointer. */
+int pnp_prove(pnp_ctx *ctx, const CircuitC *cs, int device_ptrs, ProofC *out);
+
+/* Per-stage wall-clock (ms) of the last pnp_prove, for the bench/profiles.
+ * Writes up to `cap` doubles and their names; returns the stage count. */
+int pnp_last_stage_times(pnp_ctx *ctx, double *ms, const char **names, int cap);
+
+/* ------------------------------------------------------------------ */
+/* 3. Operator API on HBM pointers (mirrors PLONK/utils/function.cuh) */
+/*    All ops are asynchronous on the context stream; pnp_sync waits.  */
+/* ------------------------------------------------------------------ */
+
+int pnp_sync(pnp_ctx *ctx);
+
+/* In-place natural-order radix-2 NTT of 2^lg_n Montgomery Fr
+ * (function.cu:249-273 Ntt / Intt; arkworks fft / ifft semantics).
+ * inverse=1 multiplies by n^-1.  coset=1 applies the g=7 coset
+ * (forward: x_i *= g^i before, inverse: x_i *= g^-i after). */
+int pnp_ntt(pnp_ctx *ctx, uint64_t *d_inout, uint32_t lg_n, int inverse, int coset);
+
+/* Ntt_coset::forward (function.cu:261-267): zero-pad n -> 8n, coset NTT. */
+int pnp_coset_lde8(pnp_ctx *ctx, const uint64_t *d_coeffs, uint64_t *d_out8, uint32_t lg_n);
+
+/* commit (KZG/kzg10.cu:31-44): MSM of n affine points with n Montgomery
+ * scalars (converted to canonical inside, arithmetic.cu:3-8), result as
+ * affine Montgomery point (infinity -> x=0, y=Fq one). Synchronous. */
+int pnp_commit(pnp_ctx *ctx, const uint64_t *d_points, const uint64_t *d_scalars,
+               uint64_t n, CommitmentC *out);
+
+/* evaluate (function.cu:162-173): sum_i c_i x^i; x and result Montgomery,
+ * host-side scalars.  Synchronous. */
+int pnp_poly_eval(pnp_ctx *ctx, const uint64_t *d_coeffs, uint64_t n,
+                  const uint64_t x[4], uint64_t out[4]);
+
+/* poly_div_poly with c = -z (kzg10.cu:87-99): in place, p <- p / (X - z),
+ * remainder dropped, top coefficient set to zero. */
+int pnp_poly_div_linear(pnp_ctx *ctx, uint64_t *d_poly, uint64_t n, const uint64_t z[4]);
+
+/* accumulate_mul_poly (mont_arithmetic.cu:334-360): out[0]=1,
+ * out[i] = prod_{j<i} in[j]; in place. */
+int pnp_prefix_product(pnp_ctx *ctx, uint64_t *d_inout, uint64_t n);
+
+/* Batch inverse in place (inv(0) = 0, like the reference inv_mod kernel). */
+int pnp_batch_inverse(pnp_ctx *ctx, uint64_t *d_inout, uint64_t n);
+
+/* ------------------------------------------------------------------ */
+/* 4. Synthetic-input utilities (bench / test plumbing, not the path)  */
+/* ------------------------------------------------------------------ */
+
+/* d_out[i] = uniform-ish Montgomery Fr from a counter-based hash of (seed,i). */
+int pnp_synth_random_fr(pnp_ctx *ctx, uint64_t *d_out, uint64_t n, uint64_t seed);
+/* d_out[i] = tau^i * G1 generator, affine Montgomery (an SRS); tau Montgomery. */
+int pnp_synth_srs(pnp_ctx *ctx, uint64_t *d_out, uint64_t n, const uint64_t tau[4]);
+/* d_out[i] = (g * w_8n^i)^n - 1 (v_h on the 8n coset) and the coset points. */
+int pnp_synth_coset_consts(pnp_ctx *ctx, uint64_t *d_vh, uint64_t *d_x, uint32_t lg_n);
+
+#ifdef __cplusplus
+}  /* extern "C" */
+#endif
+
+#ifdef __cplusplus
+static_assert(sizeof(CommitmentC) == 96, "CommitmentC layout (lib.rs:231-235)");
+static_assert(sizeof(ProofEvaluationsC) == 26 * 32, "ProofEvaluationsC layout");
+static_assert(sizeof(ProofC) == 2656, "ProofC layout (lib.rs:120-142)");
+static_assert(sizeof(CircuitC) == 72, "CircuitC layout (lib.rs:144-155)");
+static_assert(sizeof(ProverKeyC) == 44 * 8, "ProverKeyC layout (lib.rs:157-223)");
+static_assert(sizeof(CommitKeyC) == 16, "CommitKeyC layout (lib.rs:225-229)");
+#else
+_Static_assert(sizeof(ProofC) == 2656, "ProofC layout (lib.rs:120-142)");
+_Static_assert(sizeof(ProverKeyC) == 44 * 8, "ProverKeyC layout (lib.rs:157-223)");
+#endif
+
+#endif /* PNP_PLONK_H */

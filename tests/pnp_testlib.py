@@ -1,0 +1,212 @@
+"""Shared helpers for the parity tests: field constants, limb packing, the
+oracle loader (oracle/liboracle.so, test infrastructure) and a seeded
+synthetic-input builder for the gen_proof ABI structs.
+
+Synthetic inputs mirror the Merkle-circuit prover key's structure
+(SURVEY.md §8a parity envelope): random witness wires, arithmetic selectors
+and sigma polynomials (8n coset evaluations = coset LDE of the coefficients),
+q_m / custom-gate selectors / q_lookup / lookup tables all zero, one public
+input, real coset points and Z_H values on the 8n coset, SRS = [tau^i] G.
+"""
+import ctypes as C
+import os
+import subprocess
+import sys
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(REPO, "zprize23-gpu-submission_amd")
+if PKG not in sys.path:
+    sys.path.insert(0, PKG)
+
+from pnp import abi  # noqa: E402
+
+R_MOD = 0x73eda753299d7d483339d80809a1d80553bda402fffe5bfeffffffff00000001
+Q_MOD = 0x1a0111ea397fe69a4b1ba7b6434bacd764774b84f38512bf6730d2a0f6b0f6241eabfffeb153ffffb9feffffffffaaab
+R_FR = pow(2, 256, R_MOD)
+R_FQ = pow(2, 384, Q_MOD)
+FR_ROOT32_MONT = [13381757501831005802, 6564924994866501612, 789602057691799140, 6625830629041353339]
+FR_GEN = 7
+
+
+def to_limbs(x: int, nlimbs: int):
+    return [(x >> (64 * i)) & 0xFFFFFFFFFFFFFFFF for i in range(nlimbs)]
+
+
+def from_limbs(limbs) -> int:
+    return sum(int(v) << (64 * i) for i, v in enumerate(limbs))
+
+
+def fr_mont(x: int) -> int:
+    return x * R_FR % R_MOD
+
+
+def fr_unmont(x: int) -> int:
+    return x * pow(R_FR, -1, R_MOD) % R_MOD
+
+
+def fq_mont(x: int) -> int:
+    return x * R_FQ % Q_MOD
+
+
+def fq_unmont(x: int) -> int:
+    return x * pow(R_FQ, -1, Q_MOD) % Q_MOD
+
+
+def fr_root(lg: int) -> int:
+    """canonical primitive 2^lg-th root of unity (domain.cu:29-36)"""
+    w = fr_unmont(from_limbs(FR_ROOT32_MONT))
+    return pow(w, 1 << (32 - lg), R_MOD)
+
+
+def ints_to_arr(vals, nlimbs=4) -> np.ndarray:
+    out = np.zeros((len(vals), nlimbs), dtype=np.uint64)
+    for i, v in enumerate(vals):
+        out[i] = to_limbs(int(v), nlimbs)
+    return out
+
+
+def arr_to_ints(arr) -> list:
+    a = np.asarray(arr, dtype=np.uint64).reshape(-1, arr.shape[-1] if arr.ndim > 1 else 4)
+    return [from_limbs(row) for row in a]
+
+
+def rand_fr_mont_arr(rng: np.random.Generator, n: int) -> np.ndarray:
+    """n Montgomery-form Fr values (uniform canonical values, then x*R mod r)."""
+    raw = rng.integers(0, 2**64, size=(n, 4), dtype=np.uint64)
+    raw[:, 3] &= np.uint64(0x7FFFFFFFFFFFFFFF)
+    vals = [from_limbs(r) % R_MOD for r in raw]
+    return ints_to_arr([fr_mont(v) for v in vals])
+
+
+def ptr_of(a: np.ndarray):
+    return a.ctypes.data_as(abi.U64P)
+
+
+# ------------------------------------------------------------------ oracle
+_ORACLE = None
+
+
+def build_oracle():
+    d = os.path.join(REPO, "oracle")
+    subprocess.run(["make", "-s", "-C", d, "liboracle.so"], check=True)
+
+
+def oracle():
+    """oracle/liboracle.so (built on demand).  Test infrastructure only."""
+    global _ORACLE
+    if _ORACLE is None:
+        build_oracle()
+        lib = C.CDLL(os.path.join(REPO, "oracle", "liboracle.so"))
+        vp = C.c_void_p
+        lib.or_ntt.argtypes = [vp, C.c_uint32, C.c_int, C.c_int]
+        lib.or_coset_lde8.argtypes = [vp, vp, C.c_uint32]
+        lib.or_poly_eval.argtypes = [vp, C.c_uint64, vp, vp]
+        lib.or_poly_div_linear.argtypes = [vp, C.c_uint64, vp]
+        lib.or_prefix_product.argtypes = [vp, C.c_uint64]
+        lib.or_batch_inverse.argtypes = [vp, C.c_uint64]
+        lib.or_srs.argtypes = [vp, C.c_uint64, vp]
+        lib.or_commit.argtypes = [vp, vp, C.c_uint64, vp]
+        lib.or_fr_vec_to_mont.argtypes = [vp, C.c_uint64]
+        lib.or_fr_vec_from_mont.argtypes = [vp, C.c_uint64]
+        lib.or_transcript_new.restype = vp
+        lib.or_transcript_new.argtypes = [C.c_char_p]
+        lib.or_transcript_free.argtypes = [vp]
+        lib.or_transcript_append_message.argtypes = [vp, C.c_char_p, vp, C.c_size_t]
+        lib.or_transcript_append_scalar.argtypes = [vp, C.c_char_p, vp]
+        lib.or_transcript_append_point.argtypes = [vp, C.c_char_p, vp]
+        lib.or_transcript_append_pi.argtypes = [vp, C.c_char_p, vp, C.c_uint64]
+        lib.or_transcript_challenge_bytes.argtypes = [vp, C.c_char_p, vp, C.c_size_t]
+        lib.or_transcript_challenge_scalar.argtypes = [vp, C.c_char_p, vp]
+        lib.or_gen_proof.argtypes = [vp, vp, vp, vp]
+        lib.or_gen_proof.restype = C.c_int
+        lib.or_num_threads.restype = C.c_int
+        _ORACLE = lib
+    return _ORACLE
+
+
+def vp(a: np.ndarray):
+    return C.c_void_p(a.ctypes.data)
+
+
+# ------------------------------------------------------------------ synthetic inputs
+PK_ZERO_EVALS = ("q_m_evals", "range_selector_evals", "logic_selector_evals",
+                 "fixed_group_add_selector_evals", "variable_group_add_selector_evals",
+                 "q_lookup_evals")
+PK_RANDOM_COEFFS = ("q_l", "q_r", "q_o", "q_4", "q_c", "q_hl", "q_hr", "q_h4", "q_arith",
+                    "left_sigma", "right_sigma", "out_sigma", "fourth_sigma")
+
+
+class Inputs:
+    """Host-resident synthetic gen_proof inputs + the ctypes structs over them."""
+
+    def __init__(self, lg_n: int, seed: int, n_gates: int | None = None, pi_pos: int = 3):
+        lib = oracle()
+        rng = np.random.default_rng(seed)
+        n = 1 << lg_n
+        N8 = 8 * n
+        self.lg_n, self.n = lg_n, n
+        self.n_gates = n_gates if n_gates is not None else n - 3
+        self.arrays = {}
+        a = self.arrays
+        for w in ("w_l", "w_r", "w_o", "w_4"):
+            a[w] = rand_fr_mont_arr(rng, self.n_gates)
+        a["q_lookup"] = np.zeros((self.n_gates, 4), dtype=np.uint64)
+        a["pi"] = np.array(to_limbs(int(rng.integers(1, 2**62)), 4), dtype=np.uint64)
+        self.pi_pos = pi_pos
+        for name in PK_RANDOM_COEFFS:
+            c = rand_fr_mont_arr(rng, n)
+            e = np.zeros((N8, 4), dtype=np.uint64)
+            lib.or_coset_lde8(vp(c), vp(e), lg_n)
+            a[name + "_coeffs"] = c
+            a[name + "_evals"] = e
+        for name in PK_ZERO_EVALS:
+            a[name] = np.zeros((N8, 4), dtype=np.uint64)
+        for t in ("table1", "table2", "table3", "table4"):
+            a[t] = np.zeros((n, 4), dtype=np.uint64)
+        # linear_evaluations = coset points g*w^i; v_h = (g w^i)^n - 1
+        w8 = fr_root(lg_n + 3)
+        xs, vh = [], []
+        x = FR_GEN
+        gn = pow(FR_GEN, n, R_MOD)
+        w8n = pow(w8, n, R_MOD)
+        vv = gn
+        for i in range(N8):
+            xs.append(fr_mont(x))
+            vh.append(fr_mont((vv - 1) % R_MOD))
+            x = x * w8 % R_MOD
+            vv = vv * w8n % R_MOD
+        a["linear_evaluations"] = ints_to_arr(xs)
+        a["v_h_coset_8n"] = ints_to_arr(vh)
+        # SRS: [tau^i] G for i < n, affine Montgomery
+        tau = rand_fr_mont_arr(rng, 1)
+        self.tau_mont = tau
+        srs = np.zeros((n, 12), dtype=np.uint64)
+        lib.or_srs(vp(srs), n, vp(tau))
+        a["srs"] = srs
+        a["gamma_g"] = np.zeros((2, 12), dtype=np.uint64)
+        a["empty"] = np.zeros((1, 4), dtype=np.uint64)
+        self._build_structs()
+
+    def _build_structs(self):
+        a = self.arrays
+        self.circuit = abi.CircuitC(
+            n=self.n_gates, lookup_len=0, intended_pi_pos=self.pi_pos,
+            q_lookup=ptr_of(a["q_lookup"]), pi=ptr_of(a["pi"]), w_l=ptr_of(a["w_l"]),
+            w_r=ptr_of(a["w_r"]), w_o=ptr_of(a["w_o"]), w_4=ptr_of(a["w_4"]))
+        pk = abi.ProverKeyC()
+        for f in abi.PK_FIELDS:
+            key = f if f in a else None
+            if key is None:
+                # empty coeff vectors (q_m, custom selectors, q_lookup)
+                key = "empty"
+            setattr(pk, f, ptr_of(a[key]))
+        self.pk = pk
+        self.ck = abi.CommitKeyC(powers_of_g=ptr_of(a["srs"]), powers_of_gamma_g=ptr_of(a["gamma_g"]))
+
+    def oracle_proof(self) -> abi.ProofC:
+        lib = oracle()
+        out = abi.ProofC()
+        rc = lib.or_gen_proof(C.byref(self.circuit), C.byref(self.pk), C.byref(self.ck), C.byref(out))
+        assert rc == 0, rc
+        return out
