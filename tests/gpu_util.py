@@ -1,0 +1,19 @@
+"""Device-memory plumbing for the GPU parity tests (torch = allocator only)."""
+import numpy as np
+
+
+def to_dev(arr: np.ndarray):
+    import torch
+    a = np.ascontiguousarray(arr).view(np.int64)
+    return torch.from_numpy(a.copy()).to("cuda")
+
+
+def from_dev(t, shape_last=4) -> np.ndarray:
+    import torch
+    torch.cuda.synchronize()
+    return t.cpu().numpy().view(np.uint64).reshape(-1, shape_last)
+
+
+def empty_dev(n_elems: int, limbs: int = 4):
+    import torch
+    return torch.zeros((n_elems, limbs), dtype=torch.int64, device="cuda")

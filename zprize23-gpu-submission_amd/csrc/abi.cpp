@@ -1,0 +1,300 @@
+// abi.cpp — the extern "C" boundary (include/pnp_plonk.h).
+//
+// v1 gen_proof keeps the reference's contract (lib/hello.cu:4-6,
+// plonk-core/src/lib.rs:237-239): structs by value, ProofC by value,
+// synchronous, device 0, print-and-exit on device errors (caffe/common.hpp:
+// 23-30).  v2 functions return PNP_* codes and never exit.
+#include <stdarg.h>
+#include <stdlib.h>
+#include <string.h>
+#include "context.h"
+#include "ec.cuh"
+#include "protocol.h"
+
+namespace pnp {
+
+static thread_local char g_err[512] = "";
+
+void set_error(const char *fmt, ...) {
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(g_err, sizeof g_err, fmt, ap);
+    va_end(ap);
+}
+
+void DevBuf::alloc(size_t b) {
+    release();
+    if (b == 0) b = 16;
+    hipError_t e = hipMalloc(&p, b);
+    if (e != hipSuccess) {
+        p = nullptr;
+        set_error("hipMalloc(%zu) failed: %s", b, hipGetErrorString(e));
+        throw Error(PNP_E_NOMEM);
+    }
+    bytes = b;
+}
+void DevBuf::release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    bytes = 0;
+}
+
+void commit_affine(pnp_ctx *ctx, const uint64_t *d_scalars, uint64_t n, CommitmentC *out) {
+    uint64_t xyzz[24], aff[12];
+    msm_run(ctx->msm, ctx->ck_dev, d_scalars, n, xyzz, ctx->stream);
+    xyzz_to_affine_host(xyzz, aff);
+    memcpy(out->x, aff, 48);
+    memcpy(out->y, aff + 6, 48);
+}
+
+}  // namespace pnp
+
+uint64_t *pnp_ctx::buf(const std::string &name, size_t elems_fr) {
+    auto &b = work[name];
+    if (b.bytes < elems_fr * 32) b.alloc(elems_fr * 32);
+    return b.u64();
+}
+
+using namespace pnp;
+
+#define PNP_TRY(...)                                   \
+    try {                                              \
+        __VA_ARGS__;                                   \
+        return PNP_OK;                                 \
+    } catch (const Error &e) {                         \
+        return e.code;                                 \
+    } catch (const std::exception &e) {                \
+        set_error("exception: %s", e.what());          \
+        return PNP_E_DEVICE;                           \
+    }
+
+extern "C" {
+
+const char *pnp_last_error(void) { return g_err; }
+
+int pnp_ctx_create(int device, pnp_ctx **out) {
+    if (!out) return PNP_E_ARG;
+    pnp_ctx *c = new pnp_ctx();
+    try {
+        c->device = device;
+        PNP_HIP(hipSetDevice(device));
+        PNP_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    } catch (const Error &e) {
+        delete c;
+        return e.code;
+    }
+    *out = c;
+    return PNP_OK;
+}
+
+void pnp_ctx_destroy(pnp_ctx *ctx) {
+    if (!ctx) return;
+    (void)hipSetDevice(ctx->device);
+    (void)hipStreamSynchronize(ctx->stream);
+    (void)hipStreamDestroy(ctx->stream);
+    delete ctx;
+}
+
+int pnp_sync(pnp_ctx *ctx) {
+    PNP_TRY(PNP_HIP(hipStreamSynchronize(ctx->stream)));
+}
+
+int pnp_ntt(pnp_ctx *ctx, uint64_t *d, uint32_t lg_n, int inverse, int coset) {
+    if (!ctx || !d || lg_n > 28) return PNP_E_ARG;
+    PNP_TRY(ntt_run(ctx->ntt, d, lg_n, inverse != 0, coset != 0, ctx->stream));
+}
+
+int pnp_coset_lde8(pnp_ctx *ctx, const uint64_t *in, uint64_t *out8, uint32_t lg_n) {
+    if (!ctx || !in || !out8 || lg_n > 25) return PNP_E_ARG;
+    PNP_TRY(coset_lde8(ctx->ntt, in, out8, lg_n, ctx->stream));
+}
+
+int pnp_commit(pnp_ctx *ctx, const uint64_t *d_points, const uint64_t *d_scalars, uint64_t n,
+               CommitmentC *out) {
+    if (!ctx || !out || (n && (!d_points || !d_scalars))) return PNP_E_ARG;
+    PNP_TRY({
+        uint64_t xyzz[24], aff[12];
+        msm_run(ctx->msm, d_points, d_scalars, n, xyzz, ctx->stream);
+        xyzz_to_affine_host(xyzz, aff);
+        memcpy(out->x, aff, 48);
+        memcpy(out->y, aff + 6, 48);
+    });
+}
+
+int pnp_poly_eval(pnp_ctx *ctx, const uint64_t *d, uint64_t n, const uint64_t x[4], uint64_t out[4]) {
+    if (!ctx || !d || !x || !out) return PNP_E_ARG;
+    PNP_TRY({
+        Fr r;
+        k_poly_eval(d, n, from_u64_limbs<FrP>(x), ctx->scratch_a, &r, ctx->stream);
+        to_u64_limbs(r, out);
+    });
+}
+
+int pnp_poly_div_linear(pnp_ctx *ctx, uint64_t *d, uint64_t n, const uint64_t z[4]) {
+    if (!ctx || !d || !z) return PNP_E_ARG;
+    PNP_TRY(k_poly_div_linear(d, n, from_u64_limbs<FrP>(z), ctx->scratch_a, ctx->stream));
+}
+
+int pnp_prefix_product(pnp_ctx *ctx, uint64_t *d, uint64_t n) {
+    if (!ctx || !d) return PNP_E_ARG;
+    PNP_TRY(k_prefix_product(d, n, ctx->scratch_a, ctx->stream));
+}
+
+int pnp_batch_inverse(pnp_ctx *ctx, uint64_t *d, uint64_t n) {
+    if (!ctx || !d) return PNP_E_ARG;
+    PNP_TRY(k_batch_inverse(d, n, ctx->scratch_a, ctx->stream));
+}
+
+int pnp_synth_random_fr(pnp_ctx *ctx, uint64_t *d, uint64_t n, uint64_t seed) {
+    if (!ctx || !d) return PNP_E_ARG;
+    PNP_TRY(k_random_fr(d, n, seed, ctx->stream));
+}
+
+int pnp_synth_srs(pnp_ctx *ctx, uint64_t *d, uint64_t n, const uint64_t tau[4]) {
+    if (!ctx || !d || !tau) return PNP_E_ARG;
+    PNP_TRY(k_srs(d, n, from_u64_limbs<FrP>(tau), ctx->stream));
+}
+
+int pnp_synth_coset_consts(pnp_ctx *ctx, uint64_t *d_vh, uint64_t *d_x, uint32_t lg_n) {
+    if (!ctx || lg_n > 25) return PNP_E_ARG;
+    PNP_TRY(k_coset_consts(d_vh, d_x, lg_n, ctx->stream));
+}
+
+}  // extern "C"
+
+// ---------------------------------------------------------------- keys + prove
+namespace {
+
+enum FieldKind { kSkip, kEvals8, kCoeffs, kCheckZero8, kTableZero };
+
+// ProverKeyC field order (lib.rs:157-223) -> how gen_proof uses it
+const FieldKind kPkKinds[44] = {
+    kSkip, kEvals8,                                   // q_m coeffs (empty) / evals
+    kCoeffs, kEvals8, kCoeffs, kEvals8, kCoeffs, kEvals8, kCoeffs, kEvals8,  // q_l q_r q_o q_4
+    kCoeffs, kEvals8, kCoeffs, kEvals8, kCoeffs, kEvals8, kCoeffs, kEvals8,  // q_c q_hl q_hr q_h4
+    kCoeffs, kEvals8,                                 // q_arith
+    kSkip, kCheckZero8, kSkip, kCheckZero8,           // range, logic selectors
+    kSkip, kCheckZero8, kSkip, kCheckZero8,           // fixed / variable group add selectors
+    kSkip, kEvals8,                                   // q_lookup coeffs (empty) / evals
+    kTableZero, kTableZero, kTableZero, kTableZero,   // table1..4
+    kCoeffs, kEvals8, kCoeffs, kEvals8, kCoeffs, kEvals8, kCoeffs, kEvals8,  // sigmas
+    kEvals8, kEvals8};                                // linear_evaluations, v_h_coset_8n
+
+bool host_all_zero(const uint64_t *p, uint64_t words) {
+    uint64_t acc = 0;
+    for (uint64_t i = 0; i < words; i++) acc |= p[i];
+    return acc == 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+int pnp_load_prover_key(pnp_ctx *ctx, const ProverKeyC *pk, uint64_t D, int device_ptrs) {
+    if (!ctx || !pk || D == 0 || (D & (D - 1)) || D > (1ULL << 25)) return PNP_E_ARG;
+    PNP_TRY({
+        PNP_HIP(hipSetDevice(ctx->device));
+        ctx->pk_loaded = false;
+        ctx->pk_owned.clear();
+        ProverKeyC dev{};
+        uint64_t *const *src = reinterpret_cast<uint64_t *const *>(pk);
+        uint64_t **dst = reinterpret_cast<uint64_t **>(&dev);
+        for (int f = 0; f < 44; f++) {
+            FieldKind k = kPkKinds[f];
+            dst[f] = nullptr;
+            if (k == kSkip) continue;
+            uint64_t elems = (k == kEvals8 || k == kCheckZero8) ? 8 * D : D;
+            if (!src[f]) {
+                set_error("prover key field %d is null", f);
+                throw Error(PNP_E_ARG);
+            }
+            if (k == kCheckZero8 || k == kTableZero) {
+                bool nz = device_ptrs ? pnp::k_any_nonzero(src[f], 4 * elems, ctx->scratch_b, ctx->stream)
+                                      : !host_all_zero(src[f], 4 * elems);
+                if (nz) {
+                    set_error("prover key field %d is non-zero: custom-gate selectors and lookup "
+                              "tables must be zero (reference parity envelope, SURVEY.md 8a)", f);
+                    throw Error(PNP_E_ENVELOPE);
+                }
+                if (k == kCheckZero8) continue;
+            }
+            if (device_ptrs) {
+                dst[f] = src[f];
+            } else {
+                ctx->pk_owned.emplace_back(elems * 32);
+                PNP_HIP(hipMemcpyAsync(ctx->pk_owned.back().p, src[f], elems * 32,
+                                       hipMemcpyHostToDevice, ctx->stream));
+                dst[f] = ctx->pk_owned.back().u64();
+            }
+        }
+        PNP_HIP(hipStreamSynchronize(ctx->stream));
+        ctx->pk_dev = dev;
+        ctx->pk_n = D;
+        ctx->pk_loaded = true;
+    });
+}
+
+int pnp_load_commit_key(pnp_ctx *ctx, const CommitKeyC *ck, uint64_t n_points, int device_ptrs) {
+    if (!ctx || !ck || !ck->powers_of_g || n_points == 0) return PNP_E_ARG;
+    PNP_TRY({
+        PNP_HIP(hipSetDevice(ctx->device));
+        ctx->ck_loaded = false;
+        if (device_ptrs) {
+            ctx->ck_owned.release();
+            ctx->ck_dev = ck->powers_of_g;
+        } else {
+            ctx->ck_owned.alloc(n_points * 96);
+            PNP_HIP(hipMemcpyAsync(ctx->ck_owned.p, ck->powers_of_g, n_points * 96,
+                                   hipMemcpyHostToDevice, ctx->stream));
+            PNP_HIP(hipStreamSynchronize(ctx->stream));
+            ctx->ck_dev = ctx->ck_owned.u64();
+        }
+        ctx->ck_points = n_points;
+        ctx->ck_loaded = true;
+    });
+}
+
+int pnp_prove(pnp_ctx *ctx, const CircuitC *cs, int device_ptrs, ProofC *out) {
+    if (!ctx || !cs || !out) return PNP_E_ARG;
+    try {
+        return prove_impl(ctx, cs, device_ptrs, out);
+    } catch (const Error &e) {
+        return e.code;
+    }
+}
+
+int pnp_last_stage_times(pnp_ctx *ctx, double *ms, const char **names, int cap) {
+    if (!ctx) return 0;
+    int k = 0;
+    for (auto &st : ctx->stages) {
+        if (k < cap) {
+            if (ms) ms[k] = st.second;
+            if (names) names[k] = st.first.c_str();
+        }
+        k++;
+    }
+    return k;
+}
+
+// v1: lib/hello.cu:4-6.  Copies the keys per call like the reference
+// (load.cu:311-358); errors print and exit (caffe/common.hpp:23-30).
+ProofC gen_proof(CircuitC circuit, ProverKeyC pk, CommitKeyC ck) {
+    static pnp_ctx *ctx = nullptr;
+    ProofC out;
+    memset(&out, 0, sizeof out);
+    auto die = [](int rc) {
+        fprintf(stderr, "gen_proof: error %d: %s\n", rc, pnp_last_error());
+        exit(EXIT_FAILURE);
+    };
+    int rc;
+    if (!ctx && (rc = pnp_ctx_create(0, &ctx)) != PNP_OK) die(rc);
+    uint64_t bound = circuit.n > circuit.lookup_len ? circuit.n : circuit.lookup_len;
+    uint64_t D = 1;
+    while (D < bound) D <<= 1;
+    if ((rc = pnp_load_prover_key(ctx, &pk, D, 0)) != PNP_OK) die(rc);
+    if ((rc = pnp_load_commit_key(ctx, &ck, D, 0)) != PNP_OK) die(rc);
+    if ((rc = pnp_prove(ctx, &circuit, 0, &out)) != PNP_OK) die(rc);
+    return out;
+}
+
+}  // extern "C"

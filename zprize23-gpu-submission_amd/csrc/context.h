@@ -1,0 +1,38 @@
+// context.h — the per-GPU context behind the C-ABI (replaces the reference's
+// per-op SyncedMemory allocation, lib/caffe/syncedmem.cpp): one stream, the
+// NTT tables, MSM work buffers, a scratch pool and the HBM-resident keys.
+#pragma once
+#include "pnp_internal.h"
+#include <array>
+#include <memory>
+
+struct pnp_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    pnp::NttTables ntt;
+    pnp::MsmWork msm;
+    pnp::DevBuf scratch_a, scratch_b;
+
+    // ---- resident prover key (ProverKeyC mirrored in HBM) ----
+    bool pk_loaded = false;
+    uint64_t pk_n = 0;                     // domain size D
+    std::vector<pnp::DevBuf> pk_owned;     // copies (device_ptrs == 0)
+    ProverKeyC pk_dev{};                   // HBM pointers for every field
+    // ---- resident commit key ----
+    bool ck_loaded = false;
+    uint64_t ck_points = 0;
+    pnp::DevBuf ck_owned;
+    const uint64_t *ck_dev = nullptr;
+
+    // ---- per-proof working set (sized on first use, reused) ----
+    std::map<std::string, pnp::DevBuf> work;
+    uint64_t *buf(const std::string &name, size_t elems_fr);
+
+    // ---- stage timing of the last proof ----
+    std::vector<std::pair<std::string, double>> stages;
+};
+
+namespace pnp {
+void commit_affine(pnp_ctx *ctx, const uint64_t *d_scalars, uint64_t n, CommitmentC *out);
+int prove_impl(pnp_ctx *ctx, const CircuitC *cs, int device_ptrs, ProofC *out);
+}  // namespace pnp

@@ -1,0 +1,289 @@
+// field.cuh — BLS12-381 Fr / Fq Montgomery arithmetic for gfx950 (and host).
+//
+// Semantics restated from lib/PLONK/utils/mont/cuda/ff/mont_t.cuh (Montgomery
+// form, R = 2^256 / 2^384, fully reduced residues) with the constants of
+// ff/bls12-381.hpp:7-93.  The implementation is CDNA-first: 32-bit limbs so the
+// inner products map to v_mad_u64_u32 (32x32+64 -> 64, one VALU op per limb
+// product), carry chains through 64-bit adds (v_add_co / v_addc_co), and the
+// "no-carry" CIOS variant, valid because both moduli leave the top bit of the
+// top 32-bit word clear (r: 0x73eda753.., q: 0x1a0111ea..).  An element is 8 /
+// 12 VGPRs; memory layout equals the reference's 4 / 6 little-endian u64 limbs.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define PNP_HD __host__ __device__ __forceinline__
+#define PNP_LIMB(x) (uint32_t)(x##ULL), (uint32_t)(x##ULL >> 32)
+
+namespace pnp {
+
+struct FrP {
+    static constexpr int N = 8;
+    static constexpr uint32_t INV = 0xffffffffu;  // -r^-1 mod 2^32
+    static constexpr uint32_t P[8] = {PNP_LIMB(0xffffffff00000001), PNP_LIMB(0x53bda402fffe5bfe),
+                                      PNP_LIMB(0x3339d80809a1d805), PNP_LIMB(0x73eda753299d7d48)};
+    static constexpr uint32_t ONE[8] = {PNP_LIMB(0x00000001fffffffe), PNP_LIMB(0x5884b7fa00034802),
+                                        PNP_LIMB(0x998c4fefecbc4ff5), PNP_LIMB(0x1824b159acc5056f)};
+    static constexpr uint32_t R2[8] = {PNP_LIMB(0xc999e990f3f29c6d), PNP_LIMB(0x2b6cedcb87925c23),
+                                       PNP_LIMB(0x05d314967254398f), PNP_LIMB(0x0748d9d99f59ff11)};
+    // r - 2 (Fermat exponent)
+    static constexpr uint32_t PM2[8] = {PNP_LIMB(0xfffffffeffffffff), PNP_LIMB(0x53bda402fffe5bfe),
+                                        PNP_LIMB(0x3339d80809a1d805), PNP_LIMB(0x73eda753299d7d48)};
+};
+
+struct FqP {
+    static constexpr int N = 12;
+    static constexpr uint32_t INV = 0xfffcfffdu;  // -q^-1 mod 2^32
+    static constexpr uint32_t P[12] = {PNP_LIMB(0xb9feffffffffaaab), PNP_LIMB(0x1eabfffeb153ffff),
+                                       PNP_LIMB(0x6730d2a0f6b0f624), PNP_LIMB(0x64774b84f38512bf),
+                                       PNP_LIMB(0x4b1ba7b6434bacd7), PNP_LIMB(0x1a0111ea397fe69a)};
+    static constexpr uint32_t ONE[12] = {PNP_LIMB(0x760900000002fffd), PNP_LIMB(0xebf4000bc40c0002),
+                                         PNP_LIMB(0x5f48985753c758ba), PNP_LIMB(0x77ce585370525745),
+                                         PNP_LIMB(0x5c071a97a256ec6d), PNP_LIMB(0x15f65ec3fa80e493)};
+    static constexpr uint32_t R2[12] = {PNP_LIMB(0xf4df1f341c341746), PNP_LIMB(0x0a76e6a609d104f1),
+                                        PNP_LIMB(0x8de5476c4c95b6d5), PNP_LIMB(0x67eb88a9939d83c0),
+                                        PNP_LIMB(0x9a793e85b519952d), PNP_LIMB(0x11988fe592cae3aa)};
+    static constexpr uint32_t PM2[12] = {PNP_LIMB(0xb9feffffffffaaa9), PNP_LIMB(0x1eabfffeb153ffff),
+                                         PNP_LIMB(0x6730d2a0f6b0f624), PNP_LIMB(0x64774b84f38512bf),
+                                         PNP_LIMB(0x4b1ba7b6434bacd7), PNP_LIMB(0x1a0111ea397fe69a)};
+};
+
+template <class P>
+struct Fp {
+    static constexpr int N = P::N;
+    uint32_t v[N];
+
+    PNP_HD static Fp zero() {
+        Fp r;
+#pragma unroll
+        for (int i = 0; i < N; i++) r.v[i] = 0;
+        return r;
+    }
+    PNP_HD static Fp one() {
+        Fp r;
+#pragma unroll
+        for (int i = 0; i < N; i++) r.v[i] = P::ONE[i];
+        return r;
+    }
+    PNP_HD static Fp r2() {
+        Fp r;
+#pragma unroll
+        for (int i = 0; i < N; i++) r.v[i] = P::R2[i];
+        return r;
+    }
+    PNP_HD static Fp modulus() {
+        Fp r;
+#pragma unroll
+        for (int i = 0; i < N; i++) r.v[i] = P::P[i];
+        return r;
+    }
+    PNP_HD bool is_zero() const {
+        uint32_t acc = 0;
+#pragma unroll
+        for (int i = 0; i < N; i++) acc |= v[i];
+        return acc == 0;
+    }
+    PNP_HD bool operator==(const Fp &o) const {
+        uint32_t acc = 0;
+#pragma unroll
+        for (int i = 0; i < N; i++) acc |= v[i] ^ o.v[i];
+        return acc == 0;
+    }
+    PNP_HD bool operator!=(const Fp &o) const { return !(*this == o); }
+};
+
+using Fr = Fp<FrP>;
+using Fq = Fp<FqP>;
+
+// ---- raw multi-limb helpers ----
+template <int N>
+PNP_HD uint32_t add_n(uint32_t *r, const uint32_t *a, const uint32_t *b) {
+    uint64_t c = 0;
+#pragma unroll
+    for (int i = 0; i < N; i++) {
+        c = (uint64_t)a[i] + b[i] + (c >> 32);
+        r[i] = (uint32_t)c;
+    }
+    return (uint32_t)(c >> 32);
+}
+template <int N>
+PNP_HD uint32_t sub_n(uint32_t *r, const uint32_t *a, const uint32_t *b) {
+    uint32_t br = 0;
+#pragma unroll
+    for (int i = 0; i < N; i++) {
+        uint64_t d = (uint64_t)a[i] - b[i] - br;
+        r[i] = (uint32_t)d;
+        br = (uint32_t)(d >> 32) & 1u;
+    }
+    return br;
+}
+
+// r = a - P if a >= P else a   (a < 2P)
+template <class P>
+PNP_HD void reduce_once(Fp<P> &a) {
+    constexpr int N = P::N;
+    uint32_t t[N];
+    uint32_t br = sub_n<N>(t, a.v, P::P);
+#pragma unroll
+    for (int i = 0; i < N; i++) a.v[i] = br ? a.v[i] : t[i];
+}
+
+template <class P>
+PNP_HD Fp<P> operator+(const Fp<P> &a, const Fp<P> &b) {
+    Fp<P> r;
+    add_n<P::N>(r.v, a.v, b.v);  // < 2P < 2^(32N): no carry out for both moduli
+    reduce_once(r);
+    return r;
+}
+template <class P>
+PNP_HD Fp<P> operator-(const Fp<P> &a, const Fp<P> &b) {
+    constexpr int N = P::N;
+    Fp<P> r;
+    uint32_t br = sub_n<N>(r.v, a.v, b.v);
+    uint32_t t[N];
+    add_n<N>(t, r.v, P::P);
+#pragma unroll
+    for (int i = 0; i < N; i++) r.v[i] = br ? t[i] : r.v[i];
+    return r;
+}
+template <class P>
+PNP_HD Fp<P> neg(const Fp<P> &a) {
+    return Fp<P>::zero() - a;
+}
+template <class P>
+PNP_HD Fp<P> dbl(const Fp<P> &a) {
+    return a + a;
+}
+
+// Montgomery product, "no-carry" CIOS on 32-bit limbs (requires the top word
+// of P below 2^31 - 1, true for r and q).  2N^2 v_mad_u64_u32.
+template <class P>
+PNP_HD Fp<P> operator*(const Fp<P> &a, const Fp<P> &b) {
+    constexpr int N = P::N;
+    uint32_t t[N];
+#pragma unroll
+    for (int j = 0; j < N; j++) t[j] = 0;
+#pragma unroll
+    for (int i = 0; i < N; i++) {
+        uint64_t A = (uint64_t)a.v[0] * b.v[i] + t[0];
+        t[0] = (uint32_t)A;
+        uint32_t m = t[0] * P::INV;
+        uint64_t C = (uint64_t)m * P::P[0] + t[0];
+#pragma unroll
+        for (int j = 1; j < N; j++) {
+            A = (uint64_t)a.v[j] * b.v[i] + t[j] + (A >> 32);
+            t[j] = (uint32_t)A;
+            C = (uint64_t)m * P::P[j] + t[j] + (C >> 32);
+            t[j - 1] = (uint32_t)C;
+        }
+        t[N - 1] = (uint32_t)(A >> 32) + (uint32_t)(C >> 32);
+    }
+    Fp<P> r;
+#pragma unroll
+    for (int j = 0; j < N; j++) r.v[j] = t[j];
+    reduce_once(r);
+    return r;
+}
+template <class P>
+PNP_HD Fp<P> sqr(const Fp<P> &a) {
+    return a * a;
+}
+
+template <class P>
+PNP_HD Fp<P> &operator+=(Fp<P> &a, const Fp<P> &b) { return a = a + b; }
+template <class P>
+PNP_HD Fp<P> &operator-=(Fp<P> &a, const Fp<P> &b) { return a = a - b; }
+template <class P>
+PNP_HD Fp<P> &operator*=(Fp<P> &a, const Fp<P> &b) { return a = a * b; }
+
+template <class P>
+PNP_HD Fp<P> to_mont(const Fp<P> &a) { return a * Fp<P>::r2(); }
+template <class P>
+PNP_HD Fp<P> from_mont(const Fp<P> &a) {
+    Fp<P> one_raw = Fp<P>::zero();
+    one_raw.v[0] = 1;
+    return a * one_raw;
+}
+
+// x^e for a small exponent (exp_mod_kernel_, mont_arithmetic.cu:89)
+template <class P>
+PNP_HD Fp<P> pow_u64(Fp<P> base, uint64_t e) {
+    Fp<P> acc = Fp<P>::one();
+    while (e) {
+        if (e & 1) acc = acc * base;
+        base = base * base;
+        e >>= 1;
+    }
+    return acc;
+}
+
+// Fermat inverse a^(P-2); inv(0) = 0 (inv_mod_kernel_, mont_arithmetic.cu:73)
+template <class P>
+PNP_HD Fp<P> inverse(const Fp<P> &a) {
+    Fp<P> acc = Fp<P>::one();
+    for (int w = P::N - 1; w >= 0; w--) {
+        uint32_t e = P::PM2[w];
+        for (int b = 31; b >= 0; b--) {
+            acc = acc * acc;
+            if ((e >> b) & 1) acc = acc * a;
+        }
+    }
+    return acc;
+}
+
+// canonical compare a > b (gt_zkp, zk_function.cu:3-22)
+template <class P>
+PNP_HD bool gt(const Fp<P> &a, const Fp<P> &b) {
+    for (int i = P::N - 1; i >= 0; i--) {
+        if (a.v[i] > b.v[i]) return true;
+        if (a.v[i] < b.v[i]) return false;
+    }
+    return false;
+}
+
+// ---- memory helpers: 32-byte Fr as two 16-byte accesses ----
+__device__ __forceinline__ Fr load_fr(const uint64_t *base, uint64_t i) {
+    const uint4 *p = reinterpret_cast<const uint4 *>(base + 4 * i);
+    uint4 lo = p[0], hi = p[1];
+    Fr r;
+    r.v[0] = lo.x; r.v[1] = lo.y; r.v[2] = lo.z; r.v[3] = lo.w;
+    r.v[4] = hi.x; r.v[5] = hi.y; r.v[6] = hi.z; r.v[7] = hi.w;
+    return r;
+}
+__device__ __forceinline__ void store_fr(uint64_t *base, uint64_t i, const Fr &a) {
+    uint4 *p = reinterpret_cast<uint4 *>(base + 4 * i);
+    p[0] = make_uint4(a.v[0], a.v[1], a.v[2], a.v[3]);
+    p[1] = make_uint4(a.v[4], a.v[5], a.v[6], a.v[7]);
+}
+__device__ __forceinline__ Fq load_fq(const uint64_t *base) {
+    const uint4 *p = reinterpret_cast<const uint4 *>(base);
+    uint4 a = p[0], b = p[1], c = p[2];
+    Fq r;
+    r.v[0] = a.x; r.v[1] = a.y; r.v[2] = a.z; r.v[3] = a.w;
+    r.v[4] = b.x; r.v[5] = b.y; r.v[6] = b.z; r.v[7] = b.w;
+    r.v[8] = c.x; r.v[9] = c.y; r.v[10] = c.z; r.v[11] = c.w;
+    return r;
+}
+__device__ __forceinline__ void store_fq(uint64_t *base, const Fq &a) {
+    uint4 *p = reinterpret_cast<uint4 *>(base);
+    p[0] = make_uint4(a.v[0], a.v[1], a.v[2], a.v[3]);
+    p[1] = make_uint4(a.v[4], a.v[5], a.v[6], a.v[7]);
+    p[2] = make_uint4(a.v[8], a.v[9], a.v[10], a.v[11]);
+}
+
+// host-side conversion helpers (u64 limbs <-> Fp)
+template <class P>
+inline Fp<P> from_u64_limbs(const uint64_t *l) {
+    Fp<P> r;
+    for (int i = 0; i < P::N / 2; i++) {
+        r.v[2 * i] = (uint32_t)l[i];
+        r.v[2 * i + 1] = (uint32_t)(l[i] >> 32);
+    }
+    return r;
+}
+template <class P>
+inline void to_u64_limbs(const Fp<P> &a, uint64_t *l) {
+    for (int i = 0; i < P::N / 2; i++) l[i] = (uint64_t)a.v[2 * i] | ((uint64_t)a.v[2 * i + 1] << 32);
+}
+
+}  // namespace pnp

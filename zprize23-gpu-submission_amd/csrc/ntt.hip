@@ -1,0 +1,368 @@
+// ntt.hip — radix-2 NTT over BLS12-381 Fr for gfx950.
+//
+// Semantics: natural order in and out, omega_N = ROOT32^(2^(32-lg)), inverse
+// scaled by N^-1, coset generator g = 7 (forward: x_i *= g^i first, inverse:
+// x_i *= g^-i last) — the reference's Ntt/Intt/Ntt_coset/Intt_coset
+// (utils/function.cu:249-273 -> zksnark_ntt.cu:74-92 -> ntt_kernel/ntt.cuh:57-144).
+//
+// Design (MI355X-first, not the reference's CT kernels):
+//   * Decimation-in-frequency passes of K levels each over LDS tiles of 1024
+//     elements (32 KiB, four workgroups per CU).  A tile holds G = 1024/2^K
+//     interleaved sub-transforms so every global row access is G consecutive
+//     32-byte elements (G*32 B contiguous).  LDS keeps the element split in two
+//     16-byte planes so each lane's ds_read_b128 / ds_write_b128 is
+//     conflict-free.
+//   * Twiddles w_N^e come from a per-size table (computed once per context,
+//     HBM-resident; its hot part lives in L2/MALL).
+//   * The DIF output is bit-reversed; one in-place tiled pass (32x32 tiles,
+//     tile pairs swapped through LDS) restores natural order and fuses the
+//     N^-1 and g^-i scalings of the inverse / coset-inverse transforms.
+#include "pnp_internal.h"
+
+namespace pnp {
+
+static constexpr int TILE = 1024;
+static constexpr int NTT_THREADS = 256;
+
+// ---------------------------------------------------------------- tables
+__global__ void k_powers_table(uint64_t *out, uint64_t count, Fr base, uint32_t chunk) {
+    uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    uint64_t start = t * chunk;
+    if (start >= count) return;
+    Fr p = pow_u64(base, start);
+    uint64_t end = start + chunk < count ? start + chunk : count;
+    for (uint64_t i = start; i < end; i++) {
+        store_fr(out, i, p);
+        p = p * base;
+    }
+}
+
+static Fr host_root(uint32_t lg) {
+    const uint64_t root32[4] = {13381757501831005802ULL, 6564924994866501612ULL,
+                                789602057691799140ULL, 6625830629041353339ULL};
+    Fr r = from_u64_limbs<FrP>(root32);
+    return pow_u64(r, 1ULL << (32 - lg));
+}
+static Fr host_gen() {
+    Fr seven = Fr::zero();
+    seven.v[0] = 7;
+    return to_mont(seven);
+}
+
+static void powers_table(DevBuf &buf, uint64_t count, const Fr &base, hipStream_t s) {
+    buf.alloc(count * 32);
+    const uint32_t chunk = 64;
+    uint64_t threads = (count + chunk - 1) / chunk;
+    uint32_t blocks = (uint32_t)((threads + 255) / 256);
+    hipLaunchKernelGGL(k_powers_table, dim3(blocks), dim3(256), 0, s, buf.u64(), count, base, chunk);
+    PNP_HIP(hipGetLastError());
+}
+
+const uint64_t *ntt_twiddles(NttTables &t, uint32_t lg, bool inverse, hipStream_t s) {
+    auto &m = inverse ? t.inv : t.fwd;
+    auto it = m.find(lg);
+    if (it != m.end()) return it->second.u64();
+    Fr w = host_root(lg);
+    if (inverse) w = pnp::inverse(w);
+    DevBuf buf;
+    uint64_t half = lg ? (1ULL << (lg - 1)) : 1;
+    powers_table(buf, half, w, s);
+    const uint64_t *p = buf.u64();
+    m.emplace(lg, std::move(buf));
+    return p;
+}
+
+void ntt_prepare_coset(NttTables &t, hipStream_t s) {
+    if (t.coset_ready) return;
+    Fr g = host_gen();
+    Fr gi = pnp::inverse(g);
+    powers_table(t.coset_lo, 4096, g, s);
+    powers_table(t.coset_hi, 1 << 14, pow_u64(g, 4096), s);
+    powers_table(t.coset_inv_lo, 4096, gi, s);
+    powers_table(t.coset_inv_hi, 1 << 14, pow_u64(gi, 4096), s);
+    t.coset_ready = true;
+}
+
+__device__ __forceinline__ Fr coset_pow(const uint64_t *hi, const uint64_t *lo, uint64_t i) {
+    return load_fr(hi, i >> 12) * load_fr(lo, i & 4095);
+}
+
+// ---------------------------------------------------------------- DIF pass
+// One pass = K DIF levels with half sizes H_lo*2^(K-1) ... H_lo over tiles of
+// TILE elements (G = TILE >> K interleaved sub-transforms per tile).
+template <int K>
+__global__ __launch_bounds__(NTT_THREADS) void k_dif_pass(uint64_t *data, const uint64_t *tw,
+                                                           uint32_t lg_n, uint32_t lg_hlo) {
+    constexpr int G = TILE >> K;
+    constexpr int ROWS = 1 << K;
+    __shared__ uint4 lds_lo[TILE];
+    __shared__ uint4 lds_hi[TILE];
+    const uint64_t hlo = 1ULL << lg_hlo;
+    const uint64_t gid0 = (uint64_t)blockIdx.x * G;
+    // load: element (m, g) of the tile -> lds[m*G + g]
+    for (int e = threadIdx.x; e < TILE; e += NTT_THREADS) {
+        int g = e % G, m = e / G;
+        uint64_t gid = gid0 + g;
+        uint64_t j = gid & (hlo - 1), b = gid >> lg_hlo;
+        uint64_t idx = (b << (lg_hlo + K)) + j + ((uint64_t)m << lg_hlo);
+        const uint4 *src = reinterpret_cast<const uint4 *>(data + 4 * idx);
+        lds_lo[e] = src[0];
+        lds_hi[e] = src[1];
+    }
+    __syncthreads();
+    for (int l = K - 1; l >= 0; l--) {
+        const uint32_t sh = lg_n - 1 - lg_hlo - l;
+        for (int bf = threadIdx.x; bf < TILE / 2; bf += NTT_THREADS) {
+            int g = bf % G, q = bf / G;
+            int mlow = q & ((1 << l) - 1);
+            int m = ((q >> l) << (l + 1)) | mlow;
+            int e0 = m * G + g, e1 = (m + (1 << l)) * G + g;
+            uint64_t gid = gid0 + g;
+            uint64_t j = gid & (hlo - 1);
+            uint64_t r = j + ((uint64_t)mlow << lg_hlo);
+            Fr w = load_fr(tw, r << sh);
+            uint4 a0 = lds_lo[e0], a1 = lds_hi[e0], b0 = lds_lo[e1], b1 = lds_hi[e1];
+            Fr a, b;
+            a.v[0] = a0.x; a.v[1] = a0.y; a.v[2] = a0.z; a.v[3] = a0.w;
+            a.v[4] = a1.x; a.v[5] = a1.y; a.v[6] = a1.z; a.v[7] = a1.w;
+            b.v[0] = b0.x; b.v[1] = b0.y; b.v[2] = b0.z; b.v[3] = b0.w;
+            b.v[4] = b1.x; b.v[5] = b1.y; b.v[6] = b1.z; b.v[7] = b1.w;
+            Fr s = a + b;
+            Fr d = (a - b) * w;
+            lds_lo[e0] = make_uint4(s.v[0], s.v[1], s.v[2], s.v[3]);
+            lds_hi[e0] = make_uint4(s.v[4], s.v[5], s.v[6], s.v[7]);
+            lds_lo[e1] = make_uint4(d.v[0], d.v[1], d.v[2], d.v[3]);
+            lds_hi[e1] = make_uint4(d.v[4], d.v[5], d.v[6], d.v[7]);
+        }
+        __syncthreads();
+    }
+    for (int e = threadIdx.x; e < TILE; e += NTT_THREADS) {
+        int g = e % G, m = e / G;
+        uint64_t gid = gid0 + g;
+        uint64_t j = gid & (hlo - 1), b = gid >> lg_hlo;
+        uint64_t idx = (b << (lg_hlo + K)) + j + ((uint64_t)m << lg_hlo);
+        uint4 *dst = reinterpret_cast<uint4 *>(data + 4 * idx);
+        dst[0] = lds_lo[e];
+        dst[1] = lds_hi[e];
+    }
+}
+
+// small transforms (N < TILE): one workgroup does everything in LDS
+__global__ __launch_bounds__(NTT_THREADS) void k_dif_small(uint64_t *data, const uint64_t *tw,
+                                                            uint32_t lg_n) {
+    __shared__ uint4 lds_lo[TILE];
+    __shared__ uint4 lds_hi[TILE];
+    const int n = 1 << lg_n;
+    for (int e = threadIdx.x; e < n; e += NTT_THREADS) {
+        const uint4 *src = reinterpret_cast<const uint4 *>(data + 4 * (uint64_t)e);
+        lds_lo[e] = src[0];
+        lds_hi[e] = src[1];
+    }
+    __syncthreads();
+    for (int l = (int)lg_n - 1; l >= 0; l--) {
+        for (int bf = threadIdx.x; bf < n / 2; bf += NTT_THREADS) {
+            int mlow = bf & ((1 << l) - 1);
+            int m = ((bf >> l) << (l + 1)) | mlow;
+            int e0 = m, e1 = m + (1 << l);
+            Fr w = load_fr(tw, (uint64_t)mlow << (lg_n - 1 - l));
+            uint4 a0 = lds_lo[e0], a1 = lds_hi[e0], b0 = lds_lo[e1], b1 = lds_hi[e1];
+            Fr a, b;
+            a.v[0] = a0.x; a.v[1] = a0.y; a.v[2] = a0.z; a.v[3] = a0.w;
+            a.v[4] = a1.x; a.v[5] = a1.y; a.v[6] = a1.z; a.v[7] = a1.w;
+            b.v[0] = b0.x; b.v[1] = b0.y; b.v[2] = b0.z; b.v[3] = b0.w;
+            b.v[4] = b1.x; b.v[5] = b1.y; b.v[6] = b1.z; b.v[7] = b1.w;
+            Fr s = a + b;
+            Fr d = (a - b) * w;
+            lds_lo[e0] = make_uint4(s.v[0], s.v[1], s.v[2], s.v[3]);
+            lds_hi[e0] = make_uint4(s.v[4], s.v[5], s.v[6], s.v[7]);
+            lds_lo[e1] = make_uint4(d.v[0], d.v[1], d.v[2], d.v[3]);
+            lds_hi[e1] = make_uint4(d.v[4], d.v[5], d.v[6], d.v[7]);
+        }
+        __syncthreads();
+    }
+    for (int e = threadIdx.x; e < n; e += NTT_THREADS) {
+        uint4 *dst = reinterpret_cast<uint4 *>(data + 4 * (uint64_t)e);
+        dst[0] = lds_lo[e];
+        dst[1] = lds_hi[e];
+    }
+}
+
+// ---------------------------------------------------------------- bit reversal
+__device__ __forceinline__ uint32_t brev(uint32_t x, uint32_t bits) {
+    return __brev(x) >> (32 - bits);
+}
+
+// mode 0: plain, 1: * c, 2: * c * g^-i (i = natural output index)
+struct Scale {
+    int mode;
+    Fr c;
+    const uint64_t *hi, *lo;
+};
+__device__ __forceinline__ Fr apply_scale(const Scale &s, Fr x, uint64_t i) {
+    if (s.mode == 0) return x;
+    Fr f = s.c;
+    if (s.mode == 2) f = f * coset_pow(s.hi, s.lo, i);
+    return x * f;
+}
+
+// lg >= 10: index = hi5 | mid | lo5; tile(mid) <-> tile(rev(mid)) transposed.
+__global__ __launch_bounds__(256) void k_bitrev_tiles(uint64_t *data, uint32_t lg, Scale sc) {
+    __shared__ uint4 t0l[32 * 33], t0h[32 * 33], t1l[32 * 33], t1h[32 * 33];
+    const uint32_t midbits = lg - 10;
+    const uint32_t mid = blockIdx.x;
+    const uint32_t rmid = midbits ? brev(mid, midbits) : 0;
+    if (rmid < mid) return;  // each pair handled once
+    const bool self = rmid == mid;
+    // load tile(mid): rows hi (0..31), cols lo (0..31) contiguous
+    for (int e = threadIdx.x; e < 1024; e += 256) {
+        uint32_t h = e >> 5, l = e & 31;
+        uint64_t i0 = ((uint64_t)h << (lg - 5)) | ((uint64_t)mid << 5) | l;
+        const uint4 *s0 = reinterpret_cast<const uint4 *>(data + 4 * i0);
+        t0l[h * 33 + l] = s0[0];
+        t0h[h * 33 + l] = s0[1];
+        if (!self) {
+            uint64_t i1 = ((uint64_t)h << (lg - 5)) | ((uint64_t)rmid << 5) | l;
+            const uint4 *s1 = reinterpret_cast<const uint4 *>(data + 4 * i1);
+            t1l[h * 33 + l] = s1[0];
+            t1h[h * 33 + l] = s1[1];
+        }
+    }
+    __syncthreads();
+    // element at (h, mid, l) goes to (rev5(l), rev(mid), rev5(h)).
+    // write tile position rmid: dest (h', rmid, l') gets source (rev5(l'), mid, rev5(h'))
+    for (int e = threadIdx.x; e < 1024; e += 256) {
+        uint32_t h2 = e >> 5, l2 = e & 31;
+        uint32_t sh = brev(l2, 5), sl = brev(h2, 5);
+        uint64_t d0 = ((uint64_t)h2 << (lg - 5)) | ((uint64_t)rmid << 5) | l2;
+        Fr x;
+        uint4 lo = t0l[sh * 33 + sl], hi = t0h[sh * 33 + sl];
+        x.v[0] = lo.x; x.v[1] = lo.y; x.v[2] = lo.z; x.v[3] = lo.w;
+        x.v[4] = hi.x; x.v[5] = hi.y; x.v[6] = hi.z; x.v[7] = hi.w;
+        store_fr(data, d0, apply_scale(sc, x, d0));
+        if (!self) {
+            uint64_t d1 = ((uint64_t)h2 << (lg - 5)) | ((uint64_t)mid << 5) | l2;
+            uint4 lo1 = t1l[sh * 33 + sl], hi1 = t1h[sh * 33 + sl];
+            Fr y;
+            y.v[0] = lo1.x; y.v[1] = lo1.y; y.v[2] = lo1.z; y.v[3] = lo1.w;
+            y.v[4] = hi1.x; y.v[5] = hi1.y; y.v[6] = hi1.z; y.v[7] = hi1.w;
+            store_fr(data, d1, apply_scale(sc, y, d1));
+        }
+    }
+}
+
+// lg < 10: single workgroup, via LDS
+__global__ __launch_bounds__(256) void k_bitrev_small(uint64_t *data, uint32_t lg, Scale sc) {
+    __shared__ uint4 tl[1024], th[1024];
+    const uint32_t n = 1u << lg;
+    for (uint32_t e = threadIdx.x; e < n; e += 256) {
+        const uint4 *s = reinterpret_cast<const uint4 *>(data + 4 * (uint64_t)e);
+        tl[e] = s[0];
+        th[e] = s[1];
+    }
+    __syncthreads();
+    for (uint32_t e = threadIdx.x; e < n; e += 256) {
+        uint32_t src = lg ? brev(e, lg) : 0;
+        Fr x;
+        uint4 lo = tl[src], hi = th[src];
+        x.v[0] = lo.x; x.v[1] = lo.y; x.v[2] = lo.z; x.v[3] = lo.w;
+        x.v[4] = hi.x; x.v[5] = hi.y; x.v[6] = hi.z; x.v[7] = hi.w;
+        store_fr(data, e, apply_scale(sc, x, e));
+    }
+}
+
+// forward coset: x_i *= g^i
+__global__ void k_coset_scale(uint64_t *data, uint64_t n, const uint64_t *hi, const uint64_t *lo) {
+    uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    store_fr(data, i, load_fr(data, i) * coset_pow(hi, lo, i));
+}
+
+// out[i] = i < n ? in[i] * g^i : 0   (pad_poly + LDE_distribute_powers)
+__global__ void k_pad_coset(const uint64_t *in, uint64_t *out, uint64_t n, uint64_t N,
+                            const uint64_t *hi, const uint64_t *lo) {
+    uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    if (i >= N) return;
+    Fr x = Fr::zero();
+    if (i < n) x = load_fr(in, i) * coset_pow(hi, lo, i);
+    store_fr(out, i, x);
+}
+
+static void dif(NttTables &t, uint64_t *d, uint32_t lg, bool inverse, hipStream_t s) {
+    const uint64_t *tw = ntt_twiddles(t, lg, inverse, s);
+    if (lg <= 10) {
+        hipLaunchKernelGGL(k_dif_small, dim3(1), dim3(NTT_THREADS), 0, s, d, tw, lg);
+        PNP_HIP(hipGetLastError());
+        return;
+    }
+    // split lg into passes of at most 10 levels (balanced), top levels first
+    int npass = (lg + 9) / 10;
+    int rem = lg;
+    uint32_t top = lg;  // current largest half-size exponent + 1
+    for (int p = 0; p < npass; p++) {
+        int k = (rem + (npass - p) - 1) / (npass - p);
+        rem -= k;
+        uint32_t lg_hlo = top - k;  // smallest half size of this pass = 2^(top-k)
+        uint64_t groups = (1ULL << lg) >> k;
+        uint32_t blocks = (uint32_t)(groups / (TILE >> k));
+        switch (k) {
+#define PNP_CASE(KK)                                                                          \
+    case KK:                                                                                  \
+        hipLaunchKernelGGL(k_dif_pass<KK>, dim3(blocks), dim3(NTT_THREADS), 0, s, d, tw, lg, \
+                           lg_hlo);                                                           \
+        break;
+            PNP_CASE(1) PNP_CASE(2) PNP_CASE(3) PNP_CASE(4) PNP_CASE(5)
+            PNP_CASE(6) PNP_CASE(7) PNP_CASE(8) PNP_CASE(9) PNP_CASE(10)
+#undef PNP_CASE
+            default:
+                set_error("bad NTT pass size %d", k);
+                throw Error(PNP_E_ARG);
+        }
+        PNP_HIP(hipGetLastError());
+        top -= k;
+    }
+}
+
+static void bitrev(uint64_t *d, uint32_t lg, const Scale &sc, hipStream_t s) {
+    if (lg < 10) {
+        hipLaunchKernelGGL(k_bitrev_small, dim3(1), dim3(256), 0, s, d, lg, sc);
+    } else {
+        hipLaunchKernelGGL(k_bitrev_tiles, dim3(1u << (lg - 10)), dim3(256), 0, s, d, lg, sc);
+    }
+    PNP_HIP(hipGetLastError());
+}
+
+void ntt_run(NttTables &t, uint64_t *d, uint32_t lg, bool inverse, bool coset, hipStream_t s) {
+    if (lg == 0) return;
+    uint64_t n = 1ULL << lg;
+    if (coset) ntt_prepare_coset(t, s);
+    if (!inverse && coset) {
+        hipLaunchKernelGGL(k_coset_scale, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, s, d, n,
+                           t.coset_hi.u64(), t.coset_lo.u64());
+        PNP_HIP(hipGetLastError());
+    }
+    dif(t, d, lg, inverse, s);
+    Scale sc{0, Fr::one(), nullptr, nullptr};
+    if (inverse) {
+        Fr nf = Fr::zero();
+        nf.v[0] = (uint32_t)n;
+        nf.v[1] = (uint32_t)(n >> 32);
+        sc.mode = coset ? 2 : 1;
+        sc.c = pnp::inverse(to_mont(nf));
+        sc.hi = t.coset_inv_hi.u64();
+        sc.lo = t.coset_inv_lo.u64();
+    }
+    bitrev(d, lg, sc, s);
+}
+
+void coset_lde8(NttTables &t, const uint64_t *in, uint64_t *out8, uint32_t lg_n, hipStream_t s) {
+    ntt_prepare_coset(t, s);
+    uint64_t n = 1ULL << lg_n, N = n << 3;
+    hipLaunchKernelGGL(k_pad_coset, dim3((uint32_t)((N + 255) / 256)), dim3(256), 0, s, in, out8, n,
+                       N, t.coset_hi.u64(), t.coset_lo.u64());
+    PNP_HIP(hipGetLastError());
+    dif(t, out8, lg_n + 3, false, s);
+    Scale sc{0, Fr::one(), nullptr, nullptr};
+    bitrev(out8, lg_n + 3, sc, s);
+}
+
+}  // namespace pnp

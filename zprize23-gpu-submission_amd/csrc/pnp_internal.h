@@ -1,0 +1,91 @@
+// pnp_internal.h — host-side declarations shared by the HIP translation units.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <map>
+#include <string>
+#include <vector>
+#include "field.cuh"
+#include "../../include/pnp_plonk.h"
+
+namespace pnp {
+
+void set_error(const char *fmt, ...);
+
+#define PNP_HIP(expr)                                                              \
+    do {                                                                           \
+        hipError_t e_ = (expr);                                                    \
+        if (e_ != hipSuccess) {                                                    \
+            ::pnp::set_error("%s:%d %s: %s", __FILE__, __LINE__, #expr,            \
+                             hipGetErrorString(e_));                               \
+            throw ::pnp::Error(PNP_E_DEVICE);                                      \
+        }                                                                          \
+    } while (0)
+
+struct Error {
+    int code;
+    explicit Error(int c) : code(c) {}
+};
+
+// device buffer with RAII
+struct DevBuf {
+    void *p = nullptr;
+    size_t bytes = 0;
+    DevBuf() = default;
+    explicit DevBuf(size_t b) { alloc(b); }
+    DevBuf(const DevBuf &) = delete;
+    DevBuf &operator=(const DevBuf &) = delete;
+    DevBuf(DevBuf &&o) noexcept : p(o.p), bytes(o.bytes) { o.p = nullptr; o.bytes = 0; }
+    DevBuf &operator=(DevBuf &&o) noexcept {
+        if (this != &o) { release(); p = o.p; bytes = o.bytes; o.p = nullptr; o.bytes = 0; }
+        return *this;
+    }
+    ~DevBuf() { release(); }
+    void alloc(size_t b);
+    void release();
+    uint64_t *u64() const { return static_cast<uint64_t *>(p); }
+};
+
+// ---- NTT (ntt.hip) ----
+struct NttTables {
+    // tw[e] = w_N^e, e < N/2, for forward and inverse roots, per lg
+    std::map<uint32_t, DevBuf> fwd, inv;
+    DevBuf coset_hi, coset_lo;        // g^(4096 k), g^k
+    DevBuf coset_inv_hi, coset_inv_lo;  // g^-(4096 k), g^-k
+    bool coset_ready = false;
+};
+const uint64_t *ntt_twiddles(NttTables &t, uint32_t lg, bool inverse, hipStream_t s);
+void ntt_prepare_coset(NttTables &t, hipStream_t s);
+// in place natural-order NTT of 2^lg elements
+void ntt_run(NttTables &t, uint64_t *d, uint32_t lg, bool inverse, bool coset, hipStream_t s);
+// out8[i] = i < n ? in[i] * g^i : 0, then forward NTT of size 8n (Ntt_coset::forward)
+void coset_lde8(NttTables &t, const uint64_t *in, uint64_t *out8, uint32_t lg_n, hipStream_t s);
+
+// ---- MSM (msm.hip) ----
+struct MsmWork {
+    DevBuf digits, sorted, counts, offsets, buckets, seg, scal, result;
+    size_t cap_n = 0;
+};
+// sum_i s_i P_i; scalars Montgomery Fr; result written to host as XYZZ Fq (4x6 u64)
+void msm_run(MsmWork &w, const uint64_t *d_points, const uint64_t *d_scalars_mont, uint64_t n,
+             uint64_t *h_xyzz, hipStream_t s);
+// host: XYZZ -> affine Montgomery (inf -> (0, one))
+void xyzz_to_affine_host(const uint64_t *xyzz, uint64_t *aff12);
+
+// ---- poly / elementwise (poly.hip) ----
+void k_from_mont(uint64_t *d, uint64_t n, hipStream_t s);
+void k_to_mont(uint64_t *d, uint64_t n, hipStream_t s);
+void k_prefix_product(uint64_t *d, uint64_t n, DevBuf &scratch, hipStream_t s);
+void k_batch_inverse(uint64_t *d, uint64_t n, DevBuf &scratch, hipStream_t s);
+void k_poly_eval(const uint64_t *d, uint64_t n, const Fr &x, DevBuf &scratch, Fr *out,
+                 hipStream_t s);
+// several polys (same n) at the same point in one launch
+void k_poly_eval_multi(const uint64_t *const *polys, int npolys, uint64_t n, const Fr &x,
+                       DevBuf &scratch, Fr *out, hipStream_t s);
+void k_poly_div_linear(uint64_t *d, uint64_t n, const Fr &z, DevBuf &scratch, hipStream_t s);
+void k_random_fr(uint64_t *d, uint64_t n, uint64_t seed, hipStream_t s);
+void k_srs(uint64_t *d, uint64_t n, const Fr &tau, hipStream_t s);
+void k_coset_consts(uint64_t *vh, uint64_t *x, uint32_t lg_n, hipStream_t s);
+
+}  // namespace pnp

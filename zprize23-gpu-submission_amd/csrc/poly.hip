@@ -1,0 +1,354 @@
+// poly.hip — generic Fr vector kernels used along the gen_proof path.
+//
+// Reference operators restated (utils/mont/cuda/mont_arithmetic.cu):
+//   accumulate_mul_poly :334-360  exclusive prefix product (z, z2 grand products)
+//   poly_div_cuda       :305-331  quotient by (X - z), remainder dropped
+//   evaluate            :105-173  sum c_i x^i (function.cu:162-173)
+//   inv_mod             :73       per-element inverse (inv(0) = 0)
+// The reference runs log2(N) Hillis-Steele passes over the whole array (22 at
+// N = 2^22) and a per-thread square-and-multiply for x^i.  Here every scan is
+// a chunked recursion: each lane folds a chunk of K consecutive elements,
+// the chunk totals recurse (N -> N/K -> ...), then each lane re-walks its
+// chunk with its carry.  Work is ~2-3 multiplications per element and a
+// handful of launches, with every global access coalesced per chunk row.
+#include "pnp_internal.h"
+
+namespace pnp {
+
+static constexpr int CHUNK = 32;
+
+static inline uint32_t nblk(uint64_t threads, uint32_t bs = 256) {
+    return (uint32_t)((threads + bs - 1) / bs);
+}
+
+// ---------------------------------------------------------------- conversions
+__global__ void k_from_mont_(uint64_t *d, uint64_t n) {
+    uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    if (i < n) store_fr(d, i, from_mont(load_fr(d, i)));
+}
+__global__ void k_to_mont_(uint64_t *d, uint64_t n) {
+    uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    if (i < n) store_fr(d, i, to_mont(load_fr(d, i)));
+}
+void k_from_mont(uint64_t *d, uint64_t n, hipStream_t s) {
+    if (!n) return;
+    hipLaunchKernelGGL(k_from_mont_, dim3(nblk(n)), dim3(256), 0, s, d, n);
+    PNP_HIP(hipGetLastError());
+}
+void k_to_mont(uint64_t *d, uint64_t n, hipStream_t s) {
+    if (!n) return;
+    hipLaunchKernelGGL(k_to_mont_, dim3(nblk(n)), dim3(256), 0, s, d, n);
+    PNP_HIP(hipGetLastError());
+}
+
+// ---------------------------------------------------------------- prefix product
+// chunk c = [cK, cK+K): tot[c] = prod of the chunk
+__global__ void k_chunk_prod(const uint64_t *d, uint64_t n, uint64_t *tot) {
+    uint64_t c = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    uint64_t lo = c * CHUNK;
+    if (lo >= n) return;
+    uint64_t hi = lo + CHUNK < n ? lo + CHUNK : n;
+    Fr acc = load_fr(d, lo);
+    for (uint64_t i = lo + 1; i < hi; i++) acc = acc * load_fr(d, i);
+    store_fr(tot, c, acc);
+}
+// d[i] <- carry * prod_{chunk start <= j < i} d[j]; carry = exclusive prefix of chunk totals
+__global__ void k_chunk_prod_apply(uint64_t *d, uint64_t n, const uint64_t *pre) {
+    uint64_t c = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    uint64_t lo = c * CHUNK;
+    if (lo >= n) return;
+    uint64_t hi = lo + CHUNK < n ? lo + CHUNK : n;
+    Fr acc = load_fr(pre, c);
+    for (uint64_t i = lo; i < hi; i++) {
+        Fr x = load_fr(d, i);
+        store_fr(d, i, acc);
+        acc = acc * x;
+    }
+}
+__global__ void k_seq_prefix_prod(uint64_t *d, uint64_t n) {
+    Fr acc = Fr::one();
+    for (uint64_t i = 0; i < n; i++) {
+        Fr x = load_fr(d, i);
+        store_fr(d, i, acc);
+        acc = acc * x;
+    }
+}
+static void prefix_product_rec(uint64_t *d, uint64_t n, uint64_t *scratch, hipStream_t s) {
+    if (n <= CHUNK) {
+        hipLaunchKernelGGL(k_seq_prefix_prod, dim3(1), dim3(1), 0, s, d, n);
+        PNP_HIP(hipGetLastError());
+        return;
+    }
+    uint64_t nc = (n + CHUNK - 1) / CHUNK;
+    uint64_t *tot = scratch;
+    hipLaunchKernelGGL(k_chunk_prod, dim3(nblk(nc)), dim3(256), 0, s, d, n, tot);
+    PNP_HIP(hipGetLastError());
+    prefix_product_rec(tot, nc, scratch + 4 * nc, s);
+    hipLaunchKernelGGL(k_chunk_prod_apply, dim3(nblk(nc)), dim3(256), 0, s, d, n, tot);
+    PNP_HIP(hipGetLastError());
+}
+static uint64_t rec_scratch_elems(uint64_t n) {
+    uint64_t t = 0;
+    while (n > CHUNK) { n = (n + CHUNK - 1) / CHUNK; t += n; }
+    return t + 1;
+}
+void k_prefix_product(uint64_t *d, uint64_t n, DevBuf &scratch, hipStream_t s) {
+    if (!n) return;
+    size_t need = rec_scratch_elems(n) * 32;
+    if (scratch.bytes < need) scratch.alloc(need);
+    prefix_product_rec(d, n, scratch.u64(), s);
+}
+
+// ---------------------------------------------------------------- batch inverse
+__global__ void k_binv_up(const uint64_t *d, uint64_t n, uint64_t *pre, uint64_t *tot) {
+    uint64_t c = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    uint64_t lo = c * CHUNK;
+    if (lo >= n) return;
+    uint64_t hi = lo + CHUNK < n ? lo + CHUNK : n;
+    Fr acc = Fr::one();
+    for (uint64_t i = lo; i < hi; i++) {
+        store_fr(pre, i, acc);
+        Fr x = load_fr(d, i);
+        if (!x.is_zero()) acc = acc * x;
+    }
+    store_fr(tot, c, acc);
+}
+__global__ void k_binv_down(uint64_t *d, uint64_t n, const uint64_t *pre, const uint64_t *tinv) {
+    uint64_t c = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    uint64_t lo = c * CHUNK;
+    if (lo >= n) return;
+    uint64_t hi = lo + CHUNK < n ? lo + CHUNK : n;
+    Fr acc = load_fr(tinv, c);
+    for (uint64_t i = hi; i-- > lo;) {
+        Fr x = load_fr(d, i);
+        if (x.is_zero()) continue;
+        store_fr(d, i, acc * load_fr(pre, i));
+        acc = acc * x;
+    }
+}
+__global__ void k_fermat_inv(uint64_t *d, uint64_t n) {
+    uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    if (i < n) store_fr(d, i, inverse(load_fr(d, i)));
+}
+static void binv_rec(uint64_t *d, uint64_t n, uint64_t *scratch, hipStream_t s) {
+    if (n <= 4096) {
+        hipLaunchKernelGGL(k_fermat_inv, dim3(nblk(n, 64)), dim3(64), 0, s, d, n);
+        PNP_HIP(hipGetLastError());
+        return;
+    }
+    uint64_t nc = (n + CHUNK - 1) / CHUNK;
+    uint64_t *pre = scratch, *tot = scratch + 4 * n;
+    hipLaunchKernelGGL(k_binv_up, dim3(nblk(nc)), dim3(256), 0, s, d, n, pre, tot);
+    PNP_HIP(hipGetLastError());
+    binv_rec(tot, nc, tot + 4 * nc, s);
+    hipLaunchKernelGGL(k_binv_down, dim3(nblk(nc)), dim3(256), 0, s, d, n, pre, tot);
+    PNP_HIP(hipGetLastError());
+}
+void k_batch_inverse(uint64_t *d, uint64_t n, DevBuf &scratch, hipStream_t s) {
+    if (!n) return;
+    uint64_t need = 0, m = n;
+    while (m > 4096) { uint64_t nc = (m + CHUNK - 1) / CHUNK; need += m + nc; m = nc; }
+    need = (need + 1) * 32;
+    if (scratch.bytes < need) scratch.alloc(need);
+    binv_rec(d, n, scratch.u64(), s);
+}
+
+// ---------------------------------------------------------------- suffix Horner
+// H[k] = sum_{j >= k} v_j z^(j-k).  Chunk value L_c = H restricted to the chunk.
+__global__ void k_horner_chunk(const uint64_t *v, uint64_t n, Fr z, uint64_t *L) {
+    uint64_t c = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    uint64_t lo = c * CHUNK;
+    if (lo >= n) return;
+    uint64_t hi = lo + CHUNK < n ? lo + CHUNK : n;
+    Fr acc = Fr::zero();
+    for (uint64_t i = hi; i-- > lo;) acc = acc * z + load_fr(v, i);
+    store_fr(L, c, acc);
+}
+// H at chunk starts is in Hc (inclusive); write H[k] for every k of the chunk
+// (mode 0) or the shifted quotient q[k] = H[k+1] (mode 1: poly division)
+__global__ void k_horner_apply(uint64_t *v, uint64_t n, Fr z, const uint64_t *Hc, uint64_t nc,
+                               int shift) {
+    uint64_t c = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    uint64_t lo = c * CHUNK;
+    if (lo >= n) return;
+    uint64_t hi = lo + CHUNK < n ? lo + CHUNK : n;
+    Fr acc = c + 1 < nc ? load_fr(Hc, c + 1) : Fr::zero();  // H[hi]
+    for (uint64_t i = hi; i-- > lo;) {
+        Fr x = load_fr(v, i);
+        if (shift) store_fr(v, i, acc);
+        acc = acc * z + x;
+        if (!shift) store_fr(v, i, acc);
+    }
+}
+__global__ void k_seq_horner(uint64_t *v, uint64_t n, Fr z, int shift) {
+    Fr acc = Fr::zero();
+    for (uint64_t i = n; i-- > 0;) {
+        Fr x = load_fr(v, i);
+        if (shift) store_fr(v, i, acc);
+        acc = acc * z + x;
+        if (!shift) store_fr(v, i, acc);
+    }
+}
+static void horner_rec(uint64_t *v, uint64_t n, const Fr &z, int shift, uint64_t *scratch,
+                       hipStream_t s) {
+    if (n <= CHUNK) {
+        hipLaunchKernelGGL(k_seq_horner, dim3(1), dim3(1), 0, s, v, n, z, shift);
+        PNP_HIP(hipGetLastError());
+        return;
+    }
+    uint64_t nc = (n + CHUNK - 1) / CHUNK;
+    uint64_t *L = scratch;
+    hipLaunchKernelGGL(k_horner_chunk, dim3(nblk(nc)), dim3(256), 0, s, v, n, z, L);
+    PNP_HIP(hipGetLastError());
+    Fr zK = pow_u64(z, CHUNK);
+    horner_rec(L, nc, zK, 0, scratch + 4 * nc, s);  // L <- inclusive H at chunk starts
+    hipLaunchKernelGGL(k_horner_apply, dim3(nblk(nc)), dim3(256), 0, s, v, n, z, L, nc, shift);
+    PNP_HIP(hipGetLastError());
+}
+void k_poly_div_linear(uint64_t *d, uint64_t n, const Fr &z, DevBuf &scratch, hipStream_t s) {
+    if (!n) return;
+    size_t need = rec_scratch_elems(n) * 32;
+    if (scratch.bytes < need) scratch.alloc(need);
+    horner_rec(d, n, z, 1, scratch.u64(), s);
+}
+
+// ---------------------------------------------------------------- evaluation
+// partial[b] = sum over block b's chunks of sum_i c_i x^i, for each of np polys
+template <int NP>
+__global__ __launch_bounds__(256) void k_eval_partial(const uint64_t *const *polys, uint64_t n,
+                                                      Fr x, uint64_t *partial) {
+    __shared__ uint4 red_lo[256], red_hi[256];
+    uint64_t c = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    uint64_t lo = c * CHUNK;
+    Fr h[NP];
+#pragma unroll
+    for (int p = 0; p < NP; p++) h[p] = Fr::zero();
+    if (lo < n) {
+        uint64_t hi = lo + CHUNK < n ? lo + CHUNK : n;
+        for (uint64_t i = hi; i-- > lo;) {
+#pragma unroll
+            for (int p = 0; p < NP; p++) h[p] = h[p] * x + load_fr(polys[p], i);
+        }
+        Fr xs = pow_u64(x, lo);
+#pragma unroll
+        for (int p = 0; p < NP; p++) h[p] = h[p] * xs;
+    }
+#pragma unroll
+    for (int p = 0; p < NP; p++) {
+        red_lo[threadIdx.x] = make_uint4(h[p].v[0], h[p].v[1], h[p].v[2], h[p].v[3]);
+        red_hi[threadIdx.x] = make_uint4(h[p].v[4], h[p].v[5], h[p].v[6], h[p].v[7]);
+        __syncthreads();
+        for (int st = 128; st > 0; st >>= 1) {
+            if ((int)threadIdx.x < st) {
+                uint4 a0 = red_lo[threadIdx.x], a1 = red_hi[threadIdx.x];
+                uint4 b0 = red_lo[threadIdx.x + st], b1 = red_hi[threadIdx.x + st];
+                Fr a, b;
+                a.v[0] = a0.x; a.v[1] = a0.y; a.v[2] = a0.z; a.v[3] = a0.w;
+                a.v[4] = a1.x; a.v[5] = a1.y; a.v[6] = a1.z; a.v[7] = a1.w;
+                b.v[0] = b0.x; b.v[1] = b0.y; b.v[2] = b0.z; b.v[3] = b0.w;
+                b.v[4] = b1.x; b.v[5] = b1.y; b.v[6] = b1.z; b.v[7] = b1.w;
+                Fr r = a + b;
+                red_lo[threadIdx.x] = make_uint4(r.v[0], r.v[1], r.v[2], r.v[3]);
+                red_hi[threadIdx.x] = make_uint4(r.v[4], r.v[5], r.v[6], r.v[7]);
+            }
+            __syncthreads();
+        }
+        if (threadIdx.x == 0) {
+            uint4 *dst = reinterpret_cast<uint4 *>(partial + 4 * ((uint64_t)p * gridDim.x + blockIdx.x));
+            dst[0] = red_lo[0];
+            dst[1] = red_hi[0];
+        }
+        __syncthreads();
+    }
+}
+// sum partials per poly (single block per poly)
+__global__ __launch_bounds__(256) void k_sum_partials(const uint64_t *partial, uint64_t nb,
+                                                      uint64_t *out) {
+    __shared__ uint4 red_lo[256], red_hi[256];
+    const uint64_t *pp = partial + 4 * (uint64_t)blockIdx.x * nb;
+    Fr acc = Fr::zero();
+    for (uint64_t i = threadIdx.x; i < nb; i += 256) acc = acc + load_fr(pp, i);
+    red_lo[threadIdx.x] = make_uint4(acc.v[0], acc.v[1], acc.v[2], acc.v[3]);
+    red_hi[threadIdx.x] = make_uint4(acc.v[4], acc.v[5], acc.v[6], acc.v[7]);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        Fr tot = Fr::zero();
+        for (int k = 0; k < 256; k++) {
+            Fr a;
+            uint4 a0 = red_lo[k], a1 = red_hi[k];
+            a.v[0] = a0.x; a.v[1] = a0.y; a.v[2] = a0.z; a.v[3] = a0.w;
+            a.v[4] = a1.x; a.v[5] = a1.y; a.v[6] = a1.z; a.v[7] = a1.w;
+            tot = tot + a;
+        }
+        store_fr(out, blockIdx.x, tot);
+    }
+}
+
+void k_poly_eval_multi(const uint64_t *const *polys, int npolys, uint64_t n, const Fr &x,
+                       DevBuf &scratch, Fr *out, hipStream_t s) {
+    if (npolys <= 0) return;
+    uint64_t nc = (n + CHUNK - 1) / CHUNK;
+    uint32_t nb = nblk(nc);
+    // layout: [8 poly pointers][partials np*nb][results np]
+    size_t need = 64 * 8 + (size_t)npolys * nb * 32 + (size_t)npolys * 32 + 64;
+    if (scratch.bytes < need) scratch.alloc(need);
+    uint64_t *base = scratch.u64();
+    const uint64_t **dptrs = reinterpret_cast<const uint64_t **>(base);
+    uint64_t *partial = base + 64;
+    uint64_t *res = partial + (size_t)npolys * nb * 4;
+    std::vector<Fr> host((size_t)npolys);
+    for (int p0 = 0; p0 < npolys; p0 += 8) {
+        int np = npolys - p0 < 8 ? npolys - p0 : 8;
+        PNP_HIP(hipMemcpyAsync(dptrs, polys + p0, sizeof(void *) * np, hipMemcpyHostToDevice, s));
+        uint64_t *pt = partial;
+        switch (np) {
+#define PNP_EV(K)                                                                                 \
+    case K:                                                                                       \
+        hipLaunchKernelGGL(k_eval_partial<K>, dim3(nb), dim3(256), 0, s, dptrs, n, x, pt);      \
+        break;
+            PNP_EV(1) PNP_EV(2) PNP_EV(3) PNP_EV(4) PNP_EV(5) PNP_EV(6) PNP_EV(7) PNP_EV(8)
+#undef PNP_EV
+        }
+        PNP_HIP(hipGetLastError());
+        hipLaunchKernelGGL(k_sum_partials, dim3(np), dim3(256), 0, s, pt, (uint64_t)nb, res);
+        PNP_HIP(hipGetLastError());
+        PNP_HIP(hipMemcpyAsync(host.data() + p0, res, 32 * np, hipMemcpyDeviceToHost, s));
+        PNP_HIP(hipStreamSynchronize(s));  // dptrs / partial reused by the next group
+    }
+    for (int p = 0; p < npolys; p++) out[p] = host[p];
+}
+
+void k_poly_eval(const uint64_t *d, uint64_t n, const Fr &x, DevBuf &scratch, Fr *out,
+                 hipStream_t s) {
+    const uint64_t *p[1] = {d};
+    k_poly_eval_multi(p, 1, n, x, scratch, out, s);
+}
+
+// ---------------------------------------------------------------- synthetic inputs
+__device__ __forceinline__ uint64_t splitmix(uint64_t x) {
+    x += 0x9e3779b97f4a7c15ULL;
+    x = (x ^ (x >> 30)) * 0xbf58476d1ce4e5b9ULL;
+    x = (x ^ (x >> 27)) * 0x94d049bb133111ebULL;
+    return x ^ (x >> 31);
+}
+__global__ void k_random_fr_(uint64_t *d, uint64_t n, uint64_t seed) {
+    uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    Fr r;
+    uint64_t h = seed * 0x2545F4914F6CDD1DULL + i * 4;
+    for (int k = 0; k < 4; k++) {
+        uint64_t w = splitmix(h + k);
+        r.v[2 * k] = (uint32_t)w;
+        r.v[2 * k + 1] = (uint32_t)(w >> 32);
+    }
+    r.v[7] &= 0x7fffffffu;  // < 2^255 < 2r
+    reduce_once(r);
+    store_fr(d, i, r);  // uniform-ish canonical value used directly as a Montgomery residue
+}
+void k_random_fr(uint64_t *d, uint64_t n, uint64_t seed, hipStream_t s) {
+    if (!n) return;
+    hipLaunchKernelGGL(k_random_fr_, dim3(nblk(n)), dim3(256), 0, s, d, n, seed);
+    PNP_HIP(hipGetLastError());
+}
+
+}  // namespace pnp

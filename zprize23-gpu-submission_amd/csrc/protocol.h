@@ -1,0 +1,53 @@
+// protocol.h — argument blocks and launchers of the fused gen_proof passes
+// (protocol.hip).  Argument structs are passed by value as kernel arguments.
+#pragma once
+#include "pnp_internal.h"
+
+namespace pnp {
+
+__host__ __device__ inline Fr from_u64_limbs_dev(const uint64_t *l) {
+    Fr r;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        r.v[2 * i] = (uint32_t)l[i];
+        r.v[2 * i + 1] = (uint32_t)(l[i] >> 32);
+    }
+    return r;
+}
+
+struct PermArgs {
+    const uint64_t *w[4];
+    const uint64_t *sigma[4];  // sigma evaluations on the n-domain
+    Fr bk[4];                  // beta * k_j, k = 1, 7, 13, 17
+    Fr beta, gamma, omega;
+};
+
+struct QuotArgs {
+    const uint64_t *w8[4], *z8, *pi8, *f8, *t8, *h18, *h28, *z28, *l1a8, *l18;
+    const uint64_t *q_m, *q_l, *q_r, *q_o, *q_4, *q_c, *q_hl, *q_hr, *q_h4, *q_arith, *q_lookup;
+    const uint64_t *sig[4], *lin, *vh_inv;
+    Fr alpha, beta, gamma, delta, eps, zeta, lsep;
+    Fr bk[4], opd, eopd, sep2, sep3;
+};
+
+constexpr int LIN_MAX = 24;
+struct LinArgs {
+    int k;
+    const uint64_t *p[LIN_MAX];
+    Fr s[LIN_MAX];
+};
+
+void k_compress4(uint64_t *out, const uint64_t *t0, const uint64_t *t1, const uint64_t *t2,
+                 const uint64_t *t3, const Fr &z, uint64_t n, hipStream_t s);
+void k_query_f(uint64_t *out, const uint64_t *ql, uint64_t n_gates, const uint64_t *const w[4],
+               const uint64_t *tc, const Fr &z, uint64_t n, hipStream_t s);
+void k_perm_numden(uint64_t *num, uint64_t *den, const PermArgs &a, uint64_t n, hipStream_t s);
+void k_lookup_nd(uint64_t *num, uint64_t *den, const uint64_t *f, const uint64_t *t,
+                 const uint64_t *h1, const uint64_t *h2, const Fr &delta, const Fr &eps, uint64_t n,
+                 hipStream_t s);
+void k_mul_inplace(uint64_t *a, const uint64_t *b, uint64_t n, hipStream_t s);
+bool k_any_nonzero(const uint64_t *v, uint64_t words, DevBuf &scratch, hipStream_t s);
+void k_quotient(const QuotArgs &q, uint64_t N8, uint64_t *out, hipStream_t s);
+void k_lincomb(const LinArgs &a, uint64_t n, uint64_t *out, hipStream_t s);
+
+}  // namespace pnp

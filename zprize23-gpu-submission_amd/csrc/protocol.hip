@@ -1,0 +1,225 @@
+// protocol.hip — fused element-wise passes of gen_proof for gfx950.
+//
+// Each kernel below replaces a chain of the reference's one-op-per-launch
+// SyncedMemory operators (mont_arithmetic.cuh:17-110) with ONE pass that reads
+// every input once and writes its result once:
+//   k_compress4    compress(t1..t4; zeta)         zksnark_compute_query_table.cu:110-129
+//   k_query_f      compute_query_table + compress  zk_function.cu:29-36, :5-44
+//   k_perm_numden  numerator/denominator products  permutation/mod.cu:3-16, :44-101
+//   k_lookup_nd    _lookup_ratio                   permutation/mod.cu:18-42, :111-135
+//   k_mul_inplace  num * den^-1                    permutation/mod.cu:99-100
+//   k_quotient     gate + permutation + lookup     proof_system/quotient.cu:142-376,
+//                  numerators times v_h^-1         widget/arithmetic.cu:7-45,
+//                                                  proof_system/permutation.cu:6-125,
+//                                                  widget/lookup.cu:3-134
+//   k_lincomb      sum_k s_k P_k (linearisation    linearisation.cu:73-306,
+//                  polynomial, KZG opening combine) KZG/kzg10.cu:116-145
+#include "pnp_internal.h"
+#include "protocol.h"
+
+namespace pnp {
+
+static inline uint32_t nblk(uint64_t threads, uint32_t bs = 256) {
+    return (uint32_t)((threads + bs - 1) / bs);
+}
+
+__global__ void k_compress4_(uint64_t *out, const uint64_t *t0, const uint64_t *t1,
+                             const uint64_t *t2, const uint64_t *t3, Fr z, uint64_t n) {
+    uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    Fr acc = load_fr(t3, i);
+    acc = acc * z + load_fr(t2, i);
+    acc = acc * z + load_fr(t1, i);
+    acc = acc * z + load_fr(t0, i);
+    store_fr(out, i, acc);
+}
+void k_compress4(uint64_t *out, const uint64_t *t0, const uint64_t *t1, const uint64_t *t2,
+                 const uint64_t *t3, const Fr &z, uint64_t n, hipStream_t s) {
+    hipLaunchKernelGGL(k_compress4_, dim3(nblk(n)), dim3(256), 0, s, out, t0, t1, t2, t3, z, n);
+    PNP_HIP(hipGetLastError());
+}
+
+// f_i = q_lookup_i == 0 ? t_c[0] : a + z b + z^2 c + z^3 d   (q_lookup zero-padded past n_gates)
+__global__ void k_query_f_(uint64_t *out, const uint64_t *ql, uint64_t n_gates, const uint64_t *wl,
+                           const uint64_t *wr, const uint64_t *wo, const uint64_t *w4,
+                           const uint64_t *tc, Fr z, uint64_t n) {
+    uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    bool zero = true;
+    if (i < n_gates) zero = load_fr(ql, i).is_zero();
+    Fr r;
+    if (zero) {
+        r = load_fr(tc, 0);
+    } else {
+        r = load_fr(w4, i);
+        r = r * z + load_fr(wo, i);
+        r = r * z + load_fr(wr, i);
+        r = r * z + load_fr(wl, i);
+    }
+    store_fr(out, i, r);
+}
+void k_query_f(uint64_t *out, const uint64_t *ql, uint64_t n_gates, const uint64_t *const w[4],
+               const uint64_t *tc, const Fr &z, uint64_t n, hipStream_t s) {
+    hipLaunchKernelGGL(k_query_f_, dim3(nblk(n)), dim3(256), 0, s, out, ql, n_gates, w[0], w[1], w[2],
+                       w[3], tc, z, n);
+    PNP_HIP(hipGetLastError());
+}
+
+// num_i = prod_j (w_j + beta k_j w^i + gamma), den_i = prod_j (w_j + beta sigma_j + gamma)
+static constexpr int PCHUNK = 16;
+__global__ void k_perm_numden_(uint64_t *num, uint64_t *den, PermArgs a, uint64_t n) {
+    uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    uint64_t lo = t * PCHUNK;
+    if (lo >= n) return;
+    uint64_t hi = lo + PCHUNK < n ? lo + PCHUNK : n;
+    Fr root = pow_u64(a.omega, lo);
+    for (uint64_t i = lo; i < hi; i++) {
+        Fr nm = Fr::one(), dn = Fr::one();
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            Fr w = load_fr(a.w[j], i);
+            nm = nm * (w + a.bk[j] * root + a.gamma);
+            dn = dn * (w + load_fr(a.sigma[j], i) * a.beta + a.gamma);
+        }
+        store_fr(num, i, nm);
+        store_fr(den, i, dn);
+        root = root * a.omega;
+    }
+}
+void k_perm_numden(uint64_t *num, uint64_t *den, const PermArgs &a, uint64_t n, hipStream_t s) {
+    hipLaunchKernelGGL(k_perm_numden_, dim3(nblk((n + PCHUNK - 1) / PCHUNK)), dim3(256), 0, s, num, den,
+                       a, n);
+    PNP_HIP(hipGetLastError());
+}
+
+// _lookup_ratio with the reference's 8-byte shifted t_next / h1_next words
+__device__ __forceinline__ Fr load_shift8(const uint64_t *v, uint64_t i, uint64_t n) {
+    uint64_t w[4];
+    w[0] = v[4 * i + 1];
+    w[1] = v[4 * i + 2];
+    w[2] = v[4 * i + 3];
+    w[3] = i + 1 < n ? v[4 * (i + 1)] : v[0];
+    return from_u64_limbs_dev(w);
+}
+__global__ void k_lookup_nd_(uint64_t *num, uint64_t *den, const uint64_t *f, const uint64_t *t,
+                             const uint64_t *h1, const uint64_t *h2, Fr delta, Fr eps, uint64_t n) {
+    uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    Fr opd = delta + Fr::one();
+    Fr eopd = eps * opd;
+    Fr tn = load_shift8(t, i, n), h1n = load_shift8(h1, i, n);
+    Fr fi = load_fr(f, i), ti = load_fr(t, i), h1i = load_fr(h1, i), h2i = load_fr(h2, i);
+    Fr r = (eopd + ti + delta * tn) * (opd * (eps + fi));
+    Fr d = (h2i * delta + (eopd + h1i)) * ((eopd + h2i) + h1n * delta);
+    store_fr(num, i, r);
+    store_fr(den, i, d);
+}
+void k_lookup_nd(uint64_t *num, uint64_t *den, const uint64_t *f, const uint64_t *t,
+                 const uint64_t *h1, const uint64_t *h2, const Fr &delta, const Fr &eps, uint64_t n,
+                 hipStream_t s) {
+    hipLaunchKernelGGL(k_lookup_nd_, dim3(nblk(n)), dim3(256), 0, s, num, den, f, t, h1, h2, delta, eps,
+                       n);
+    PNP_HIP(hipGetLastError());
+}
+
+__global__ void k_mul_inplace_(uint64_t *a, const uint64_t *b, uint64_t n) {
+    uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    if (i < n) store_fr(a, i, load_fr(a, i) * load_fr(b, i));
+}
+void k_mul_inplace(uint64_t *a, const uint64_t *b, uint64_t n, hipStream_t s) {
+    hipLaunchKernelGGL(k_mul_inplace_, dim3(nblk(n)), dim3(256), 0, s, a, b, n);
+    PNP_HIP(hipGetLastError());
+}
+
+// any non-zero word -> *flag = 1
+__global__ void k_any_nonzero_(const uint64_t *v, uint64_t words, unsigned *flag) {
+    uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    uint64_t acc = 0;
+    for (; i < words; i += stride) acc |= v[i];
+    if (__any(acc != 0) && (threadIdx.x & 63) == 0) atomicOr(flag, 1u);
+}
+bool k_any_nonzero(const uint64_t *v, uint64_t words, DevBuf &scratch, hipStream_t s) {
+    if (!words) return false;
+    if (scratch.bytes < 16) scratch.alloc(16);
+    unsigned *flag = static_cast<unsigned *>(scratch.p);
+    PNP_HIP(hipMemsetAsync(flag, 0, 4, s));
+    uint64_t blocks = (words + 255) / 256;
+    if (blocks > 4096) blocks = 4096;
+    hipLaunchKernelGGL(k_any_nonzero_, dim3((uint32_t)blocks), dim3(256), 0, s, v, words, flag);
+    PNP_HIP(hipGetLastError());
+    unsigned h = 0;
+    PNP_HIP(hipMemcpyAsync(&h, flag, 4, hipMemcpyDeviceToHost, s));
+    PNP_HIP(hipStreamSynchronize(s));
+    return h != 0;
+}
+
+// ---------------------------------------------------------------- quotient
+__device__ __forceinline__ Fr ld(const uint64_t *p, uint64_t i) {
+    return p ? load_fr(p, i) : Fr::zero();
+}
+__device__ __forceinline__ Fr pow5(const Fr &a) {
+    Fr a2 = a * a;
+    return a2 * a2 * a;
+}
+
+__global__ __launch_bounds__(256) void k_quotient_(QuotArgs q, uint64_t N8, uint64_t *out) {
+    uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    if (i >= N8) return;
+    uint64_t nx = i + 8 < N8 ? i + 8 : i + 8 - N8;
+    Fr a = load_fr(q.w8[0], i), b = load_fr(q.w8[1], i), c = load_fr(q.w8[2], i), d = load_fr(q.w8[3], i);
+    // compute_quotient_i (widget/arithmetic.cu:7-45) + pi
+    Fr acc = a * b * load_fr(q.q_m, i);
+    acc += a * load_fr(q.q_l, i);
+    acc += b * load_fr(q.q_r, i);
+    acc += c * load_fr(q.q_o, i);
+    acc += d * load_fr(q.q_4, i);
+    acc += pow5(a) * load_fr(q.q_hl, i);
+    acc += pow5(b) * load_fr(q.q_hr, i);
+    acc += pow5(d) * load_fr(q.q_h4, i);
+    acc += load_fr(q.q_c, i);
+    Fr num = acc * load_fr(q.q_arith, i) + ld(q.pi8, i);
+    // permutation_compute_quotient (proof_system/permutation.cu:267-296)
+    Fr x = load_fr(q.lin, i);
+    Fr zi = load_fr(q.z8, i), zn = load_fr(q.z8, nx);
+    Fr pa = (x * q.beta + a + q.gamma) * (x * q.bk[1] + b + q.gamma) *
+            (x * q.bk[2] + c + q.gamma) * (x * q.bk[3] + d + q.gamma);
+    pa = pa * zi * q.alpha;
+    Fr pb = (load_fr(q.sig[0], i) * q.beta + a + q.gamma) * (load_fr(q.sig[1], i) * q.beta + b + q.gamma) *
+            (load_fr(q.sig[2], i) * q.beta + c + q.gamma) * (load_fr(q.sig[3], i) * q.beta + d + q.gamma);
+    pb = pb * zn * q.alpha;
+    num += pa - pb + (zi - Fr::one()) * load_fr(q.l1a8, i);
+    // _compute_quotient_i (widget/lookup.cu:3-134)
+    Fr f = ld(q.f8, i), tt = ld(q.t8, i), ttn = ld(q.t8, nx);
+    Fr h1 = ld(q.h18, i), h1n = ld(q.h18, nx), h2 = ld(q.h28, i);
+    Fr z2 = load_fr(q.z28, i), z2n = load_fr(q.z28, nx);
+    Fr ct = d;
+    ct = ct * q.zeta + c;
+    ct = ct * q.zeta + b;
+    ct = ct * q.zeta + a;
+    Fr lk = (ct - f) * ld(q.q_lookup, i) * q.lsep;
+    lk += z2 * q.opd * (f + q.eps) * (tt + q.eopd + ttn * q.delta) * q.sep2;
+    lk -= z2n * (h1 + q.eopd + h2 * q.delta) * (h2 + q.eopd + h1n * q.delta) * q.sep2;
+    lk += (z2 - Fr::one()) * (load_fr(q.l18, i) * q.sep3);
+    num += lk;
+    store_fr(out, i, num * load_fr(q.vh_inv, i));
+}
+void k_quotient(const QuotArgs &q, uint64_t N8, uint64_t *out, hipStream_t s) {
+    hipLaunchKernelGGL(k_quotient_, dim3(nblk(N8)), dim3(256), 0, s, q, N8, out);
+    PNP_HIP(hipGetLastError());
+}
+
+// ---------------------------------------------------------------- linear combination
+__global__ __launch_bounds__(256) void k_lincomb_(LinArgs a, uint64_t n, uint64_t *out) {
+    uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    Fr acc = Fr::zero();
+    for (int k = 0; k < a.k; k++) acc += load_fr(a.p[k], i) * a.s[k];
+    store_fr(out, i, acc);
+}
+void k_lincomb(const LinArgs &a, uint64_t n, uint64_t *out, hipStream_t s) {
+    hipLaunchKernelGGL(k_lincomb_, dim3(nblk(n)), dim3(256), 0, s, a, n, out);
+    PNP_HIP(hipGetLastError());
+}
+
+}  // namespace pnp

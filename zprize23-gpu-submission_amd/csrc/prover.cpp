@@ -1,0 +1,511 @@
+// prover.cpp — gen_proof orchestration on one MI355X.
+//
+// Protocol order, transcript labels and formulas follow the reference's
+// prove() (lib/PLONK/src/gen_proof.cuh:10-489) step by step, including its
+// circuit-class shortcuts: transcript "Merkle tree", h1 = h2 =
+// 0 (combine_split skipped), empty q_m / custom-selector / q_lookup coeffs, one
+// public input, the 8-byte t_next / h1_next shift.  Inputs outside that class
+// (non-zero custom-gate selectors or lookup tables) are rejected with
+// PNP_E_ENVELOPE instead of silently diverging.
+//
+// What differs is HOW it runs on MI355X:
+//   * the prover key and SRS are HBM-resident (pnp_load_*), no per-proof H2D
+//     copies (the reference re-copies ~23 GB per proof, gen_proof.cuh:64-78,
+//     166-180, quotient.cu:201-367);
+//   * one stream, buffers sized once and reused (no per-op allocation);
+//   * fused passes (protocol.hip) instead of ~100 single-op launches;
+//   * MSMs of polynomials that are identically zero (h1, h2, and f / table
+//     when the lookup tables are empty) are not launched: their commitment is
+//     the point at infinity, exactly what the MSM would return;
+//   * the 14 commitments in the openings whose values never reach the proof
+//     (gen_proof.cuh:421, 450: aw/saw commits only feed empty randomness) are
+//     not computed; z_comm is the z commitment (saw_commits[0] == commit(z)).
+#include <chrono>
+#include <string.h>
+#include "context.h"
+#include "protocol.h"
+#include "transcript.h"
+
+namespace pnp {
+
+namespace {
+
+struct Timer {
+    pnp_ctx *ctx;
+    std::chrono::steady_clock::time_point t0;
+    explicit Timer(pnp_ctx *c) : ctx(c), t0(std::chrono::steady_clock::now()) { ctx->stages.clear(); }
+    void mark(const char *name) {
+        PNP_HIP(hipStreamSynchronize(ctx->stream));
+        auto t1 = std::chrono::steady_clock::now();
+        ctx->stages.emplace_back(name, std::chrono::duration<double, std::milli>(t1 - t0).count());
+        t0 = t1;
+    }
+};
+
+Fr fr_from_u64(uint64_t x) {
+    Fr r = Fr::zero();
+    r.v[0] = (uint32_t)x;
+    r.v[1] = (uint32_t)(x >> 32);
+    return to_mont(r);
+}
+
+Fr root_of_unity(uint32_t lg) {
+    const uint64_t root32[4] = {13381757501831005802ULL, 6564924994866501612ULL,
+                                789602057691799140ULL, 6625830629041353339ULL};
+    return pow_u64(from_u64_limbs<FrP>(root32), 1ULL << (32 - lg));
+}
+
+void append_comm(Transcript &t, const char *label, const CommitmentC &c) {
+    t.append_point(label, c.x, c.y);
+}
+
+void set_infinity(CommitmentC *c) {
+    memset(c, 0, sizeof *c);
+    to_u64_limbs(Fq::one(), c->y);
+}
+
+void store_fr_host(uint64_t out[4], const Fr &a) { to_u64_limbs(a, out); }
+
+}  // namespace
+
+int prove_impl(pnp_ctx *ctx, const CircuitC *cs, int device_ptrs, ProofC *out) {
+    if (!ctx->pk_loaded || !ctx->ck_loaded) {
+        set_error("prover key / commit key not loaded");
+        return PNP_E_NOKEY;
+    }
+    memset(out, 0, sizeof *out);
+    hipStream_t s = ctx->stream;
+    PNP_HIP(hipSetDevice(ctx->device));
+    uint64_t bound = cs->n > cs->lookup_len ? cs->n : cs->lookup_len;
+    uint64_t n = 1;
+    uint32_t lg = 0;
+    while (n < bound) { n <<= 1; lg++; }
+    if (n != ctx->pk_n) {
+        set_error("circuit domain %llu != prover key domain %llu", (unsigned long long)n,
+                  (unsigned long long)ctx->pk_n);
+        return PNP_E_ARG;
+    }
+    if (ctx->ck_points < n) {
+        set_error("commit key has %llu points, need %llu", (unsigned long long)ctx->ck_points,
+                  (unsigned long long)n);
+        return PNP_E_ARG;
+    }
+    if (cs->intended_pi_pos >= n || !cs->pi) {
+        set_error("public input position out of range");
+        return PNP_E_ARG;
+    }
+    const uint64_t N8 = 8 * n, ng = cs->n;
+    const ProverKeyC &pk = ctx->pk_dev;
+    Timer tm(ctx);
+    auto &nt = ctx->ntt;
+
+    // ---------------- inputs: padded witness evaluations (pad_poly)
+    uint64_t *wsc[4], *wpoly[4];
+    const uint64_t *wsrc[4] = {cs->w_l, cs->w_r, cs->w_o, cs->w_4};
+    const hipMemcpyKind kind = device_ptrs ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
+    for (int j = 0; j < 4; j++) {
+        wsc[j] = ctx->buf("wsc" + std::to_string(j), n);
+        wpoly[j] = ctx->buf("wpoly" + std::to_string(j), n);
+        PNP_HIP(hipMemcpyAsync(wsc[j], wsrc[j], 32 * ng, kind, s));
+        if (n > ng) PNP_HIP(hipMemsetAsync(wsc[j] + 4 * ng, 0, 32 * (n - ng), s));
+    }
+    uint64_t *qlk = ctx->buf("qlk", n);
+    PNP_HIP(hipMemcpyAsync(qlk, cs->q_lookup, 32 * ng, kind, s));
+    tm.mark("inputs");
+
+    Transcript tr("Merkle tree");
+    tr.append_pi("pi", cs->pi, cs->intended_pi_pos);
+
+    // ---------------- round 1: witness polynomials (gen_proof.cuh:25-50)
+    for (int j = 0; j < 4; j++) {
+        PNP_HIP(hipMemcpyAsync(wpoly[j], wsc[j], 32 * n, hipMemcpyDeviceToDevice, s));
+        ntt_run(nt, wpoly[j], lg, true, false, s);
+    }
+    tm.mark("r1_intt");
+    CommitmentC *wc[4] = {&out->a_comm, &out->b_comm, &out->c_comm, &out->d_comm};
+    for (int j = 0; j < 4; j++) commit_affine(ctx, wpoly[j], n, wc[j]);
+    append_comm(tr, "w_l", *wc[0]);
+    append_comm(tr, "w_r", *wc[1]);
+    append_comm(tr, "w_o", *wc[2]);
+    append_comm(tr, "w_4", *wc[3]);
+    tm.mark("r1_commit");
+
+    // ---------------- round 2: lookup (gen_proof.cuh:52-125)
+    Fr zeta = tr.challenge_scalar("zeta");
+    tr.append_scalar("zeta", zeta);
+    uint64_t *tc = ctx->buf("tc", n), *table_poly = ctx->buf("table_poly", n);
+    k_compress4(tc, pk.table1, pk.table2, pk.table3, pk.table4, zeta, n, s);
+    const bool table_zero = !k_any_nonzero(tc, 4 * n, ctx->scratch_b, s);
+    uint64_t *fc = ctx->buf("fc", n), *f_poly = ctx->buf("f_poly", n);
+    const uint64_t *wconst[4] = {wsc[0], wsc[1], wsc[2], wsc[3]};
+    k_query_f(fc, qlk, ng, wconst, tc, zeta, n, s);
+    const bool f_zero = !k_any_nonzero(fc, 4 * n, ctx->scratch_b, s);
+    PNP_HIP(hipMemcpyAsync(table_poly, tc, 32 * n, hipMemcpyDeviceToDevice, s));
+    PNP_HIP(hipMemcpyAsync(f_poly, fc, 32 * n, hipMemcpyDeviceToDevice, s));
+    if (!table_zero) ntt_run(nt, table_poly, lg, true, false, s);
+    if (!f_zero) ntt_run(nt, f_poly, lg, true, false, s);
+    if (f_zero) set_infinity(&out->f_comm); else commit_affine(ctx, f_poly, n, &out->f_comm);
+    append_comm(tr, "f", out->f_comm);
+    // h1 = h2 = 0 (combine_split skipped): commitments are the point at infinity
+    uint64_t *zero_n = ctx->buf("zero_n", n);
+    PNP_HIP(hipMemsetAsync(zero_n, 0, 32 * n, s));
+    set_infinity(&out->h_1_comm);
+    set_infinity(&out->h_2_comm);
+    append_comm(tr, "h1", out->h_1_comm);
+    append_comm(tr, "h2", out->h_2_comm);
+    tm.mark("r2_lookup");
+
+    // ---------------- round 3: permutation (gen_proof.cuh:127-208)
+    Fr beta = tr.challenge_scalar("beta");
+    tr.append_scalar("beta", beta);
+    Fr gamma = tr.challenge_scalar("gamma");
+    tr.append_scalar("gamma", gamma);
+    Fr delta = tr.challenge_scalar("delta");
+    tr.append_scalar("delta", delta);
+    Fr eps = tr.challenge_scalar("epsilon");
+    tr.append_scalar("epsilon", eps);
+    if (beta == gamma || beta == delta || beta == eps || gamma == delta || gamma == eps ||
+        delta == eps) {
+        set_error("challenges must be different");  // gen_proof.cuh:152-157 asserts
+        return PNP_E_ARG;
+    }
+    PermArgs pa;
+    const uint64_t *sigc[4] = {pk.left_sigma_coeffs, pk.right_sigma_coeffs, pk.out_sigma_coeffs,
+                               pk.fourth_sigma_coeffs};
+    for (int j = 0; j < 4; j++) {
+        uint64_t *sg = ctx->buf("sig" + std::to_string(j), n);
+        PNP_HIP(hipMemcpyAsync(sg, sigc[j], 32 * n, hipMemcpyDeviceToDevice, s));
+        ntt_run(nt, sg, lg, false, false, s);  // NTT.forward(sigma_polys[j])
+        pa.w[j] = wsc[j];
+        pa.sigma[j] = sg;
+    }
+    const uint64_t kv[4] = {1, 7, 13, 17};  // K1..K3 (permutation/constants.cu:3-15)
+    for (int j = 0; j < 4; j++) pa.bk[j] = beta * fr_from_u64(kv[j]);
+    pa.beta = beta;
+    pa.gamma = gamma;
+    pa.omega = root_of_unity(lg);
+    uint64_t *num = ctx->buf("num", n), *den = ctx->buf("den", n);
+    uint64_t *z_poly = ctx->buf("z_poly", n);
+    k_perm_numden(num, den, pa, n, s);
+    k_batch_inverse(den, n, ctx->scratch_a, s);
+    k_mul_inplace(num, den, n, s);
+    k_prefix_product(num, n, ctx->scratch_a, s);
+    PNP_HIP(hipMemcpyAsync(z_poly, num, 32 * n, hipMemcpyDeviceToDevice, s));
+    ntt_run(nt, z_poly, lg, true, false, s);
+    tm.mark("r3_z");
+    commit_affine(ctx, z_poly, n, &out->z_comm);
+    append_comm(tr, "z", out->z_comm);
+    // lookup grand product (permutation/mod.cu:111-144), h1 = h2 = 0
+    uint64_t *z2_poly = ctx->buf("z2_poly", n);
+    k_lookup_nd(num, den, fc, tc, zero_n, zero_n, delta, eps, n, s);
+    k_batch_inverse(den, n, ctx->scratch_a, s);
+    k_mul_inplace(num, den, n, s);
+    k_prefix_product(num, n, ctx->scratch_a, s);
+    PNP_HIP(hipMemcpyAsync(z2_poly, num, 32 * n, hipMemcpyDeviceToDevice, s));
+    ntt_run(nt, z2_poly, lg, true, false, s);
+    commit_affine(ctx, z2_poly, n, &out->z_2_comm);  // not appended (gen_proof.cuh:200-205)
+    // public input poly (pi.cu:11-15)
+    uint64_t *pi_poly = ctx->buf("pi_poly", n);
+    PNP_HIP(hipMemsetAsync(pi_poly, 0, 32 * n, s));
+    {
+        uint64_t piv[4];
+        to_u64_limbs(to_mont(from_u64_limbs<FrP>(cs->pi)), piv);
+        PNP_HIP(hipMemcpyAsync(pi_poly + 4 * cs->intended_pi_pos, piv, 32, hipMemcpyHostToDevice, s));
+        PNP_HIP(hipStreamSynchronize(s));
+    }
+    ntt_run(nt, pi_poly, lg, true, false, s);
+    tm.mark("r3_z2_pi");
+
+    // ---------------- round 4: quotient (gen_proof.cuh:209-267, quotient.cu:142-376)
+    Fr alpha = tr.challenge_scalar("alpha");
+    tr.append_scalar("alpha", alpha);
+    Fr range_c = tr.challenge_scalar("range separation challenge");
+    tr.append_scalar("range seperation challenge", range_c);
+    Fr logic_c = tr.challenge_scalar("logic separation challenge");
+    tr.append_scalar("logic seperation challenge", logic_c);
+    Fr fixed_c = tr.challenge_scalar("fixed base separation challenge");
+    tr.append_scalar("fixed base separation challenge", fixed_c);
+    Fr var_c = tr.challenge_scalar("variable base separation challenge");
+    tr.append_scalar("variable base separation challenge", var_c);
+    Fr lsep = tr.challenge_scalar("lookup separation challenge");
+    tr.append_scalar("lookup separation challenge", lsep);
+
+    QuotArgs q;
+    for (int j = 0; j < 4; j++) {
+        uint64_t *w8 = ctx->buf("w8_" + std::to_string(j), N8);
+        coset_lde8(nt, wpoly[j], w8, lg, s);
+        q.w8[j] = w8;
+    }
+    uint64_t *z8 = ctx->buf("z8", N8), *pi8 = ctx->buf("pi8", N8), *z28 = ctx->buf("z28", N8);
+    coset_lde8(nt, z_poly, z8, lg, s);
+    coset_lde8(nt, pi_poly, pi8, lg, s);
+    coset_lde8(nt, z2_poly, z28, lg, s);
+    q.z8 = z8;
+    q.pi8 = pi8;
+    q.z28 = z28;
+    q.f8 = q.t8 = nullptr;
+    if (!f_zero) {
+        uint64_t *f8 = ctx->buf("f8", N8);
+        coset_lde8(nt, f_poly, f8, lg, s);
+        q.f8 = f8;
+    }
+    if (!table_zero) {
+        uint64_t *t8 = ctx->buf("t8", N8);
+        coset_lde8(nt, table_poly, t8, lg, s);
+        q.t8 = t8;
+    }
+    q.h18 = q.h28 = nullptr;  // h1 = h2 = 0
+    // compute_first_lagrange_poly_scaled(n, alpha^2) and (n, 1) (quotient.cu:3-8)
+    Fr alpha2 = alpha * alpha;
+    uint64_t *l1a = ctx->buf("l1a", n), *l1 = ctx->buf("l1", n);
+    uint64_t *l1a8 = ctx->buf("l1a8", N8), *l18 = ctx->buf("l18", N8);
+    {
+        uint64_t v[4];
+        PNP_HIP(hipMemsetAsync(l1a, 0, 32 * n, s));
+        PNP_HIP(hipMemsetAsync(l1, 0, 32 * n, s));
+        to_u64_limbs(alpha2, v);
+        PNP_HIP(hipMemcpyAsync(l1a, v, 32, hipMemcpyHostToDevice, s));
+        PNP_HIP(hipStreamSynchronize(s));
+        to_u64_limbs(Fr::one(), v);
+        PNP_HIP(hipMemcpyAsync(l1, v, 32, hipMemcpyHostToDevice, s));
+        PNP_HIP(hipStreamSynchronize(s));
+    }
+    ntt_run(nt, l1a, lg, true, false, s);
+    ntt_run(nt, l1, lg, true, false, s);
+    coset_lde8(nt, l1a, l1a8, lg, s);
+    coset_lde8(nt, l1, l18, lg, s);
+    q.l1a8 = l1a8;
+    q.l18 = l18;
+    q.q_m = pk.q_m_evals;
+    q.q_l = pk.q_l_evals;
+    q.q_r = pk.q_r_evals;
+    q.q_o = pk.q_o_evals;
+    q.q_4 = pk.q_4_evals;
+    q.q_c = pk.q_c_evals;
+    q.q_hl = pk.q_hl_evals;
+    q.q_hr = pk.q_hr_evals;
+    q.q_h4 = pk.q_h4_evals;
+    q.q_arith = pk.q_arith_evals;
+    q.q_lookup = pk.q_lookup_evals;
+    q.sig[0] = pk.left_sigma_evals;
+    q.sig[1] = pk.right_sigma_evals;
+    q.sig[2] = pk.out_sigma_evals;
+    q.sig[3] = pk.fourth_sigma_evals;
+    q.lin = pk.linear_evaluations;
+    uint64_t *vh_inv = ctx->buf("vh_inv", N8);
+    PNP_HIP(hipMemcpyAsync(vh_inv, pk.v_h_coset_8n, 32 * N8, hipMemcpyDeviceToDevice, s));
+    k_batch_inverse(vh_inv, N8, ctx->scratch_a, s);
+    q.vh_inv = vh_inv;
+    q.alpha = alpha;
+    q.beta = beta;
+    q.gamma = gamma;
+    q.delta = delta;
+    q.eps = eps;
+    q.zeta = zeta;
+    q.lsep = lsep;
+    for (int j = 0; j < 4; j++) q.bk[j] = pa.bk[j];
+    q.opd = delta + Fr::one();
+    q.eopd = eps * q.opd;
+    q.sep2 = lsep * lsep;
+    q.sep3 = q.sep2 * lsep;
+    tm.mark("r4_lde");
+    uint64_t *t_poly = ctx->buf("t_poly", N8);
+    k_quotient(q, N8, t_poly, s);
+    tm.mark("r4_quotient");
+    ntt_run(nt, t_poly, lg + 3, true, true, s);  // Intt_coset
+    tm.mark("r4_intt8");
+    CommitmentC *tcm[8] = {&out->t_1_comm, &out->t_2_comm, &out->t_3_comm, &out->t_4_comm,
+                           &out->t_5_comm, &out->t_6_comm, &out->t_7_comm, &out->t_8_comm};
+    for (int k = 0; k < 8; k++) commit_affine(ctx, t_poly + 4 * (uint64_t)k * n, n, tcm[k]);
+    const char *tl[8] = {"t_1", "t_2", "t_3", "t_4", "t_5", "t_6", "t_7", "t_8"};
+    for (int k = 0; k < 8; k++) append_comm(tr, tl[k], *tcm[k]);
+    tm.mark("r4_commit");
+
+    // ---------------- round 5: linearisation (linearisation.cu:73-306)
+    Fr zc = tr.challenge_scalar("z");
+    tr.append_scalar("z", zc);
+    Fr omega = root_of_unity(lg);
+    Fr zw = zc * omega;
+    Fr vh = pow_u64(zc, n) - Fr::one();
+    Fr zn = vh + Fr::one();
+    Fr l1e = vh * inverse(fr_from_u64(n) * (zc - Fr::one()));
+    ProofEvaluationsC *ev = &out->evaluations;
+    {
+        // evaluations at z
+        const uint64_t *pz[12] = {wpoly[0], wpoly[1], wpoly[2], wpoly[3], pk.left_sigma_coeffs,
+                                  pk.right_sigma_coeffs, pk.out_sigma_coeffs, pk.q_arith_coeffs,
+                                  pk.q_c_coeffs, pk.q_l_coeffs, pk.q_r_coeffs, pk.q_hl_coeffs};
+        Fr rz[12];
+        k_poly_eval_multi(pz, 12, n, zc, ctx->scratch_a, rz, s);
+        const uint64_t *pz2[2] = {pk.q_hr_coeffs, pk.q_h4_coeffs};
+        Fr rz2[2];
+        k_poly_eval_multi(pz2, 2, n, zc, ctx->scratch_a, rz2, s);
+        // evaluations at z * omega
+        const uint64_t *pw[4] = {z_poly, wpoly[0], wpoly[1], wpoly[3]};
+        Fr rw[4];
+        k_poly_eval_multi(pw, 4, n, zw, ctx->scratch_a, rw, s);
+        Fr z2n;
+        k_poly_eval(z2_poly, n, zw, ctx->scratch_a, &z2n, s);
+        Fr f_eval = Fr::zero(), t_eval = Fr::zero(), t_next = Fr::zero();
+        if (!f_zero) k_poly_eval(f_poly, n, zc, ctx->scratch_a, &f_eval, s);
+        if (!table_zero) {
+            k_poly_eval(table_poly, n, zc, ctx->scratch_a, &t_eval, s);
+            k_poly_eval(table_poly, n, zw, ctx->scratch_a, &t_next, s);
+        }
+        store_fr_host(ev->wire_evals.a_eval, rz[0]);
+        store_fr_host(ev->wire_evals.b_eval, rz[1]);
+        store_fr_host(ev->wire_evals.c_eval, rz[2]);
+        store_fr_host(ev->wire_evals.d_eval, rz[3]);
+        store_fr_host(ev->perm_evals.left_sigma_eval, rz[4]);
+        store_fr_host(ev->perm_evals.right_sigma_eval, rz[5]);
+        store_fr_host(ev->perm_evals.out_sigma_eval, rz[6]);
+        store_fr_host(ev->perm_evals.permutation_eval, rw[0]);
+        CustomEvaluationsC *cu = &ev->custom_evals;
+        store_fr_host(cu->q_arith_eval, rz[7]);
+        store_fr_host(cu->q_c_eval, rz[8]);
+        store_fr_host(cu->q_l_eval, rz[9]);
+        store_fr_host(cu->q_r_eval, rz[10]);
+        store_fr_host(cu->q_hl_eval, rz[11]);
+        store_fr_host(cu->q_hr_eval, rz2[0]);
+        store_fr_host(cu->q_h4_eval, rz2[1]);
+        store_fr_host(cu->a_next_eval, rw[1]);
+        store_fr_host(cu->b_next_eval, rw[2]);
+        store_fr_host(cu->d_next_eval, rw[3]);
+        LookupEvaluationsC *lk = &ev->lookup_evals;  // q_lookup, h1, h1_next, h2 evals = 0
+        store_fr_host(lk->z2_next_eval, z2n);
+        store_fr_host(lk->f_eval, f_eval);
+        store_fr_host(lk->table_eval, t_eval);
+        store_fr_host(lk->table_next_eval, t_next);
+    }
+    tm.mark("r5_evals");
+    auto ld = [](const uint64_t *p) { return from_u64_limbs<FrP>(p); };
+    const Fr ae = ld(ev->wire_evals.a_eval), be = ld(ev->wire_evals.b_eval),
+             ce = ld(ev->wire_evals.c_eval), de = ld(ev->wire_evals.d_eval);
+    const Fr qae = ld(ev->custom_evals.q_arith_eval);
+    LinArgs la;
+    la.k = 0;
+    auto push = [&](const uint64_t *p, const Fr &sc) {
+        la.p[la.k] = p;
+        la.s[la.k] = sc;
+        la.k++;
+    };
+    auto p5 = [](const Fr &x) { Fr x2 = x * x; return x2 * x2 * x; };
+    // compute_linearisation_arithmetic (widget/arithmetic.cu:47-80), q_m coeffs empty
+    push(pk.q_l_coeffs, ae * qae);
+    push(pk.q_r_coeffs, be * qae);
+    push(pk.q_o_coeffs, ce * qae);
+    push(pk.q_4_coeffs, de * qae);
+    push(pk.q_hl_coeffs, p5(ae) * qae);
+    push(pk.q_hr_coeffs, p5(be) * qae);
+    push(pk.q_h4_coeffs, p5(de) * qae);
+    push(pk.q_c_coeffs, qae);
+    // compute_linearisation_permutation (proof_system/permutation.cu:231-265)
+    {
+        Fr bz = beta * zc;
+        Fr a = (ae + bz + gamma) * (be + fr_from_u64(7) * bz + gamma) *
+               (ce + fr_from_u64(13) * bz + gamma) * (de + fr_from_u64(17) * bz + gamma) * alpha;
+        push(z_poly, a + l1e * alpha2);
+        const Fr s1 = ld(ev->perm_evals.left_sigma_eval), s2 = ld(ev->perm_evals.right_sigma_eval),
+                 s3 = ld(ev->perm_evals.out_sigma_eval), pe = ld(ev->perm_evals.permutation_eval);
+        Fr b = (ae + beta * s1 + gamma) * (be + beta * s2 + gamma) * (ce + beta * s3 + gamma) *
+               (beta * pe) * alpha;
+        push(pk.fourth_sigma_coeffs, neg(b));
+    }
+    // compute_linearisation_lookup (widget/lookup.cu:136-199); q_lookup coeffs empty,
+    // the h1_poly term is identically zero (h1 = 0)
+    {
+        const LookupEvaluationsC *lk = &ev->lookup_evals;
+        Fr sep2 = lsep * lsep, sep3 = sep2 * lsep, opd = delta + Fr::one(), eopd = eps * opd;
+        Fr b0 = eps + ld(lk->f_eval);
+        Fr b1 = eopd + ld(lk->table_eval) + delta * ld(lk->table_next_eval);
+        push(z2_poly, opd * b0 * b1 * sep2 + l1e * sep3);
+    }
+    // - Z_H(z) * sum_k z^(kn) t_(k+1)  (linearisation.cu:250-292)
+    {
+        Fr p = neg(vh);
+        for (int k = 0; k < 8; k++) {
+            push(t_poly + 4 * (uint64_t)k * n, p);
+            p = p * zn;
+        }
+    }
+    uint64_t *lin = ctx->buf("lin", n);
+    k_lincomb(la, n, lin, s);
+    tm.mark("r5_lin");
+
+    // transcript appends (gen_proof.cuh:373-403)
+    tr.append_scalar("a_eval", ae);
+    tr.append_scalar("b_eval", be);
+    tr.append_scalar("c_eval", ce);
+    tr.append_scalar("d_eval", de);
+    tr.append_scalar("left_sig_eval", ld(ev->perm_evals.left_sigma_eval));
+    tr.append_scalar("right_sig_eval", ld(ev->perm_evals.right_sigma_eval));
+    tr.append_scalar("out_sig_eval", ld(ev->perm_evals.out_sigma_eval));
+    tr.append_scalar("perm_eval", ld(ev->perm_evals.permutation_eval));
+    const LookupEvaluationsC *lk = &ev->lookup_evals;
+    tr.append_scalar("f_eval", ld(lk->f_eval));
+    tr.append_scalar("q_lookup_eval", ld(lk->q_lookup_eval));
+    tr.append_scalar("lookup_perm_eval", ld(lk->z2_next_eval));
+    tr.append_scalar("h_1_eval", ld(lk->h1_eval));
+    tr.append_scalar("h_1_next_eval", ld(lk->h1_next_eval));
+    tr.append_scalar("h_2_eval", ld(lk->h2_eval));
+    const CustomEvaluationsC *cu = &ev->custom_evals;
+    tr.append_scalar("q_arith_eval", ld(cu->q_arith_eval));
+    tr.append_scalar("q_c_eval", ld(cu->q_c_eval));
+    tr.append_scalar("q_l_eval", ld(cu->q_l_eval));
+    tr.append_scalar("q_r_eval", ld(cu->q_r_eval));
+    tr.append_scalar("q_hl_eval", ld(cu->q_hl_eval));
+    tr.append_scalar("q_hr_eval", ld(cu->q_hr_eval));
+    tr.append_scalar("q_h4_eval", ld(cu->q_h4_eval));
+    tr.append_scalar("a_next_eval", ld(cu->a_next_eval));
+    tr.append_scalar("b_next_eval", ld(cu->b_next_eval));
+    tr.append_scalar("d_next_eval", ld(cu->d_next_eval));
+
+    // ---------------- round 6: openings (gen_proof.cuh:405-463, kzg10.cu:116-145)
+    uint64_t *comb = ctx->buf("comb", n);
+    {
+        Fr aw = tr.challenge_scalar("aggregate_witness");
+        const uint64_t *awp[11] = {lin, pk.left_sigma_coeffs, pk.right_sigma_coeffs,
+                                   pk.out_sigma_coeffs, f_poly, zero_n /* h2 */, table_poly,
+                                   wpoly[0], wpoly[1], wpoly[2], wpoly[3]};
+        LinArgs oa;
+        oa.k = 0;
+        Fr p = Fr::one();
+        for (int k = 0; k < 11; k++) {
+            bool skip = (k == 4 && f_zero) || k == 5 || (k == 6 && table_zero);
+            if (!skip) {
+                oa.p[oa.k] = awp[k];
+                oa.s[oa.k] = p;
+                oa.k++;
+            }
+            p = p * aw;
+        }
+        k_lincomb(oa, n, comb, s);
+        k_poly_div_linear(comb, n, zc, ctx->scratch_a, s);
+        commit_affine(ctx, comb, n, &out->aw_opening);
+    }
+    tm.mark("r6_aw");
+    {
+        Fr saw = tr.challenge_scalar("aggregate_witness");
+        const uint64_t *sawp[7] = {z_poly, wpoly[0], wpoly[1], wpoly[3], zero_n /* h1 */, z2_poly,
+                                   table_poly};
+        LinArgs oa;
+        oa.k = 0;
+        Fr p = Fr::one();
+        for (int k = 0; k < 7; k++) {
+            bool skip = k == 4 || (k == 6 && table_zero);
+            if (!skip) {
+                oa.p[oa.k] = sawp[k];
+                oa.s[oa.k] = p;
+                oa.k++;
+            }
+            p = p * saw;
+        }
+        k_lincomb(oa, n, comb, s);
+        k_poly_div_linear(comb, n, zw, ctx->scratch_a, s);
+        commit_affine(ctx, comb, n, &out->saw_opening);
+    }
+    tm.mark("r6_saw");
+    return PNP_OK;
+}
+
+}  // namespace pnp

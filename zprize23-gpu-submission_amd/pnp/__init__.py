@@ -1,0 +1,164 @@
+"""Python host mirror of the gen_proof C-ABI (include/pnp_plonk.h).
+
+The reference host is Rust: Prover::prove_pnp (plonk-core/src/proof_system/
+prover.rs:693-907) marshals CircuitC / ProverKeyC / CommitKeyC and calls the
+extern "C" gen_proof (plonk-core/src/lib.rs:237-239).  Rust is not available
+in this image, so tests and the bench drive the same ABI through ctypes:
+
+    lib = pnp.load()                      # libpnp_plonk.so, fails loudly if absent
+    proof = lib.gen_proof(circuit, pk, ck)   # v1, by value, like lib.rs
+
+plus the v2 resident-key API (Context) used by the bench.  This package holds
+no compute: every field/curve operation runs in the HIP library.
+"""
+import ctypes as C
+import os
+
+from . import abi
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(os.path.dirname(_HERE), "lib", "libpnp_plonk.so")
+_LIB = None
+
+PNP_OK = 0
+ERRORS = {-1: "PNP_E_ARG", -2: "PNP_E_DEVICE", -3: "PNP_E_NOKEY", -4: "PNP_E_ENVELOPE",
+          -5: "PNP_E_NOMEM"}
+
+# exported symbols declared by include/pnp_plonk.h (checked by tests/test_abi.py)
+SYMBOLS = ("gen_proof", "pnp_last_error", "pnp_ctx_create", "pnp_ctx_destroy",
+           "pnp_load_prover_key", "pnp_load_commit_key", "pnp_prove", "pnp_last_stage_times",
+           "pnp_sync", "pnp_ntt", "pnp_coset_lde8", "pnp_commit", "pnp_poly_eval",
+           "pnp_poly_div_linear", "pnp_prefix_product", "pnp_batch_inverse",
+           "pnp_synth_random_fr", "pnp_synth_srs", "pnp_synth_coset_consts")
+
+
+class PnpError(RuntimeError):
+    pass
+
+
+def load(path: str = LIB_PATH):
+    """Load the HIP library.  There is no CPU fallback: a missing library raises."""
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    if not os.path.exists(path):
+        raise PnpError(f"{path} not built (run __graft_entry__.build() or make -C csrc)")
+    lib = C.CDLL(path)
+    vp, u64, i32 = C.c_void_p, C.c_uint64, C.c_int
+    lib.gen_proof.argtypes = [abi.CircuitC, abi.ProverKeyC, abi.CommitKeyC]
+    lib.gen_proof.restype = abi.ProofC
+    lib.pnp_last_error.restype = C.c_char_p
+    lib.pnp_ctx_create.argtypes = [i32, C.POINTER(vp)]
+    lib.pnp_ctx_destroy.argtypes = [vp]
+    lib.pnp_ctx_destroy.restype = None
+    lib.pnp_load_prover_key.argtypes = [vp, C.POINTER(abi.ProverKeyC), u64, i32]
+    lib.pnp_load_commit_key.argtypes = [vp, C.POINTER(abi.CommitKeyC), u64, i32]
+    lib.pnp_prove.argtypes = [vp, C.POINTER(abi.CircuitC), i32, C.POINTER(abi.ProofC)]
+    lib.pnp_last_stage_times.argtypes = [vp, C.POINTER(C.c_double), C.POINTER(C.c_char_p), i32]
+    lib.pnp_sync.argtypes = [vp]
+    lib.pnp_ntt.argtypes = [vp, vp, C.c_uint32, i32, i32]
+    lib.pnp_coset_lde8.argtypes = [vp, vp, vp, C.c_uint32]
+    lib.pnp_commit.argtypes = [vp, vp, vp, u64, C.POINTER(abi.CommitmentC)]
+    lib.pnp_poly_eval.argtypes = [vp, vp, u64, vp, vp]
+    lib.pnp_poly_div_linear.argtypes = [vp, vp, u64, vp]
+    lib.pnp_prefix_product.argtypes = [vp, vp, u64]
+    lib.pnp_batch_inverse.argtypes = [vp, vp, u64]
+    lib.pnp_synth_random_fr.argtypes = [vp, vp, u64, u64]
+    lib.pnp_synth_srs.argtypes = [vp, vp, u64, vp]
+    lib.pnp_synth_coset_consts.argtypes = [vp, vp, vp, C.c_uint32]
+    for name in SYMBOLS:
+        if name.startswith("pnp_") and name not in ("pnp_last_error", "pnp_ctx_destroy"):
+            getattr(lib, name).restype = C.c_int if name != "pnp_last_error" else C.c_char_p
+    _LIB = lib
+    return lib
+
+
+def check(rc: int, what: str = ""):
+    if rc != PNP_OK:
+        msg = load().pnp_last_error()
+        raise PnpError(f"{what}: {ERRORS.get(rc, rc)}: {msg.decode() if msg else ''}")
+
+
+class Context:
+    """One MI355X: stream, NTT tables, MSM buffers and HBM-resident keys."""
+
+    def __init__(self, device: int = 0):
+        self.lib = load()
+        h = C.c_void_p()
+        check(self.lib.pnp_ctx_create(device, C.byref(h)), "pnp_ctx_create")
+        self.h = h
+
+    def close(self):
+        if self.h:
+            self.lib.pnp_ctx_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ---- keys / prove
+    def load_prover_key(self, pk: abi.ProverKeyC, domain: int, device_ptrs: bool):
+        check(self.lib.pnp_load_prover_key(self.h, C.byref(pk), domain, int(device_ptrs)),
+              "pnp_load_prover_key")
+
+    def load_commit_key(self, ck: abi.CommitKeyC, n_points: int, device_ptrs: bool):
+        check(self.lib.pnp_load_commit_key(self.h, C.byref(ck), n_points, int(device_ptrs)),
+              "pnp_load_commit_key")
+
+    def prove(self, cs: abi.CircuitC, device_ptrs: bool) -> abi.ProofC:
+        out = abi.ProofC()
+        check(self.lib.pnp_prove(self.h, C.byref(cs), int(device_ptrs), C.byref(out)), "pnp_prove")
+        return out
+
+    def stage_times(self):
+        cap = 64
+        ms = (C.c_double * cap)()
+        names = (C.c_char_p * cap)()
+        k = self.lib.pnp_last_stage_times(self.h, ms, names, cap)
+        return [(names[i].decode(), ms[i]) for i in range(min(k, cap))]
+
+    # ---- operator API (HBM addresses as ints)
+    def sync(self):
+        check(self.lib.pnp_sync(self.h), "pnp_sync")
+
+    def ntt(self, addr: int, lg_n: int, inverse: bool = False, coset: bool = False):
+        check(self.lib.pnp_ntt(self.h, C.c_void_p(addr), lg_n, int(inverse), int(coset)), "pnp_ntt")
+
+    def coset_lde8(self, src: int, dst: int, lg_n: int):
+        check(self.lib.pnp_coset_lde8(self.h, C.c_void_p(src), C.c_void_p(dst), lg_n), "pnp_coset_lde8")
+
+    def commit(self, points: int, scalars: int, n: int) -> abi.CommitmentC:
+        out = abi.CommitmentC()
+        check(self.lib.pnp_commit(self.h, C.c_void_p(points), C.c_void_p(scalars), n, C.byref(out)),
+              "pnp_commit")
+        return out
+
+    def poly_eval(self, addr: int, n: int, x_limbs):
+        x = (C.c_uint64 * 4)(*x_limbs)
+        out = (C.c_uint64 * 4)()
+        check(self.lib.pnp_poly_eval(self.h, C.c_void_p(addr), n, x, out), "pnp_poly_eval")
+        return list(out)
+
+    def poly_div_linear(self, addr: int, n: int, z_limbs):
+        z = (C.c_uint64 * 4)(*z_limbs)
+        check(self.lib.pnp_poly_div_linear(self.h, C.c_void_p(addr), n, z), "pnp_poly_div_linear")
+
+    def prefix_product(self, addr: int, n: int):
+        check(self.lib.pnp_prefix_product(self.h, C.c_void_p(addr), n), "pnp_prefix_product")
+
+    def batch_inverse(self, addr: int, n: int):
+        check(self.lib.pnp_batch_inverse(self.h, C.c_void_p(addr), n), "pnp_batch_inverse")
+
+    def random_fr(self, addr: int, n: int, seed: int):
+        check(self.lib.pnp_synth_random_fr(self.h, C.c_void_p(addr), n, seed), "pnp_synth_random_fr")
+
+    def srs(self, addr: int, n: int, tau_limbs):
+        t = (C.c_uint64 * 4)(*tau_limbs)
+        check(self.lib.pnp_synth_srs(self.h, C.c_void_p(addr), n, t), "pnp_synth_srs")
+
+    def coset_consts(self, vh: int, x: int, lg_n: int):
+        check(self.lib.pnp_synth_coset_consts(self.h, C.c_void_p(vh), C.c_void_p(x), lg_n),
+              "pnp_synth_coset_consts")
