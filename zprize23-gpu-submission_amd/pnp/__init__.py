@@ -43,6 +43,14 @@ def load(path: str = LIB_PATH):
         return _LIB
     if not os.path.exists(path):
         raise PnpError(f"{path} not built (run __graft_entry__.build() or make -C csrc)")
+    # One HIP runtime per process: torch bundles its own libamdhip64.so.7.  If
+    # our library were loaded first it would pull /opt/rocm's copy and torch's
+    # later HSA init fails ("No HIP GPUs are available").  Loading torch first
+    # makes the soname resolve to the already-loaded runtime for both.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     lib = C.CDLL(path)
     vp, u64, i32 = C.c_void_p, C.c_uint64, C.c_int
     lib.gen_proof.argtypes = [abi.CircuitC, abi.ProverKeyC, abi.CommitKeyC]
