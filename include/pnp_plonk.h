@@ -230,6 +230,12 @@ int pnp_prove(pnp_ctx *ctx, const CircuitC *cs, int device_ptrs, ProofC *out);
  * Writes up to `cap` doubles and their names; returns the stage count. */
 int pnp_last_stage_times(pnp_ctx *ctx, double *ms, const char **names, int cap);
 
+/* Live per-kernel timing with HIP events recorded on the context stream
+ * around the named kernels ("msm_accumulate", "quotient"); totals since the
+ * last enable.  Used by bench.py for the roofline numbers. */
+int pnp_kernel_timing(pnp_ctx *ctx, int enable);
+int pnp_kernel_stats(pnp_ctx *ctx, const char *name, double *total_ms, int *launches);
+
 /* ------------------------------------------------------------------ */
 /* 3. Operator API on HBM pointers (mirrors PLONK/utils/function.cuh) */
 /*    All ops are asynchronous on the context stream; pnp_sync waits.  */

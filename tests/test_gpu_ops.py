@@ -160,3 +160,28 @@ def test_batch_inverse_large(ctx):
     d = to_dev(x)
     ctx.batch_inverse(d.data_ptr(), n)
     assert (from_dev(d) == exp).all()
+
+
+def test_synth_srs_and_coset_consts(ctx):
+    """The bench's on-GPU input generators match the CPU restatement."""
+    import torch
+    lib = oracle()
+    rng = np.random.default_rng(77)
+    n = 257
+    tau = rand_fr_mont_arr(rng, 1)
+    exp = np.zeros((n, 12), dtype=np.uint64)
+    lib.or_srs(vp(exp), n, vp(tau))
+    d = empty_dev(n, 12)
+    ctx.srs(d.data_ptr(), n, [int(v) for v in tau[0]])
+    assert (from_dev(d, 12) == exp).all()
+    from pnp_testlib import Inputs
+    inp = Inputs(6, 1)
+    vh, x = empty_dev(8 << 6), empty_dev(8 << 6)
+    ctx.coset_consts(vh.data_ptr(), x.data_ptr(), 6)
+    assert (from_dev(vh) == inp.arrays["v_h_coset_8n"]).all()
+    assert (from_dev(x) == inp.arrays["linear_evaluations"]).all()
+    r = empty_dev(4096)
+    ctx.random_fr(r.data_ptr(), 4096, 5)
+    vals = from_dev(r)
+    assert all(from_limbs(v) < R_MOD for v in vals[:256])
+    assert len({tuple(v) for v in vals}) == 4096

@@ -47,6 +47,40 @@ void commit_affine(pnp_ctx *ctx, const uint64_t *d_scalars, uint64_t n, Commitme
     memcpy(out->y, aff + 6, 48);
 }
 
+hipEvent_t KernelTimer::get() {
+    if (!pool.empty()) {
+        hipEvent_t e = pool.back();
+        pool.pop_back();
+        return e;
+    }
+    hipEvent_t e;
+    PNP_HIP(hipEventCreate(&e));
+    return e;
+}
+void KernelTimer::begin(const char *, hipStream_t s, hipEvent_t &e0) {
+    if (!enabled) return;
+    e0 = get();
+    PNP_HIP(hipEventRecord(e0, s));
+}
+void KernelTimer::end(const char *name, hipStream_t s, hipEvent_t e0) {
+    if (!enabled || !e0) return;
+    hipEvent_t e1 = get();
+    PNP_HIP(hipEventRecord(e1, s));
+    pending.push_back({name, {e0, e1}});
+}
+void KernelTimer::collect() {
+    for (auto &p : pending) {
+        float ms = 0;
+        PNP_HIP(hipEventElapsedTime(&ms, p.second.first, p.second.second));
+        auto &st = stats[p.first];
+        st.first += ms;
+        st.second += 1;
+        pool.push_back(p.second.first);
+        pool.push_back(p.second.second);
+    }
+    pending.clear();
+}
+
 }  // namespace pnp
 
 uint64_t *pnp_ctx::buf(const std::string &name, size_t elems_fr) {
@@ -93,6 +127,22 @@ void pnp_ctx_destroy(pnp_ctx *ctx) {
     (void)hipStreamSynchronize(ctx->stream);
     (void)hipStreamDestroy(ctx->stream);
     delete ctx;
+}
+
+int pnp_kernel_timing(pnp_ctx *ctx, int enable) {
+    if (!ctx) return PNP_E_ARG;
+    ctx->ktimer.enabled = enable != 0;
+    ctx->msm.timer = enable ? &ctx->ktimer : nullptr;
+    if (enable) ctx->ktimer.stats.clear();
+    return PNP_OK;
+}
+
+int pnp_kernel_stats(pnp_ctx *ctx, const char *name, double *total_ms, int *launches) {
+    if (!ctx || !name) return PNP_E_ARG;
+    auto it = ctx->ktimer.stats.find(name);
+    if (total_ms) *total_ms = it == ctx->ktimer.stats.end() ? 0.0 : it->second.first;
+    if (launches) *launches = it == ctx->ktimer.stats.end() ? 0 : it->second.second;
+    return PNP_OK;
 }
 
 int pnp_sync(pnp_ctx *ctx) {

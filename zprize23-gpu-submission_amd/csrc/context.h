@@ -28,6 +28,8 @@ struct pnp_ctx {
     std::map<std::string, pnp::DevBuf> work;
     uint64_t *buf(const std::string &name, size_t elems_fr);
 
+    pnp::KernelTimer ktimer;
+
     // ---- stage timing of the last proof ----
     std::vector<std::pair<std::string, double>> stages;
 };

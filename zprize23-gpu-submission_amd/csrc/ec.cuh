@@ -10,12 +10,18 @@
 #pragma once
 #include "field.cuh"
 
-// Point operations are out-of-line on the device: each one is ~10-18 Fq
-// products (~10-16k instructions); inlining them into unrolled callers made
-// compile times explode without a measurable speed benefit.
-#define PNP_EC static __host__ __device__ __noinline__
+// Point operations are force-inlined: out-of-line versions pass the 192-byte
+// XYZZ result through scratch (512-1184 B/lane of spills, 2 waves/SIMD).
+// Callers keep their loops rolled (#pragma unroll 1) so code size and
+// compile time stay bounded (each op is ~10-18 Fq products).
+#define PNP_EC static __host__ __device__ __forceinline__
 
 namespace pnp {
+
+#ifdef __HIP_DEVICE_COMPILE__
+// one definition per translation unit that includes ec.cuh
+__device__ __noinline__ Fq fq_mul_ool(Fq a, Fq b) { return a * b; }
+#endif
 
 struct Xyzz {
     Fq x, y, zz, zzz;
@@ -33,14 +39,14 @@ struct Xyzz {
 // 2 * (x, y) affine (mdbl-2008-s-1)
 PNP_EC Xyzz dbl_affine(const Fq &x, const Fq &y) {
     Fq u = dbl(y);
-    Fq v = sqr(u);
-    Fq w = u * v;
-    Fq s = x * v;
-    Fq x2 = sqr(x);
+    Fq v = fq_mul(u, u);
+    Fq w = fq_mul(u, v);
+    Fq s = fq_mul(x, v);
+    Fq x2 = fq_mul(x, x);
     Fq m = dbl(x2) + x2;
     Xyzz r;
-    r.x = sqr(m) - dbl(s);
-    r.y = m * (s - r.x) - w * y;
+    r.x = fq_mul(m, m) - dbl(s);
+    r.y = fq_mul(m, s - r.x) - fq_mul(w, y);
     r.zz = v;
     r.zzz = w;
     return r;
@@ -50,16 +56,16 @@ PNP_EC Xyzz dbl_affine(const Fq &x, const Fq &y) {
 PNP_EC Xyzz dbl(const Xyzz &p) {
     if (p.is_inf()) return p;
     Fq u = dbl(p.y);
-    Fq v = sqr(u);
-    Fq w = u * v;
-    Fq s = p.x * v;
-    Fq x2 = sqr(p.x);
+    Fq v = fq_mul(u, u);
+    Fq w = fq_mul(u, v);
+    Fq s = fq_mul(p.x, v);
+    Fq x2 = fq_mul(p.x, p.x);
     Fq m = dbl(x2) + x2;
     Xyzz r;
-    r.x = sqr(m) - dbl(s);
-    r.y = m * (s - r.x) - w * p.y;
-    r.zz = v * p.zz;
-    r.zzz = w * p.zzz;
+    r.x = fq_mul(m, m) - dbl(s);
+    r.y = fq_mul(m, s - r.x) - fq_mul(w, p.y);
+    r.zz = fq_mul(v, p.zz);
+    r.zzz = fq_mul(w, p.zzz);
     return r;
 }
 
@@ -73,22 +79,22 @@ PNP_EC Xyzz madd(const Xyzz &p, const Fq &x2, const Fq &y2) {
         r.zzz = Fq::one();
         return r;
     }
-    Fq u2 = x2 * p.zz;
-    Fq s2 = y2 * p.zzz;
+    Fq u2 = fq_mul(x2, p.zz);
+    Fq s2 = fq_mul(y2, p.zzz);
     Fq P = u2 - p.x;
     Fq R = s2 - p.y;
     if (P.is_zero()) {
         if (R.is_zero()) return dbl_affine(x2, y2);
         return Xyzz::inf();
     }
-    Fq pp = sqr(P);
-    Fq ppp = P * pp;
-    Fq q = p.x * pp;
+    Fq pp = fq_mul(P, P);
+    Fq ppp = fq_mul(P, pp);
+    Fq q = fq_mul(p.x, pp);
     Xyzz r;
-    r.x = sqr(R) - ppp - dbl(q);
-    r.y = R * (q - r.x) - p.y * ppp;
-    r.zz = p.zz * pp;
-    r.zzz = p.zzz * ppp;
+    r.x = fq_mul(R, R) - ppp - dbl(q);
+    r.y = fq_mul(R, q - r.x) - fq_mul(p.y, ppp);
+    r.zz = fq_mul(p.zz, pp);
+    r.zzz = fq_mul(p.zzz, ppp);
     return r;
 }
 
@@ -96,24 +102,24 @@ PNP_EC Xyzz madd(const Xyzz &p, const Fq &x2, const Fq &y2) {
 PNP_EC Xyzz add(const Xyzz &p, const Xyzz &q) {
     if (p.is_inf()) return q;
     if (q.is_inf()) return p;
-    Fq u1 = p.x * q.zz;
-    Fq u2 = q.x * p.zz;
-    Fq s1 = p.y * q.zzz;
-    Fq s2 = q.y * p.zzz;
+    Fq u1 = fq_mul(p.x, q.zz);
+    Fq u2 = fq_mul(q.x, p.zz);
+    Fq s1 = fq_mul(p.y, q.zzz);
+    Fq s2 = fq_mul(q.y, p.zzz);
     Fq P = u2 - u1;
     Fq R = s2 - s1;
     if (P.is_zero()) {
         if (R.is_zero()) return dbl(p);
         return Xyzz::inf();
     }
-    Fq pp = sqr(P);
-    Fq ppp = P * pp;
-    Fq qq = u1 * pp;
+    Fq pp = fq_mul(P, P);
+    Fq ppp = fq_mul(P, pp);
+    Fq qq = fq_mul(u1, pp);
     Xyzz r;
-    r.x = sqr(R) - ppp - dbl(qq);
-    r.y = R * (qq - r.x) - s1 * ppp;
-    r.zz = p.zz * q.zz * pp;
-    r.zzz = p.zzz * q.zzz * ppp;
+    r.x = fq_mul(R, R) - ppp - dbl(qq);
+    r.y = fq_mul(R, qq - r.x) - fq_mul(s1, ppp);
+    r.zz = fq_mul(fq_mul(p.zz, q.zz), pp);
+    r.zzz = fq_mul(fq_mul(p.zzz, q.zzz), ppp);
     return r;
 }
 

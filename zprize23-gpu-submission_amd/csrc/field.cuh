@@ -155,10 +155,74 @@ PNP_HD Fp<P> dbl(const Fp<P> &a) {
     return a + a;
 }
 
+#ifdef __HIP_DEVICE_COMPILE__
+// One limb product accumulated into a 96-bit column accumulator (acc2:acc):
+// v_mad_u64_u32 writes its 64-bit carry-out to VCC, v_addc_co_u32 folds it
+// into the third word.  Measured on gfx950: v_mad_u64_u32 is half rate, the
+// same as v_mul_lo_u32 or a 64-bit add, so two instructions per product is
+// the floor for 32-bit limbs.
+__device__ __forceinline__ void mac96(uint64_t &acc, uint32_t &acc2, uint32_t a, uint32_t b) {
+    asm("v_mad_u64_u32 %0, vcc, %2, %3, %0\n\tv_addc_co_u32 %1, vcc, 0, %1, vcc"
+        : "+v"(acc), "+v"(acc2)
+        : "v"(a), "v"(b)
+        : "vcc");
+}
+
+// a*b and m*p into the same column in one asm block (halves the hazard
+// s_nop the compiler places after every opaque asm statement)
+__device__ __forceinline__ void mac96x2(uint64_t &acc, uint32_t &acc2, uint32_t a, uint32_t b,
+                                        uint32_t m, uint32_t p) {
+    asm("v_mad_u64_u32 %0, vcc, %2, %3, %0\n\t"
+        "v_addc_co_u32 %1, vcc, 0, %1, vcc\n\t"
+        "v_mad_u64_u32 %0, vcc, %4, %5, %0\n\t"
+        "v_addc_co_u32 %1, vcc, 0, %1, vcc"
+        : "+v"(acc), "+v"(acc2)
+        : "v"(a), "v"(b), "v"(m), "s"(p)
+        : "vcc");
+}
+
+// Montgomery product by finely-integrated product scanning (FIPS): column k
+// of a*b and of m*p are summed into one 96-bit accumulator; m_k is chosen so
+// the low word of column k (k < N) vanishes; columns N..2N-1 are the result.
+// 2N^2 (mad + addc) + N mul_lo + ~3 movs per column, no CIOS temporaries.
+template <class P>
+__device__ __forceinline__ Fp<P> mont_mul_dev(const Fp<P> &a, const Fp<P> &b) {
+    constexpr int N = P::N;
+    uint32_t m[N];
+    Fp<P> r;
+    uint64_t acc = 0;
+    uint32_t acc2 = 0;
+#pragma unroll
+    for (int k = 0; k < N; k++) {
+#pragma unroll
+        for (int j = 0; j < k; j++) mac96x2(acc, acc2, a.v[j], b.v[k - j], m[j], P::P[k - j]);
+        mac96(acc, acc2, a.v[k], b.v[0]);
+        m[k] = (uint32_t)acc * P::INV;
+        mac96(acc, acc2, m[k], P::P[0]);
+        acc = (acc >> 32) | ((uint64_t)acc2 << 32);
+        acc2 = 0;
+    }
+#pragma unroll
+    for (int k = N; k < 2 * N; k++) {
+#pragma unroll
+        for (int j = k - N + 1; j < N; j++) mac96x2(acc, acc2, a.v[j], b.v[k - j], m[j], P::P[k - j]);
+        r.v[k - N] = (uint32_t)acc;
+        acc = (acc >> 32) | ((uint64_t)acc2 << 32);
+        acc2 = 0;
+    }
+    reduce_once(r);  // result < 2P < 2^(32N) for both moduli
+    return r;
+}
+#endif
+
 // Montgomery product, "no-carry" CIOS on 32-bit limbs (requires the top word
-// of P below 2^31 - 1, true for r and q).  2N^2 v_mad_u64_u32.
+// of P below 2^31 - 1, true for r and q).  2N^2 v_mad_u64_u32.  Host path;
+// the device uses mont_mul_dev above.
 template <class P>
 PNP_HD Fp<P> operator*(const Fp<P> &a, const Fp<P> &b) {
+#ifdef __HIP_DEVICE_COMPILE__
+    return mont_mul_dev(a, b);
+#endif
     constexpr int N = P::N;
     uint32_t t[N];
 #pragma unroll
@@ -187,6 +251,20 @@ PNP_HD Fp<P> operator*(const Fp<P> &a, const Fp<P> &b) {
 template <class P>
 PNP_HD Fp<P> sqr(const Fp<P> &a) {
     return a * a;
+}
+
+// Out-of-line Fq product for the EC formulas: one copy of the 288-mad body
+// per kernel instead of 10-18 inlined copies per point operation (inlining
+// all of them made LLVM's scheduler take 30-40 min per translation unit).
+#ifdef __HIP_DEVICE_COMPILE__
+__device__ __noinline__ Fq fq_mul_ool(Fq a, Fq b);
+#endif
+PNP_HD Fq fq_mul(const Fq &a, const Fq &b) {
+#if defined(__HIP_DEVICE_COMPILE__) && defined(PNP_FQ_OUTLINE)
+    return fq_mul_ool(a, b);
+#else
+    return a * b;
+#endif
 }
 
 template <class P>

@@ -269,9 +269,12 @@ void msm_run(MsmWork &wk, const uint64_t *d_points, const uint64_t *d_scalars, u
                        sorted);
     PNP_HIP(hipGetLastError());
     uint64_t *bk = wk.buckets.u64();
+    hipEvent_t ev0 = nullptr;
+    if (wk.timer) wk.timer->begin("msm_accumulate", s, ev0);
     hipLaunchKernelGGL(k_accumulate, dim3((uint32_t)((WB + 255) / 256)), dim3(256), 0, s, d_points,
                        sorted, counts, g.NB, g.nch, g.W, bk);
     PNP_HIP(hipGetLastError());
+    if (wk.timer) wk.timer->end("msm_accumulate", s, ev0);
     // running-sum tree: per window NB entries -> 1
     const uint64_t *inT = bk, *inS = bk;
     uint64_t *free_ptr = bk + WB * 24;
@@ -301,6 +304,7 @@ void msm_run(MsmWork &wk, const uint64_t *d_points, const uint64_t *d_scalars, u
     std::vector<uint64_t> win((size_t)g.W * 24);
     PNP_HIP(hipMemcpyAsync(win.data(), inT, win.size() * 8, hipMemcpyDeviceToHost, s));
     PNP_HIP(hipStreamSynchronize(s));
+    if (wk.timer) wk.timer->collect();
     Xyzz acc = Xyzz::inf();
     for (int w = g.W - 1; w >= 0; w--) {
         for (int k = 0; k < g.c; k++) acc = dbl(acc);

@@ -62,10 +62,23 @@ void ntt_run(NttTables &t, uint64_t *d, uint32_t lg, bool inverse, bool coset, h
 // out8[i] = i < n ? in[i] * g^i : 0, then forward NTT of size 8n (Ntt_coset::forward)
 void coset_lde8(NttTables &t, const uint64_t *in, uint64_t *out8, uint32_t lg_n, hipStream_t s);
 
+// ---- live per-kernel timing with HIP events on the launching stream ----
+struct KernelTimer {
+    bool enabled = false;
+    std::map<std::string, std::pair<double, int>> stats;  // name -> (total ms, launches)
+    std::vector<std::pair<std::string, std::pair<hipEvent_t, hipEvent_t>>> pending;
+    std::vector<hipEvent_t> pool;
+    hipEvent_t get();
+    void begin(const char *name, hipStream_t s, hipEvent_t &e0);
+    void end(const char *name, hipStream_t s, hipEvent_t e0);
+    void collect();  // call after the stream is synchronized
+};
+
 // ---- MSM (msm.hip) ----
 struct MsmWork {
     DevBuf digits, sorted, counts, offsets, buckets, seg, scal, result;
     size_t cap_n = 0;
+    KernelTimer *timer = nullptr;
 };
 // sum_i s_i P_i; scalars Montgomery Fr; result written to host as XYZZ Fq (4x6 u64)
 void msm_run(MsmWork &w, const uint64_t *d_points, const uint64_t *d_scalars_mont, uint64_t n,

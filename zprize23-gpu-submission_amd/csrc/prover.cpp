@@ -310,8 +310,12 @@ int prove_impl(pnp_ctx *ctx, const CircuitC *cs, int device_ptrs, ProofC *out) {
     q.sep3 = q.sep2 * lsep;
     tm.mark("r4_lde");
     uint64_t *t_poly = ctx->buf("t_poly", N8);
+    hipEvent_t qe0 = nullptr;
+    ctx->ktimer.begin("quotient", s, qe0);
     k_quotient(q, N8, t_poly, s);
+    ctx->ktimer.end("quotient", s, qe0);
     tm.mark("r4_quotient");
+    ctx->ktimer.collect();
     ntt_run(nt, t_poly, lg + 3, true, true, s);  // Intt_coset
     tm.mark("r4_intt8");
     CommitmentC *tcm[8] = {&out->t_1_comm, &out->t_2_comm, &out->t_3_comm, &out->t_4_comm,

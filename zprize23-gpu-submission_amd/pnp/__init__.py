@@ -27,6 +27,7 @@ ERRORS = {-1: "PNP_E_ARG", -2: "PNP_E_DEVICE", -3: "PNP_E_NOKEY", -4: "PNP_E_ENV
 # exported symbols declared by include/pnp_plonk.h (checked by tests/test_abi.py)
 SYMBOLS = ("gen_proof", "pnp_last_error", "pnp_ctx_create", "pnp_ctx_destroy",
            "pnp_load_prover_key", "pnp_load_commit_key", "pnp_prove", "pnp_last_stage_times",
+           "pnp_kernel_timing", "pnp_kernel_stats",
            "pnp_sync", "pnp_ntt", "pnp_coset_lde8", "pnp_commit", "pnp_poly_eval",
            "pnp_poly_div_linear", "pnp_prefix_product", "pnp_batch_inverse",
            "pnp_synth_random_fr", "pnp_synth_srs", "pnp_synth_coset_consts")
@@ -63,6 +64,8 @@ def load(path: str = LIB_PATH):
     lib.pnp_load_commit_key.argtypes = [vp, C.POINTER(abi.CommitKeyC), u64, i32]
     lib.pnp_prove.argtypes = [vp, C.POINTER(abi.CircuitC), i32, C.POINTER(abi.ProofC)]
     lib.pnp_last_stage_times.argtypes = [vp, C.POINTER(C.c_double), C.POINTER(C.c_char_p), i32]
+    lib.pnp_kernel_timing.argtypes = [vp, i32]
+    lib.pnp_kernel_stats.argtypes = [vp, C.c_char_p, C.POINTER(C.c_double), C.POINTER(C.c_int)]
     lib.pnp_sync.argtypes = [vp]
     lib.pnp_ntt.argtypes = [vp, vp, C.c_uint32, i32, i32]
     lib.pnp_coset_lde8.argtypes = [vp, vp, vp, C.c_uint32]
@@ -127,6 +130,15 @@ class Context:
         names = (C.c_char_p * cap)()
         k = self.lib.pnp_last_stage_times(self.h, ms, names, cap)
         return [(names[i].decode(), ms[i]) for i in range(min(k, cap))]
+
+    def kernel_timing(self, enable: bool):
+        check(self.lib.pnp_kernel_timing(self.h, int(enable)), "pnp_kernel_timing")
+
+    def kernel_stats(self, name: str):
+        ms, cnt = C.c_double(), C.c_int()
+        check(self.lib.pnp_kernel_stats(self.h, name.encode(), C.byref(ms), C.byref(cnt)),
+              "pnp_kernel_stats")
+        return ms.value, cnt.value
 
     # ---- operator API (HBM addresses as ints)
     def sync(self):
