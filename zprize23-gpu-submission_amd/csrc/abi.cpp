@@ -81,6 +81,18 @@ void KernelTimer::collect() {
     pending.clear();
 }
 
+void commit_affine_batch(pnp_ctx *ctx, const uint64_t *const *d_scalars, int B, uint64_t n,
+                         CommitmentC *const *out) {
+    std::vector<uint64_t> xyzz((size_t)B * 24);
+    msm_run_batch(ctx->msm, ctx->ck_dev, d_scalars, B, n, xyzz.data(), ctx->stream);
+    for (int b = 0; b < B; b++) {
+        uint64_t aff[12];
+        xyzz_to_affine_host(xyzz.data() + 24 * b, aff);
+        memcpy(out[b]->x, aff, 48);
+        memcpy(out[b]->y, aff + 6, 48);
+    }
+}
+
 }  // namespace pnp
 
 uint64_t *pnp_ctx::buf(const std::string &name, size_t elems_fr) {

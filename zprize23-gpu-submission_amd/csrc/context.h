@@ -36,5 +36,8 @@ struct pnp_ctx {
 
 namespace pnp {
 void commit_affine(pnp_ctx *ctx, const uint64_t *d_scalars, uint64_t n, CommitmentC *out);
+// B commitments over the resident SRS in one batched MSM
+void commit_affine_batch(pnp_ctx *ctx, const uint64_t *const *d_scalars, int B, uint64_t n,
+                         CommitmentC *const *out);
 int prove_impl(pnp_ctx *ctx, const CircuitC *cs, int device_ptrs, ProofC *out);
 }  // namespace pnp

@@ -222,35 +222,37 @@ __global__ __launch_bounds__(256) void k_reduce(const uint64_t *inT, const uint6
     store_xyzz(outS + 24 * t, run);
 }
 
-void msm_run(MsmWork &wk, const uint64_t *d_points, const uint64_t *d_scalars, uint64_t n,
-             uint64_t *h_xyzz, hipStream_t s) {
-    if (n == 0) {
+// B independent MSMs over the same n points: the B*W windows are treated as
+// one set of "virtual windows" so every stage runs once for the whole batch.
+void msm_run_batch(MsmWork &wk, const uint64_t *d_points, const uint64_t *const *d_scalars, int B,
+                   uint64_t n, uint64_t *h_xyzz, hipStream_t s) {
+    if (n == 0 || B == 0) {
         Xyzz r = Xyzz::inf();
-        for (int i = 0; i < 6; i++) {
-            h_xyzz[i] = 0;
+        for (int b = 0; b < B; b++) {
+            uint64_t *o = h_xyzz + 24 * b;
+            to_u64_limbs(r.x, o); to_u64_limbs(r.y, o + 6); to_u64_limbs(r.zz, o + 12);
+            to_u64_limbs(r.zzz, o + 18);
         }
-        uint64_t *o = h_xyzz;
-        to_u64_limbs(r.x, o); to_u64_limbs(r.y, o + 6); to_u64_limbs(r.zz, o + 12);
-        to_u64_limbs(r.zzz, o + 18);
         return;
     }
     MsmCfg g = msm_cfg(n);
-    const uint64_t WB = (uint64_t)g.W * g.NB;
-    // buffers (grown on demand, kept for later calls)
+    const int WW = g.W * B;  // virtual windows
+    const uint64_t WB = (uint64_t)WW * g.NB;
     auto need = [](DevBuf &b, size_t bytes) { if (b.bytes < bytes) b.alloc(bytes); };
-    need(wk.digits, (uint64_t)g.W * n * 2);
+    need(wk.digits, (uint64_t)WW * n * 2);
     need(wk.counts, (WB * g.nch + 1) * 4);
-    need(wk.sorted, (uint64_t)g.W * n * 4);
-    // bucket tree storage: leaves + levels (T and S)
-    need(wk.buckets, (WB + WB / 2 + 64 * (uint64_t)g.W) * 24 * 8);
+    need(wk.sorted, (uint64_t)WW * n * 4);
+    need(wk.buckets, (WB + WB / 2 + 64 * (uint64_t)WW) * 24 * 8);
     uint16_t *keys = static_cast<uint16_t *>(wk.digits.p);
     uint32_t *counts = static_cast<uint32_t *>(wk.counts.p);
     uint32_t *sorted = static_cast<uint32_t *>(wk.sorted.p);
 
-    hipLaunchKernelGGL(k_digits, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, s, d_scalars, n,
-                       g.c, g.W, keys);
-    PNP_HIP(hipGetLastError());
-    dim3 grid((uint32_t)g.nch, (uint32_t)g.W);
+    for (int b = 0; b < B; b++) {
+        hipLaunchKernelGGL(k_digits, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, s, d_scalars[b], n,
+                           g.c, g.W, keys + (uint64_t)b * g.W * n);
+        PNP_HIP(hipGetLastError());
+    }
+    dim3 grid((uint32_t)g.nch, (uint32_t)WW);
     size_t lds = (size_t)g.NB * 4;
     static bool attr_set = false;
     if (!attr_set) {
@@ -272,13 +274,13 @@ void msm_run(MsmWork &wk, const uint64_t *d_points, const uint64_t *d_scalars, u
     hipEvent_t ev0 = nullptr;
     if (wk.timer) wk.timer->begin("msm_accumulate", s, ev0);
     hipLaunchKernelGGL(k_accumulate, dim3((uint32_t)((WB + 255) / 256)), dim3(256), 0, s, d_points,
-                       sorted, counts, g.NB, g.nch, g.W, bk);
+                       sorted, counts, g.NB, g.nch, WW, bk);
     PNP_HIP(hipGetLastError());
     if (wk.timer) wk.timer->end("msm_accumulate", s, ev0);
-    // running-sum tree: per window NB entries -> 1
+    // running-sum tree: per virtual window NB entries -> 1
     const uint64_t *inT = bk, *inS = bk;
     uint64_t *free_ptr = bk + WB * 24;
-    uint64_t m = WB;  // entries at this level (all windows)
+    uint64_t m = WB;
     uint32_t lg_len = 0;
     uint64_t per_win = g.NB;
     while (per_win > 1) {
@@ -300,26 +302,34 @@ void msm_run(MsmWork &wk, const uint64_t *d_points, const uint64_t *d_scalars, u
         per_win /= G;
         lg_len += (G == 8 ? 3 : G == 4 ? 2 : 1);
     }
-    // inT now holds W window sums
-    std::vector<uint64_t> win((size_t)g.W * 24);
+    std::vector<uint64_t> win((size_t)WW * 24);
     PNP_HIP(hipMemcpyAsync(win.data(), inT, win.size() * 8, hipMemcpyDeviceToHost, s));
     PNP_HIP(hipStreamSynchronize(s));
     if (wk.timer) wk.timer->collect();
-    Xyzz acc = Xyzz::inf();
-    for (int w = g.W - 1; w >= 0; w--) {
-        for (int k = 0; k < g.c; k++) acc = dbl(acc);
-        const uint64_t *e = &win[(size_t)w * 24];
-        Xyzz ww;
-        ww.x = from_u64_limbs<FqP>(e);
-        ww.y = from_u64_limbs<FqP>(e + 6);
-        ww.zz = from_u64_limbs<FqP>(e + 12);
-        ww.zzz = from_u64_limbs<FqP>(e + 18);
-        acc = add(acc, ww);
+    for (int b = 0; b < B; b++) {
+        Xyzz acc = Xyzz::inf();
+        for (int w = g.W - 1; w >= 0; w--) {
+            for (int k = 0; k < g.c; k++) acc = dbl(acc);
+            const uint64_t *e = &win[((size_t)b * g.W + w) * 24];
+            Xyzz ww;
+            ww.x = from_u64_limbs<FqP>(e);
+            ww.y = from_u64_limbs<FqP>(e + 6);
+            ww.zz = from_u64_limbs<FqP>(e + 12);
+            ww.zzz = from_u64_limbs<FqP>(e + 18);
+            acc = add(acc, ww);
+        }
+        uint64_t *o = h_xyzz + 24 * b;
+        to_u64_limbs(acc.x, o);
+        to_u64_limbs(acc.y, o + 6);
+        to_u64_limbs(acc.zz, o + 12);
+        to_u64_limbs(acc.zzz, o + 18);
     }
-    to_u64_limbs(acc.x, h_xyzz);
-    to_u64_limbs(acc.y, h_xyzz + 6);
-    to_u64_limbs(acc.zz, h_xyzz + 12);
-    to_u64_limbs(acc.zzz, h_xyzz + 18);
+}
+
+void msm_run(MsmWork &wk, const uint64_t *d_points, const uint64_t *d_scalars, uint64_t n,
+             uint64_t *h_xyzz, hipStream_t s) {
+    const uint64_t *sc[1] = {d_scalars};
+    msm_run_batch(wk, d_points, sc, 1, n, h_xyzz, s);
 }
 
 void xyzz_to_affine_host(const uint64_t *xyzz, uint64_t *aff12) {

@@ -83,6 +83,8 @@ struct MsmWork {
 // sum_i s_i P_i; scalars Montgomery Fr; result written to host as XYZZ Fq (4x6 u64)
 void msm_run(MsmWork &w, const uint64_t *d_points, const uint64_t *d_scalars_mont, uint64_t n,
              uint64_t *h_xyzz, hipStream_t s);
+void msm_run_batch(MsmWork &w, const uint64_t *d_points, const uint64_t *const *d_scalars, int B,
+                   uint64_t n, uint64_t *h_xyzz, hipStream_t s);
 // host: XYZZ -> affine Montgomery (inf -> (0, one))
 void xyzz_to_affine_host(const uint64_t *xyzz, uint64_t *aff12);
 

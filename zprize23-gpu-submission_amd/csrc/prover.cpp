@@ -123,7 +123,10 @@ int prove_impl(pnp_ctx *ctx, const CircuitC *cs, int device_ptrs, ProofC *out) {
     }
     tm.mark("r1_intt");
     CommitmentC *wc[4] = {&out->a_comm, &out->b_comm, &out->c_comm, &out->d_comm};
-    for (int j = 0; j < 4; j++) commit_affine(ctx, wpoly[j], n, wc[j]);
+    {
+        const uint64_t *sc[4] = {wpoly[0], wpoly[1], wpoly[2], wpoly[3]};
+        commit_affine_batch(ctx, sc, 4, n, wc);
+    }
     append_comm(tr, "w_l", *wc[0]);
     append_comm(tr, "w_r", *wc[1]);
     append_comm(tr, "w_o", *wc[2]);
@@ -203,7 +206,8 @@ int prove_impl(pnp_ctx *ctx, const CircuitC *cs, int device_ptrs, ProofC *out) {
     k_prefix_product(num, n, ctx->scratch_a, s);
     PNP_HIP(hipMemcpyAsync(z2_poly, num, 32 * n, hipMemcpyDeviceToDevice, s));
     ntt_run(nt, z2_poly, lg, true, false, s);
-    commit_affine(ctx, z2_poly, n, &out->z_2_comm);  // not appended (gen_proof.cuh:200-205)
+    // z_2_comm is not appended to the transcript (gen_proof.cuh:200-205): its
+    // MSM is batched with the quotient chunks in round 4
     // public input poly (pi.cu:11-15)
     uint64_t *pi_poly = ctx->buf("pi_poly", n);
     PNP_HIP(hipMemsetAsync(pi_poly, 0, 32 * n, s));
@@ -320,7 +324,17 @@ int prove_impl(pnp_ctx *ctx, const CircuitC *cs, int device_ptrs, ProofC *out) {
     tm.mark("r4_intt8");
     CommitmentC *tcm[8] = {&out->t_1_comm, &out->t_2_comm, &out->t_3_comm, &out->t_4_comm,
                            &out->t_5_comm, &out->t_6_comm, &out->t_7_comm, &out->t_8_comm};
-    for (int k = 0; k < 8; k++) commit_affine(ctx, t_poly + 4 * (uint64_t)k * n, n, tcm[k]);
+    {
+        const uint64_t *sc[9];
+        CommitmentC *oc[9];
+        for (int k = 0; k < 8; k++) {
+            sc[k] = t_poly + 4 * (uint64_t)k * n;
+            oc[k] = tcm[k];
+        }
+        sc[8] = z2_poly;
+        oc[8] = &out->z_2_comm;
+        commit_affine_batch(ctx, sc, 9, n, oc);
+    }
     const char *tl[8] = {"t_1", "t_2", "t_3", "t_4", "t_5", "t_6", "t_7", "t_8"};
     for (int k = 0; k < 8; k++) append_comm(tr, tl[k], *tcm[k]);
     tm.mark("r4_commit");
@@ -465,9 +479,13 @@ int prove_impl(pnp_ctx *ctx, const CircuitC *cs, int device_ptrs, ProofC *out) {
     tr.append_scalar("d_next_eval", ld(cu->d_next_eval));
 
     // ---------------- round 6: openings (gen_proof.cuh:405-463, kzg10.cu:116-145)
-    uint64_t *comb = ctx->buf("comb", n);
+    // Both "aggregate_witness" challenges are squeezed back to back in the
+    // reference (nothing is appended in between), so both witness
+    // polynomials are built first and committed in one batched MSM.
+    uint64_t *comb = ctx->buf("comb", n), *comb2 = ctx->buf("comb2", n);
+    Fr aw = tr.challenge_scalar("aggregate_witness");
+    Fr saw = tr.challenge_scalar("aggregate_witness");
     {
-        Fr aw = tr.challenge_scalar("aggregate_witness");
         const uint64_t *awp[11] = {lin, pk.left_sigma_coeffs, pk.right_sigma_coeffs,
                                    pk.out_sigma_coeffs, f_poly, zero_n /* h2 */, table_poly,
                                    wpoly[0], wpoly[1], wpoly[2], wpoly[3]};
@@ -485,11 +503,8 @@ int prove_impl(pnp_ctx *ctx, const CircuitC *cs, int device_ptrs, ProofC *out) {
         }
         k_lincomb(oa, n, comb, s);
         k_poly_div_linear(comb, n, zc, ctx->scratch_a, s);
-        commit_affine(ctx, comb, n, &out->aw_opening);
     }
-    tm.mark("r6_aw");
     {
-        Fr saw = tr.challenge_scalar("aggregate_witness");
         const uint64_t *sawp[7] = {z_poly, wpoly[0], wpoly[1], wpoly[3], zero_n /* h1 */, z2_poly,
                                    table_poly};
         LinArgs oa;
@@ -504,11 +519,16 @@ int prove_impl(pnp_ctx *ctx, const CircuitC *cs, int device_ptrs, ProofC *out) {
             }
             p = p * saw;
         }
-        k_lincomb(oa, n, comb, s);
-        k_poly_div_linear(comb, n, zw, ctx->scratch_a, s);
-        commit_affine(ctx, comb, n, &out->saw_opening);
+        k_lincomb(oa, n, comb2, s);
+        k_poly_div_linear(comb2, n, zw, ctx->scratch_a, s);
     }
-    tm.mark("r6_saw");
+    tm.mark("r6_witness");
+    {
+        const uint64_t *sc[2] = {comb, comb2};
+        CommitmentC *oc[2] = {&out->aw_opening, &out->saw_opening};
+        commit_affine_batch(ctx, sc, 2, n, oc);
+    }
+    tm.mark("r6_commit");
     return PNP_OK;
 }
 
