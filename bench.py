@@ -3,11 +3,13 @@
 One step = one gen_proof of the HEIGHT=15 Poseidon-Merkle circuit shape
 (3,161,924 gates -> domain n = 2^22, quotient on the 8n = 2^25 coset) with the
 prover key, SRS and witness already resident in HBM (v2 API, pnp_prove with
-device pointers).  Inputs are synthetic (seeded, generated on the GPU): random
-witness wires, random arithmetic selectors / sigma polynomials whose 8n
-evaluations are their coset LDE, zero custom-gate selectors / lookup tables /
-q_lookup (the Merkle circuit's structure), real coset points and Z_H values,
-SRS = [tau^i] G.
+device pointers).  Inputs are synthetic (seeded, generated on the GPU by
+pnp_synth_circuit): a SATISFYING random arithmetic circuit of the same size
+(random a, d and selectors, copy cycles b_i = a_pi(i), c solved per gate), so
+the quotient has degree < 6n and t_7 = t_8 = 0 as in the real Merkle circuit;
+zero custom-gate selectors / lookup tables / q_lookup (the Merkle circuit's
+structure); prover-key evaluations = coset LDE of the coefficients; real coset
+points and Z_H values; SRS = [tau^i] G.
 
     python bench.py [--gpus N --steps K --warmup W]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
@@ -51,24 +53,40 @@ class Synthetic:
 
         def alloc(name, elems, limbs=4):
             t = torch.zeros((elems, limbs), dtype=torch.int64, device=dev)
+            torch.cuda.synchronize()  # the zero-fill runs on torch's stream, ours is separate
             keep[name] = t
             return t.data_ptr()
 
         s = seed * 1000
-        w = {}
-        for i, name in enumerate(("w_l", "w_r", "w_o", "w_4")):
-            w[name] = alloc(name, gates)
-            ctx.random_fr(w[name], gates, s + i)
+        # satisfying random arithmetic circuit (pnp_synth_circuit): random a, d
+        # and selectors, b_i = a_pi(i) copy cycles, c solved from each gate
+        w = {name: alloc(name, gates) for name in ("w_l", "w_r", "w_o", "w_4")}
+        ctx.random_fr(w["w_l"], gates, s + 1)
+        ctx.random_fr(w["w_4"], gates, s + 4)
         qlk = alloc("q_lookup", gates)
         self.pi = (C.c_uint64 * 4)(123456789 + seed, 0, 0, 0)
+        ev = {p: alloc(p + "_nevals", n) for p in self.POLYS}
+        sel_in = ("q_l", "q_r", "q_o", "q_4", "q_c", "q_hl", "q_hr", "q_h4")
+        for i, p in enumerate(sel_in):
+            ctx.random_fr(ev[p], n, s + 100 + i)
+        ctx.synth_circuit([w["w_l"], w["w_r"], w["w_o"], w["w_4"]],
+                          [ev[p] for p in sel_in] + [ev["q_arith"]],
+                          [ev[p] for p in ("left_sigma", "right_sigma", "out_sigma", "fourth_sigma")],
+                          n, gates, 7, list(self.pi))
         pk = abi.ProverKeyC()
-        for i, p in enumerate(self.POLYS):
+        for p in self.POLYS:
             c = alloc(p + "_coeffs", n)
             e = alloc(p + "_evals", N8)
-            ctx.random_fr(c, n, s + 100 + i)
-            ctx.coset_lde8(c, e, lg_n)
+            torch.cuda.synchronize()
+            ctx.sync()
+            keep[p + "_coeffs"].copy_(keep[p + "_nevals"])
+            torch.cuda.synchronize()
+            ctx.ntt(c, lg_n, inverse=True)        # coefficients of the n-domain evaluations
+            ctx.coset_lde8(c, e, lg_n)            # 8n coset evaluations (prover key form)
+            ctx.sync()
             setattr(pk, p + "_coeffs", abi.ptr(c))
             setattr(pk, p + "_evals", abi.ptr(e))
+            del keep[p + "_nevals"]
         zero8 = alloc("zero8", N8)
         zero_n = alloc("zero_n", n)
         empty = alloc("empty", 1)

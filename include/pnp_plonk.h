@@ -282,6 +282,14 @@ int pnp_batch_inverse(pnp_ctx *ctx, uint64_t *d_inout, uint64_t n);
 int pnp_synth_random_fr(pnp_ctx *ctx, uint64_t *d_out, uint64_t n, uint64_t seed);
 /* d_out[i] = tau^i * G1 generator, affine Montgomery (an SRS); tau Montgomery. */
 int pnp_synth_srs(pnp_ctx *ctx, uint64_t *d_out, uint64_t n, const uint64_t tau[4]);
+/* Satisfying random arithmetic circuit on the n-domain (tests/bench):
+ * in:  w[0] = a, w[3] = d (n_gates each), sel[0..7] = q_l q_r q_o q_4 q_c q_hl
+ *      q_hr q_h4 evaluations (n each, rows >= n_gates ignored);
+ * out: w[1] = b (b_i = a_pi(i)), w[2] = c (solved from the gate), sel[8] =
+ *      q_arith evaluations, sigma[0..3] evaluations (copy cycles b_i <-> a_pi(i)). */
+int pnp_synth_circuit(pnp_ctx *ctx, uint64_t *const w[4], uint64_t *const sel[9],
+                      uint64_t *const sigma[4], uint64_t n, uint64_t n_gates, uint64_t pi_pos,
+                      const uint64_t pi_canon[4]);
 /* d_out[i] = (g * w_8n^i)^n - 1 (v_h on the 8n coset) and the coset points. */
 int pnp_synth_coset_consts(pnp_ctx *ctx, uint64_t *d_vh, uint64_t *d_x, uint32_t lg_n);
 

@@ -137,25 +137,103 @@ PK_RANDOM_COEFFS = ("q_l", "q_r", "q_o", "q_4", "q_c", "q_hl", "q_hr", "q_h4", "
                     "left_sigma", "right_sigma", "out_sigma", "fourth_sigma")
 
 
-class Inputs:
-    """Host-resident synthetic gen_proof inputs + the ctypes structs over them."""
+def perm_mult(n_gates: int) -> int:
+    """Multiplier A of the row permutation pi(i) = (A*i + 1) mod n_gates."""
+    import math
+    A = 0x9E3779B1 % n_gates if n_gates > 2 else 1
+    while math.gcd(A, n_gates) != 1:
+        A += 1
+    return A
 
-    def __init__(self, lg_n: int, seed: int, n_gates: int | None = None, pi_pos: int = 3):
+
+def satisfying_witness(sel, a, d, n_gates, pi_pos, pi_mont, lg_n):
+    """Solve a satisfying witness / sigma for random arithmetic gates.
+
+    Gate row i (q_arith = 1 for i < n_gates, 0 on padding rows):
+        q_l a + q_r b + q_o c + q_4 d + q_hl a^5 + q_hr b^5 + q_h4 d^5 + q_c (+ PI_i) = 0
+    Copy constraints: b_i = a_pi(i), pi(i) = (A i + 1) mod n_gates, giving the
+    2-cycles {(b, i), (a, pi(i))}; c and d slots map to themselves.
+    All values are canonical ints; returns (b, c, sigma[4]) canonical ints.
+    Mirrored on the GPU by pnp_synth_circuit (csrc/synth.hip)."""
+    n = 1 << lg_n
+    w = fr_root(lg_n)
+    A = perm_mult(n_gates)
+    K = [1, 7, 13, 17]
+    b = [0] * n
+    c = [0] * n
+    sig = [[0] * n for _ in range(4)]
+    wp = [pow(w, i, R_MOD) for i in range(n)]
+    for i in range(n):
+        for j in range(4):
+            sig[j][i] = K[j] * wp[i] % R_MOD
+    for i in range(n_gates):
+        pi_i = (A * i + 1) % n_gates
+        b[i] = a[pi_i]
+        sig[1][i] = wp[pi_i]                      # (b, i) -> (a, pi(i))
+        sig[0][pi_i] = 7 * wp[i] % R_MOD          # (a, pi(i)) -> (b, i)
+        ql, qr, qo, q4, qc, qhl, qhr, qh4 = (sel[k][i] for k in
+                                             ("q_l", "q_r", "q_o", "q_4", "q_c", "q_hl", "q_hr", "q_h4"))
+        acc = (ql * a[i] + qr * b[i] + q4 * d[i] + qhl * pow(a[i], 5, R_MOD) + qhr * pow(b[i], 5, R_MOD)
+               + qh4 * pow(d[i], 5, R_MOD) + qc) % R_MOD
+        if i == pi_pos:
+            acc = (acc + fr_unmont(pi_mont)) % R_MOD
+        c[i] = (-acc) * pow(qo, -1, R_MOD) % R_MOD
+    return b, c, sig
+
+
+class Inputs:
+    """Host-resident synthetic gen_proof inputs + the ctypes structs over them.
+
+    satisfying=True (default): a satisfying random arithmetic circuit with copy
+    constraints (see satisfying_witness), so the quotient has degree < 6n and
+    t_7 = t_8 = 0 exactly as in the real Merkle circuit.  satisfying=False:
+    independent random witness / selectors / sigmas (still valid inputs)."""
+
+    def __init__(self, lg_n: int, seed: int, n_gates: int | None = None, pi_pos: int = 3,
+                 satisfying: bool = True):
         lib = oracle()
         rng = np.random.default_rng(seed)
         n = 1 << lg_n
         N8 = 8 * n
         self.lg_n, self.n = lg_n, n
         self.n_gates = n_gates if n_gates is not None else n - 3
+        self.pi_pos = pi_pos
         self.arrays = {}
         a = self.arrays
-        for w in ("w_l", "w_r", "w_o", "w_4"):
-            a[w] = rand_fr_mont_arr(rng, self.n_gates)
-        a["q_lookup"] = np.zeros((self.n_gates, 4), dtype=np.uint64)
+        ng = self.n_gates
         a["pi"] = np.array(to_limbs(int(rng.integers(1, 2**62)), 4), dtype=np.uint64)
-        self.pi_pos = pi_pos
+        a["q_lookup"] = np.zeros((ng, 4), dtype=np.uint64)
+
+        def rnd(cnt):
+            return [int(v) for v in (from_limbs(r) % R_MOD for r in
+                                     rng.integers(0, 2**64, size=(cnt, 4), dtype=np.uint64))]
+
+        def mont_arr(vals):
+            return ints_to_arr([fr_mont(v) for v in vals])
+
+        evals = {}
+        if satisfying:
+            sel = {k: rnd(ng) + [0] * (n - ng) for k in
+                   ("q_l", "q_r", "q_o", "q_4", "q_c", "q_hl", "q_hr", "q_h4")}
+            sel["q_arith"] = [1] * ng + [0] * (n - ng)
+            wa, wd = rnd(ng) + [0] * (n - ng), rnd(ng) + [0] * (n - ng)
+            pi_m = fr_mont(from_limbs(a["pi"]) % R_MOD)
+            wb, wc, sig = satisfying_witness(sel, wa, wd, ng, pi_pos, pi_m, lg_n)
+            for k, v in sel.items():
+                evals[k] = v
+            for j, name in enumerate(("left_sigma", "right_sigma", "out_sigma", "fourth_sigma")):
+                evals[name] = sig[j]
+            for name, vals in (("w_l", wa), ("w_r", wb), ("w_o", wc), ("w_4", wd)):
+                a[name] = mont_arr(vals[:ng])
+        else:
+            for name in ("w_l", "w_r", "w_o", "w_4"):
+                a[name] = mont_arr(rnd(ng))
         for name in PK_RANDOM_COEFFS:
-            c = rand_fr_mont_arr(rng, n)
+            if satisfying:
+                c = mont_arr(evals[name])
+                lib.or_ntt(vp(c), lg_n, 1, 0)  # coefficients of the n-domain evaluations
+            else:
+                c = rand_fr_mont_arr(rng, n)
             e = np.zeros((N8, 4), dtype=np.uint64)
             lib.or_coset_lde8(vp(c), vp(e), lg_n)
             a[name + "_coeffs"] = c

@@ -48,3 +48,77 @@ def test_gen_proof_v2_resident(tmp_path):
     names = [n for n, _ in ctx.stage_times()]
     assert "r4_quotient" in names
     ctx.close()
+
+
+def test_synth_circuit_matches_cpu_generator():
+    """pnp_synth_circuit (bench generator) == tests' satisfying_witness."""
+    import numpy as np
+    import pnp
+    from gpu_util import to_dev, from_dev, empty_dev
+    from pnp_testlib import (satisfying_witness, rand_fr_mont_arr, arr_to_ints, fr_unmont,
+                             fr_mont, ints_to_arr)
+    lg, ng, pos = 6, 50, 7
+    n = 1 << lg
+    rng = np.random.default_rng(11)
+    names = ("q_l", "q_r", "q_o", "q_4", "q_c", "q_hl", "q_hr", "q_h4")
+    sel_m = {k: rand_fr_mont_arr(rng, n) for k in names}
+    for k in names:
+        sel_m[k][ng:] = 0
+    a_m, d_m = rand_fr_mont_arr(rng, ng), rand_fr_mont_arr(rng, ng)
+    pi = [12345, 0, 0, 0]
+    ctx = pnp.Context(0)
+    w = [to_dev(a_m), empty_dev(ng), empty_dev(ng), to_dev(d_m)]
+    sel = [to_dev(sel_m[k]) for k in names] + [empty_dev(n)]
+    sig = [empty_dev(n) for _ in range(4)]
+    ctx.synth_circuit([t.data_ptr() for t in w], [t.data_ptr() for t in sel],
+                      [t.data_ptr() for t in sig], n, ng, pos, pi)
+    un = lambda arr: [fr_unmont(v) for v in arr_to_ints(arr)]
+    sel_c = {k: un(sel_m[k]) for k in names}
+    sel_c["q_arith"] = [1] * ng + [0] * (n - ng)
+    b, c, sg = satisfying_witness(sel_c, un(a_m) + [0] * (n - ng), un(d_m) + [0] * (n - ng),
+                                  ng, pos, fr_mont(12345), lg)
+    assert un(from_dev(w[1])) == b[:ng]
+    assert un(from_dev(w[2])) == c[:ng]
+    assert un(from_dev(sel[8])) == sel_c["q_arith"]
+    for j in range(4):
+        assert un(from_dev(sig[j])) == sg[j]
+    ctx.close()
+
+
+def test_gen_proof_parity_2e14():
+    """Larger parity point: satisfying circuit at n = 2^14 (8n = 2^17 coset)."""
+    import pnp
+    inp = Inputs(14, 21, n_gates=(1 << 14) - 1000, pi_pos=99)
+    exp = inp.oracle_proof()
+    got = pnp.load().gen_proof(inp.circuit, inp.pk, inp.ck)
+    assert _diff(got, exp) == []
+
+
+def test_full_size_height15_properties():
+    """BASELINE config 4 size (3,161,924 gates, n = 2^22): properties that hold
+    for any correct prover on a satisfying circuit: deg t < 6n so t_7 = t_8 =
+    infinity while t_1..t_6 are not; h1 = h2 = f = infinity; z2 commits to
+    [1, 0, ...] = G; proving is deterministic."""
+    import os
+    import sys
+    import pnp
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from bench import Synthetic, HEIGHT15_GATES
+    ctx = pnp.Context(0)
+    syn = Synthetic(ctx, 22, HEIGHT15_GATES, seed=5)
+    ctx.load_prover_key(syn.pk, syn.n, device_ptrs=True)
+    ctx.load_commit_key(syn.ck, syn.n, device_ptrs=True)
+    p1 = ctx.prove(syn.cs, device_ptrs=True)
+    p2 = ctx.prove(syn.cs, device_ptrs=True)
+    assert abi.proof_to_bytes(p1) == abi.proof_to_bytes(p2)
+    inf = lambda c: all(v == 0 for v in c.x)
+    assert inf(p1.t_7_comm) and inf(p1.t_8_comm)
+    assert not any(inf(getattr(p1, f"t_{k}_comm")) for k in range(1, 7))
+    assert inf(p1.h_1_comm) and inf(p1.h_2_comm) and inf(p1.f_comm)
+    assert not inf(p1.a_comm) and not inf(p1.z_comm) and not inf(p1.aw_opening)
+    # z2 = constant 1 polynomial -> commitment = powers_of_g[0] = G (tau^0 G)
+    import torch
+    g0 = syn.keep["srs"][0].cpu().numpy().view("uint64")
+    assert list(p1.z_2_comm.x) == [int(v) for v in g0[:6]]
+    assert list(p1.z_2_comm.y) == [int(v) for v in g0[6:]]
+    ctx.close()

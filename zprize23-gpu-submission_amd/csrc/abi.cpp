@@ -217,6 +217,15 @@ int pnp_synth_srs(pnp_ctx *ctx, uint64_t *d, uint64_t n, const uint64_t tau[4]) 
     PNP_TRY(k_srs(d, n, from_u64_limbs<FrP>(tau), ctx->stream));
 }
 
+int pnp_synth_circuit(pnp_ctx *ctx, uint64_t *const w[4], uint64_t *const sel[9],
+                      uint64_t *const sigma[4], uint64_t n, uint64_t n_gates, uint64_t pi_pos,
+                      const uint64_t pi_canon[4]) {
+    if (!ctx || !w || !sel || !sigma || !pi_canon || n_gates == 0 || n_gates > n || pi_pos >= n_gates)
+        return PNP_E_ARG;
+    PNP_TRY(k_synth_circuit(w, sel, sigma, n, n_gates, pi_pos, to_mont(from_u64_limbs<FrP>(pi_canon)),
+                            ctx->stream));
+}
+
 int pnp_synth_coset_consts(pnp_ctx *ctx, uint64_t *d_vh, uint64_t *d_x, uint32_t lg_n) {
     if (!ctx || lg_n > 25) return PNP_E_ARG;
     PNP_TRY(k_coset_consts(d_vh, d_x, lg_n, ctx->stream));

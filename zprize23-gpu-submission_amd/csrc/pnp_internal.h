@@ -102,5 +102,8 @@ void k_poly_div_linear(uint64_t *d, uint64_t n, const Fr &z, DevBuf &scratch, hi
 void k_random_fr(uint64_t *d, uint64_t n, uint64_t seed, hipStream_t s);
 void k_srs(uint64_t *d, uint64_t n, const Fr &tau, hipStream_t s);
 void k_coset_consts(uint64_t *vh, uint64_t *x, uint32_t lg_n, hipStream_t s);
+void k_synth_circuit(uint64_t *const w[4], uint64_t *const sel[9], uint64_t *const sigma[4],
+                     uint64_t n, uint64_t n_gates, uint64_t pi_pos, const Fr &pi_mont,
+                     hipStream_t s);
 
 }  // namespace pnp

@@ -325,15 +325,23 @@ int prove_impl(pnp_ctx *ctx, const CircuitC *cs, int device_ptrs, ProofC *out) {
     CommitmentC *tcm[8] = {&out->t_1_comm, &out->t_2_comm, &out->t_3_comm, &out->t_4_comm,
                            &out->t_5_comm, &out->t_6_comm, &out->t_7_comm, &out->t_8_comm};
     {
+        // chunks that are identically zero (t_7, t_8 for a satisfying circuit:
+        // deg t < 6n) commit to the point at infinity without an MSM
         const uint64_t *sc[9];
         CommitmentC *oc[9];
+        int nb = 0;
         for (int k = 0; k < 8; k++) {
-            sc[k] = t_poly + 4 * (uint64_t)k * n;
-            oc[k] = tcm[k];
+            const uint64_t *chunk = t_poly + 4 * (uint64_t)k * n;
+            if (!k_any_nonzero(chunk, 4 * n, ctx->scratch_b, s)) {
+                set_infinity(tcm[k]);
+                continue;
+            }
+            sc[nb] = chunk;
+            oc[nb++] = tcm[k];
         }
-        sc[8] = z2_poly;
-        oc[8] = &out->z_2_comm;
-        commit_affine_batch(ctx, sc, 9, n, oc);
+        sc[nb] = z2_poly;
+        oc[nb++] = &out->z_2_comm;
+        commit_affine_batch(ctx, sc, nb, n, oc);
     }
     const char *tl[8] = {"t_1", "t_2", "t_3", "t_4", "t_5", "t_6", "t_7", "t_8"};
     for (int k = 0; k < 8; k++) append_comm(tr, tl[k], *tcm[k]);

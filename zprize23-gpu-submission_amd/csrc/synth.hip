@@ -100,4 +100,62 @@ void k_coset_consts(uint64_t *vh, uint64_t *x, uint32_t lg_n, hipStream_t s) {
     PNP_HIP(hipStreamSynchronize(s));  // vh8 is freed on return
 }
 
+// Satisfying random arithmetic circuit (bench / tests; mirrors
+// tests/pnp_testlib.py satisfying_witness).  Row i < n_gates:
+//   q_l a + q_r b + q_o c + q_4 d + q_hl a^5 + q_hr b^5 + q_h4 d^5 + q_c (+PI) = 0,
+// b_i = a_pi(i) with pi(i) = (A i + 1) mod n_gates (2-cycles (b,i) <-> (a,pi(i))),
+// c solved from the gate, q_arith = 1; padding rows have q_arith = 0 and
+// identity sigma.  sigma_j(w^i) = k_j w^target (k = 1, 7, 13, 17).
+__global__ void k_synth_circuit_(const uint64_t *a, uint64_t *b, uint64_t *c, const uint64_t *d,
+                                 const uint64_t *ql, const uint64_t *qr, const uint64_t *qo,
+                                 const uint64_t *q4, const uint64_t *qc, const uint64_t *qhl,
+                                 const uint64_t *qhr, const uint64_t *qh4, uint64_t *qarith,
+                                 uint64_t *s0, uint64_t *s1, uint64_t *s2, uint64_t *s3, uint64_t n,
+                                 uint64_t ng, uint64_t A, uint64_t pi_pos, Fr pi, Fr omega, Fr k1,
+                                 Fr k2, Fr k3) {
+    uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    Fr wi = pow_u64(omega, i);
+    store_fr(s2, i, k2 * wi);
+    store_fr(s3, i, k3 * wi);
+    if (i >= ng) {
+        store_fr(s0, i, wi);
+        store_fr(s1, i, k1 * wi);
+        store_fr(qarith, i, Fr::zero());
+        return;
+    }
+    uint64_t pi_i = (uint64_t)(((unsigned __int128)A * i + 1) % ng);
+    Fr ai = load_fr(a, i), bi = load_fr(a, pi_i), di = load_fr(d, i);
+    store_fr(b, i, bi);
+    store_fr(s1, i, pow_u64(omega, pi_i));
+    store_fr(s0, pi_i, k1 * wi);
+    auto p5 = [](const Fr &x) { Fr x2 = x * x; return x2 * x2 * x; };
+    Fr acc = load_fr(ql, i) * ai + load_fr(qr, i) * bi + load_fr(q4, i) * di +
+             load_fr(qhl, i) * p5(ai) + load_fr(qhr, i) * p5(bi) + load_fr(qh4, i) * p5(di) +
+             load_fr(qc, i);
+    if (i == pi_pos) acc = acc + pi;
+    store_fr(c, i, neg(acc) * inverse(load_fr(qo, i)));
+    store_fr(qarith, i, Fr::one());
+}
+
+void k_synth_circuit(uint64_t *const w[4], uint64_t *const sel[9], uint64_t *const sigma[4],
+                     uint64_t n, uint64_t n_gates, uint64_t pi_pos, const Fr &pi_mont,
+                     hipStream_t s) {
+    uint64_t A = 0x9E3779B1ULL % n_gates;
+    if (n_gates <= 2) A = 1;
+    auto gcd = [](uint64_t x, uint64_t y) { while (y) { uint64_t t = x % y; x = y; y = t; } return x; };
+    while (gcd(A, n_gates) != 1) A++;
+    uint32_t lg = 0;
+    while ((1ULL << lg) < n) lg++;
+    const uint64_t root32[4] = {13381757501831005802ULL, 6564924994866501612ULL,
+                                789602057691799140ULL, 6625830629041353339ULL};
+    Fr omega = pow_u64(from_u64_limbs<FrP>(root32), 1ULL << (32 - lg));
+    auto fr_small = [](uint32_t v) { Fr r = Fr::zero(); r.v[0] = v; return to_mont(r); };
+    hipLaunchKernelGGL(k_synth_circuit_, dim3(nblk(n)), dim3(256), 0, s, w[0], w[1], w[2], w[3],
+                       sel[0], sel[1], sel[2], sel[3], sel[4], sel[5], sel[6], sel[7], sel[8],
+                       sigma[0], sigma[1], sigma[2], sigma[3], n, n_gates, A, pi_pos, pi_mont, omega,
+                       fr_small(7), fr_small(13), fr_small(17));
+    PNP_HIP(hipGetLastError());
+}
+
 }  // namespace pnp

@@ -30,7 +30,7 @@ SYMBOLS = ("gen_proof", "pnp_last_error", "pnp_ctx_create", "pnp_ctx_destroy",
            "pnp_kernel_timing", "pnp_kernel_stats",
            "pnp_sync", "pnp_ntt", "pnp_coset_lde8", "pnp_commit", "pnp_poly_eval",
            "pnp_poly_div_linear", "pnp_prefix_product", "pnp_batch_inverse",
-           "pnp_synth_random_fr", "pnp_synth_srs", "pnp_synth_coset_consts")
+           "pnp_synth_random_fr", "pnp_synth_srs", "pnp_synth_coset_consts", "pnp_synth_circuit")
 
 
 class PnpError(RuntimeError):
@@ -77,6 +77,8 @@ def load(path: str = LIB_PATH):
     lib.pnp_synth_random_fr.argtypes = [vp, vp, u64, u64]
     lib.pnp_synth_srs.argtypes = [vp, vp, u64, vp]
     lib.pnp_synth_coset_consts.argtypes = [vp, vp, vp, C.c_uint32]
+    lib.pnp_synth_circuit.argtypes = [vp, C.c_void_p * 4, C.c_void_p * 9, C.c_void_p * 4, u64, u64,
+                                      u64, vp]
     for name in SYMBOLS:
         if name.startswith("pnp_") and name not in ("pnp_last_error", "pnp_ctx_destroy"):
             getattr(lib, name).restype = C.c_int if name != "pnp_last_error" else C.c_char_p
@@ -178,6 +180,15 @@ class Context:
     def srs(self, addr: int, n: int, tau_limbs):
         t = (C.c_uint64 * 4)(*tau_limbs)
         check(self.lib.pnp_synth_srs(self.h, C.c_void_p(addr), n, t), "pnp_synth_srs")
+
+    def synth_circuit(self, w, sel, sigma, n: int, n_gates: int, pi_pos: int, pi_limbs):
+        """w: 4 addrs (a in, b out, c out, d in); sel: 9 addrs (8 in, q_arith out);
+        sigma: 4 addrs out (see include/pnp_plonk.h)."""
+        W = (C.c_void_p * 4)(*w)
+        S = (C.c_void_p * 9)(*sel)
+        G = (C.c_void_p * 4)(*sigma)
+        p = (C.c_uint64 * 4)(*pi_limbs)
+        check(self.lib.pnp_synth_circuit(self.h, W, S, G, n, n_gates, pi_pos, p), "pnp_synth_circuit")
 
     def coset_consts(self, vh: int, x: int, lg_n: int):
         check(self.lib.pnp_synth_coset_consts(self.h, C.c_void_p(vh), C.c_void_p(x), lg_n),
