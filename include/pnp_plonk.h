@@ -235,6 +235,24 @@ int pnp_last_stage_times(pnp_ctx *ctx, double *ms, const char **names, int cap);
  * last enable.  Used by bench.py for the roofline numbers. */
 int pnp_kernel_timing(pnp_ctx *ctx, int enable);
 int pnp_kernel_stats(pnp_ctx *ctx, const char *name, double *total_ms, int *launches);
+/* Algorithmic bytes the timed launches of `name` were credited with (sum over
+ * launches; e.g. msm_accumulate: points*(96 B point + 32 B scalar) of the
+ * windows it processed). */
+int pnp_kernel_bytes(pnp_ctx *ctx, const char *name, double *bytes);
+
+/* Multi-GPU: window-sharded MSM (one process per GPU, every rank runs
+ * pnp_prove on the same inputs).  Each MSM batch's virtual windows (c-bit
+ * windows x batched MSMs) are split into `world` contiguous slices of
+ * ceil(WW/world); rank r accumulates and reduces slice r only.  The library
+ * then writes its slice's window sums (XYZZ, 192 B each) to
+ * d_xbuf + r * bytes_per_rank, synchronizes its stream and calls
+ * allgather(user, bytes_per_rank), which must leave every rank's slice at its
+ * offset in d_xbuf on every rank (an in-place all-gather, e.g. RCCL) and
+ * return 0 once the data is visible to the device.  All other work is
+ * replicated, so every rank returns the same ProofC.  world = 1 disables. */
+typedef int (*pnp_allgather_fn)(void *user, uint64_t bytes_per_rank);
+int pnp_set_msm_shard(pnp_ctx *ctx, int rank, int world, pnp_allgather_fn allgather,
+                      void *user, uint64_t *d_xbuf, uint64_t xbuf_bytes);
 
 /* ------------------------------------------------------------------ */
 /* 3. Operator API on HBM pointers (mirrors PLONK/utils/function.cuh) */

@@ -187,10 +187,14 @@ class Inputs:
     satisfying=True (default): a satisfying random arithmetic circuit with copy
     constraints (see satisfying_witness), so the quotient has degree < 6n and
     t_7 = t_8 = 0 exactly as in the real Merkle circuit.  satisfying=False:
-    independent random witness / selectors / sigmas (still valid inputs)."""
+    independent random witness / selectors / sigmas (still valid inputs).
+    lookup_rows > 0: that many random gates get a non-zero q_lookup witness, so
+    the query table f is non-zero and z2 is a real grand product (the general
+    lookup branch); qm_qlookup_evals: random q_m / q_lookup 8n evaluations, so
+    the quotient's q_m and q_lookup terms are live."""
 
     def __init__(self, lg_n: int, seed: int, n_gates: int | None = None, pi_pos: int = 3,
-                 satisfying: bool = True):
+                 satisfying: bool = True, lookup_rows: int = 0, qm_qlookup_evals: bool = False):
         lib = oracle()
         rng = np.random.default_rng(seed)
         n = 1 << lg_n
@@ -240,6 +244,12 @@ class Inputs:
             a[name + "_evals"] = e
         for name in PK_ZERO_EVALS:
             a[name] = np.zeros((N8, 4), dtype=np.uint64)
+        if qm_qlookup_evals:
+            a["q_m_evals"] = rand_fr_mont_arr(rng, N8)
+            a["q_lookup_evals"] = rand_fr_mont_arr(rng, N8)
+        if lookup_rows:
+            rows = rng.choice(ng, size=min(lookup_rows, ng), replace=False)
+            a["q_lookup"][rows] = rand_fr_mont_arr(rng, len(rows))
         for t in ("table1", "table2", "table3", "table4"):
             a[t] = np.zeros((n, 4), dtype=np.uint64)
         # linear_evaluations = coset points g*w^i; v_h = (g w^i)^n - 1

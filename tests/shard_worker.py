@@ -1,0 +1,59 @@
+"""One rank of the multi-process sharding tests (tests/test_shard.py).
+
+    RANK=r WORLD_SIZE=N MASTER_ADDR=127.0.0.1 MASTER_PORT=p \
+        python shard_worker.py {cpu|gpu} OUT_PREFIX [lg seed]
+
+cpu: exercises pnp.shard.WindowExchange over gloo with host tensors.
+gpu: every rank proves the same seeded instance on cuda:0 with window-sharded
+     MSMs (gloo exchange through host memory, since the ranks share one GPU)
+     and writes its ProofC bytes to OUT_PREFIX.<rank>."""
+import os
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+sys.path.insert(0, os.path.join(os.path.dirname(HERE), "zprize23-gpu-submission_amd"))
+
+
+def main():
+    mode, out = sys.argv[1], sys.argv[2]
+    rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+    import torch
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from pnp.shard import WindowExchange
+    if mode == "cpu":
+        ex = WindowExchange(rank, world, capacity_bytes=1 << 14)
+        for w in (24, 24 * 7, 8):  # slot sizes in u64 words (window sums are 24 words)
+            ex.buf.zero_()
+            ex.buf[rank * w:(rank + 1) * w] = torch.arange(w) + 1000 * (rank + 1)
+            ex.gather(w * 8)
+            exp = torch.cat([torch.arange(w) + 1000 * (r + 1) for r in range(world)])
+            assert torch.equal(ex.buf[:w * world], exp), (w, ex.buf[:w * world])
+            assert int(ex.buf[w * world:].abs().sum()) == 0
+        cb = ex.c_callback()
+        assert cb(None, 24 * 8) == 0 and ex.calls == 4
+        assert cb(None, 1 << 20) == 1 and ex.error is not None  # oversize slot -> error code
+        with open(f"{out}.{rank}", "w") as f:
+            f.write("ok")
+    else:
+        lg, seed = int(sys.argv[3]), int(sys.argv[4])
+        import pnp
+        from pnp import abi
+        from pnp_testlib import Inputs
+        inp = Inputs(lg, seed)
+        ctx = pnp.Context(0)
+        ex = WindowExchange(rank, world, device="cuda")
+        ctx.set_msm_shard(ex)
+        ctx.load_prover_key(inp.pk, inp.n, device_ptrs=False)
+        ctx.load_commit_key(inp.ck, inp.n, device_ptrs=False)
+        proof = ctx.prove(inp.circuit, device_ptrs=False)
+        assert ex.calls > 0
+        with open(f"{out}.{rank}", "wb") as f:
+            f.write(abi.proof_to_bytes(proof))
+        ctx.close()
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

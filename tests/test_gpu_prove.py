@@ -35,6 +35,24 @@ def test_gen_proof_v1_parity(lg, seed):
     assert abi.proof_to_bytes(got) == abi.proof_to_bytes(exp)
 
 
+@pytest.mark.parametrize("lookup_rows,extra", [(0, True), (17, False), (40, True)])
+def test_gen_proof_general_lookup_and_selectors(lookup_rows, extra):
+    """Branches outside the lookup-trivial fast path: non-zero q_lookup witness
+    (f != 0, z2 a real grand product, z2 committed by MSM) and live q_m /
+    q_lookup quotient terms."""
+    import pnp
+    inp = Inputs(8, 30 + lookup_rows, lookup_rows=lookup_rows, qm_qlookup_evals=extra)
+    exp = inp.oracle_proof()
+    ctx = pnp.Context(0)
+    ctx.load_prover_key(inp.pk, inp.n, device_ptrs=False)
+    ctx.load_commit_key(inp.ck, inp.n, device_ptrs=False)
+    got = ctx.prove(inp.circuit, device_ptrs=False)
+    assert _diff(got, exp) == []
+    if lookup_rows:
+        assert any(v != 0 for v in exp.f_comm.x)
+    ctx.close()
+
+
 def test_gen_proof_v2_resident(tmp_path):
     import pnp
     inp = Inputs(10, 9, n_gates=1000, pi_pos=17)

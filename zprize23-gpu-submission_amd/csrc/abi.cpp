@@ -62,21 +62,22 @@ void KernelTimer::begin(const char *, hipStream_t s, hipEvent_t &e0) {
     e0 = get();
     PNP_HIP(hipEventRecord(e0, s));
 }
-void KernelTimer::end(const char *name, hipStream_t s, hipEvent_t e0) {
+void KernelTimer::end(const char *name, hipStream_t s, hipEvent_t e0, double bytes) {
     if (!enabled || !e0) return;
     hipEvent_t e1 = get();
     PNP_HIP(hipEventRecord(e1, s));
-    pending.push_back({name, {e0, e1}});
+    pending.push_back({name, e0, e1, bytes});
 }
 void KernelTimer::collect() {
     for (auto &p : pending) {
         float ms = 0;
-        PNP_HIP(hipEventElapsedTime(&ms, p.second.first, p.second.second));
-        auto &st = stats[p.first];
-        st.first += ms;
-        st.second += 1;
-        pool.push_back(p.second.first);
-        pool.push_back(p.second.second);
+        PNP_HIP(hipEventElapsedTime(&ms, p.e0, p.e1));
+        auto &st = stats[p.name];
+        st.ms += ms;
+        st.bytes += p.bytes;
+        st.launches += 1;
+        pool.push_back(p.e0);
+        pool.push_back(p.e1);
     }
     pending.clear();
 }
@@ -152,8 +153,28 @@ int pnp_kernel_timing(pnp_ctx *ctx, int enable) {
 int pnp_kernel_stats(pnp_ctx *ctx, const char *name, double *total_ms, int *launches) {
     if (!ctx || !name) return PNP_E_ARG;
     auto it = ctx->ktimer.stats.find(name);
-    if (total_ms) *total_ms = it == ctx->ktimer.stats.end() ? 0.0 : it->second.first;
-    if (launches) *launches = it == ctx->ktimer.stats.end() ? 0 : it->second.second;
+    if (total_ms) *total_ms = it == ctx->ktimer.stats.end() ? 0.0 : it->second.ms;
+    if (launches) *launches = it == ctx->ktimer.stats.end() ? 0 : it->second.launches;
+    return PNP_OK;
+}
+
+int pnp_kernel_bytes(pnp_ctx *ctx, const char *name, double *bytes) {
+    if (!ctx || !name || !bytes) return PNP_E_ARG;
+    auto it = ctx->ktimer.stats.find(name);
+    *bytes = it == ctx->ktimer.stats.end() ? 0.0 : it->second.bytes;
+    return PNP_OK;
+}
+
+int pnp_set_msm_shard(pnp_ctx *ctx, int rank, int world, pnp_allgather_fn allgather, void *user,
+                      uint64_t *d_xbuf, uint64_t xbuf_bytes) {
+    if (!ctx || world < 1 || rank < 0 || rank >= world) return PNP_E_ARG;
+    if (world > 1 && (!allgather || !d_xbuf)) return PNP_E_ARG;
+    ctx->msm.rank = world > 1 ? rank : 0;
+    ctx->msm.world = world;
+    ctx->msm.allgather = world > 1 ? allgather : nullptr;
+    ctx->msm.user = user;
+    ctx->msm.xbuf = world > 1 ? d_xbuf : nullptr;
+    ctx->msm.xbuf_bytes = world > 1 ? xbuf_bytes : 0;
     return PNP_OK;
 }
 
@@ -297,6 +318,23 @@ int pnp_load_prover_key(pnp_ctx *ctx, const ProverKeyC *pk, uint64_t D, int devi
                                        hipMemcpyHostToDevice, ctx->stream));
                 dst[f] = ctx->pk_owned.back().u64();
             }
+        }
+        // key-derived constants, computed once per key instead of per proof:
+        // zero-selector flags (the quotient kernel skips known-zero selectors)
+        // and the sigma n-domain evaluations (gen_proof.cuh:159-165 recomputes
+        // NTT.forward(sigma_coeffs) every proof)
+        ctx->pk_qm_zero = !pnp::k_any_nonzero(dev.q_m_evals, 4 * 8 * D, ctx->scratch_b, ctx->stream);
+        ctx->pk_qlookup_zero =
+            !pnp::k_any_nonzero(dev.q_lookup_evals, 4 * 8 * D, ctx->scratch_b, ctx->stream);
+        const uint64_t *sigc[4] = {dev.left_sigma_coeffs, dev.right_sigma_coeffs,
+                                   dev.out_sigma_coeffs, dev.fourth_sigma_coeffs};
+        uint32_t lg = 0;
+        while ((1ULL << lg) < D) lg++;
+        for (int j = 0; j < 4; j++) {
+            if (ctx->pk_sigma_n[j].bytes < 32 * D) ctx->pk_sigma_n[j].alloc(32 * D);
+            PNP_HIP(hipMemcpyAsync(ctx->pk_sigma_n[j].p, sigc[j], 32 * D, hipMemcpyDeviceToDevice,
+                                   ctx->stream));
+            pnp::ntt_run(ctx->ntt, ctx->pk_sigma_n[j].u64(), lg, false, false, ctx->stream);
         }
         PNP_HIP(hipStreamSynchronize(ctx->stream));
         ctx->pk_dev = dev;

@@ -18,6 +18,8 @@ struct pnp_ctx {
     uint64_t pk_n = 0;                     // domain size D
     std::vector<pnp::DevBuf> pk_owned;     // copies (device_ptrs == 0)
     ProverKeyC pk_dev{};                   // HBM pointers for every field
+    bool pk_qm_zero = false, pk_qlookup_zero = false;  // all-zero 8n selector evaluations
+    pnp::DevBuf pk_sigma_n[4];             // sigma evaluations on the n-domain
     // ---- resident commit key ----
     bool ck_loaded = false;
     uint64_t ck_points = 0;

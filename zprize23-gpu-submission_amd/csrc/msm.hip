@@ -21,6 +21,7 @@
 //   6. k_reduce     : window sums sum_b b*B_b by a running-sum tree:
 //                     groups of 8 entries merge as T' = sum T + len * sum t*S.
 //   7. host         : Horner over the windows (c doublings each) + affine.
+#include <algorithm>
 #include "pnp_internal.h"
 #include "ec.cuh"
 
@@ -236,75 +237,111 @@ void msm_run_batch(MsmWork &wk, const uint64_t *d_points, const uint64_t *const 
         return;
     }
     MsmCfg g = msm_cfg(n);
-    const int WW = g.W * B;  // virtual windows
-    const uint64_t WB = (uint64_t)WW * g.NB;
+    const int WW = g.W * B;  // virtual windows (c-bit windows x batched MSMs)
+    // window sharding: rank r owns virtual windows [v0, v0 + nown)
+    const int per = (WW + wk.world - 1) / wk.world;
+    const int v0 = std::min(wk.rank * per, WW);
+    const int nown = std::min(v0 + per, WW) - v0;
+    const uint64_t WB = (uint64_t)nown * g.NB;
     auto need = [](DevBuf &b, size_t bytes) { if (b.bytes < bytes) b.alloc(bytes); };
     need(wk.digits, (uint64_t)WW * n * 2);
     need(wk.counts, (WB * g.nch + 1) * 4);
-    need(wk.sorted, (uint64_t)WW * n * 4);
-    need(wk.buckets, (WB + WB / 2 + 64 * (uint64_t)WW) * 24 * 8);
+    need(wk.sorted, (uint64_t)nown * n * 4);
+    need(wk.buckets, (WB + WB / 2 + 64 * (uint64_t)nown) * 24 * 8);
     uint16_t *keys = static_cast<uint16_t *>(wk.digits.p);
     uint32_t *counts = static_cast<uint32_t *>(wk.counts.p);
     uint32_t *sorted = static_cast<uint32_t *>(wk.sorted.p);
 
-    for (int b = 0; b < B; b++) {
-        hipLaunchKernelGGL(k_digits, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, s, d_scalars[b], n,
-                           g.c, g.W, keys + (uint64_t)b * g.W * n);
-        PNP_HIP(hipGetLastError());
-    }
-    dim3 grid((uint32_t)g.nch, (uint32_t)WW);
-    size_t lds = (size_t)g.NB * 4;
-    static bool attr_set = false;
-    if (!attr_set) {
-        PNP_HIP(hipFuncSetAttribute((const void *)k_hist,
-                                    hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-        PNP_HIP(hipFuncSetAttribute((const void *)k_scatter,
-                                    hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-        attr_set = true;
-    }
-    hipLaunchKernelGGL(k_hist, grid, dim3(1024), lds, s, keys, n, g.NB, g.chunk, g.nch, counts);
-    PNP_HIP(hipGetLastError());
-    const uint64_t ncount = WB * g.nch;
-    PNP_HIP(hipMemsetAsync(counts + ncount, 0, 4, s));
-    scan_u32(counts, ncount + 1, wk.offsets, s);  // counts[ncount] = total
-    hipLaunchKernelGGL(k_scatter, grid, dim3(1024), lds, s, keys, n, g.NB, g.chunk, g.nch, counts,
-                       sorted);
-    PNP_HIP(hipGetLastError());
-    uint64_t *bk = wk.buckets.u64();
-    hipEvent_t ev0 = nullptr;
-    if (wk.timer) wk.timer->begin("msm_accumulate", s, ev0);
-    hipLaunchKernelGGL(k_accumulate, dim3((uint32_t)((WB + 255) / 256)), dim3(256), 0, s, d_points,
-                       sorted, counts, g.NB, g.nch, WW, bk);
-    PNP_HIP(hipGetLastError());
-    if (wk.timer) wk.timer->end("msm_accumulate", s, ev0);
-    // running-sum tree: per virtual window NB entries -> 1
-    const uint64_t *inT = bk, *inS = bk;
-    uint64_t *free_ptr = bk + WB * 24;
-    uint64_t m = WB;
-    uint32_t lg_len = 0;
-    uint64_t per_win = g.NB;
-    while (per_win > 1) {
-        int G = per_win >= 8 ? 8 : (int)per_win;
-        uint64_t nout = m / G;
-        uint64_t *oT = free_ptr, *oS = free_ptr + nout * 24;
-        free_ptr += 2 * nout * 24;
-        uint32_t blocks = (uint32_t)((nout + 255) / 256);
-        switch (G) {
-            case 8: hipLaunchKernelGGL(k_reduce<8>, dim3(blocks), dim3(256), 0, s, inT, inS, nout, lg_len, oT, oS); break;
-            case 4: hipLaunchKernelGGL(k_reduce<4>, dim3(blocks), dim3(256), 0, s, inT, inS, nout, lg_len, oT, oS); break;
-            case 2: hipLaunchKernelGGL(k_reduce<2>, dim3(blocks), dim3(256), 0, s, inT, inS, nout, lg_len, oT, oS); break;
-            default: set_error("msm reduce"); throw Error(PNP_E_ARG);
+    const uint64_t *inT = nullptr;
+    if (nown > 0) {
+        for (int b = 0; b < B; b++) {
+            if ((b + 1) * g.W <= v0 || b * g.W >= v0 + nown) continue;  // no owned window
+            hipLaunchKernelGGL(k_digits, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, s,
+                               d_scalars[b], n, g.c, g.W, keys + (uint64_t)b * g.W * n);
+            PNP_HIP(hipGetLastError());
         }
+        const uint16_t *own_keys = keys + (uint64_t)v0 * n;
+        dim3 grid((uint32_t)g.nch, (uint32_t)nown);
+        size_t lds = (size_t)g.NB * 4;
+        static bool attr_set = false;
+        if (!attr_set) {
+            PNP_HIP(hipFuncSetAttribute((const void *)k_hist,
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+            PNP_HIP(hipFuncSetAttribute((const void *)k_scatter,
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+            attr_set = true;
+        }
+        hipLaunchKernelGGL(k_hist, grid, dim3(1024), lds, s, own_keys, n, g.NB, g.chunk, g.nch,
+                           counts);
         PNP_HIP(hipGetLastError());
-        inT = oT;
-        inS = oS;
-        m = nout;
-        per_win /= G;
-        lg_len += (G == 8 ? 3 : G == 4 ? 2 : 1);
+        const uint64_t ncount = WB * g.nch;
+        PNP_HIP(hipMemsetAsync(counts + ncount, 0, 4, s));
+        scan_u32(counts, ncount + 1, wk.offsets, s);  // counts[ncount] = total
+        hipLaunchKernelGGL(k_scatter, grid, dim3(1024), lds, s, own_keys, n, g.NB, g.chunk, g.nch,
+                           counts, sorted);
+        PNP_HIP(hipGetLastError());
+        uint64_t *bk = wk.buckets.u64();
+        hipEvent_t ev0 = nullptr;
+        if (wk.timer) wk.timer->begin("msm_accumulate", s, ev0);
+        hipLaunchKernelGGL(k_accumulate, dim3((uint32_t)((WB + 255) / 256)), dim3(256), 0, s,
+                           d_points, sorted, counts, g.NB, g.nch, nown, bk);
+        PNP_HIP(hipGetLastError());
+        // algorithmic bytes: each point (96 B) and scalar (32 B)
+        // once per owned window-sweep
+        if (wk.timer)
+            wk.timer->end("msm_accumulate", s, ev0, (double)n * 128.0 * nown / g.W);
+        // running-sum tree: per virtual window NB entries -> 1
+        const uint64_t *inS = bk;
+        inT = bk;
+        uint64_t *free_ptr = bk + WB * 24;
+        uint64_t m = WB;
+        uint32_t lg_len = 0;
+        uint64_t per_win = g.NB;
+        while (per_win > 1) {
+            int G = per_win >= 8 ? 8 : (int)per_win;
+            uint64_t nout = m / G;
+            uint64_t *oT = free_ptr, *oS = free_ptr + nout * 24;
+            free_ptr += 2 * nout * 24;
+            uint32_t blocks = (uint32_t)((nout + 255) / 256);
+            switch (G) {
+                case 8: hipLaunchKernelGGL(k_reduce<8>, dim3(blocks), dim3(256), 0, s, inT, inS, nout, lg_len, oT, oS); break;
+                case 4: hipLaunchKernelGGL(k_reduce<4>, dim3(blocks), dim3(256), 0, s, inT, inS, nout, lg_len, oT, oS); break;
+                case 2: hipLaunchKernelGGL(k_reduce<2>, dim3(blocks), dim3(256), 0, s, inT, inS, nout, lg_len, oT, oS); break;
+                default: set_error("msm reduce"); throw Error(PNP_E_ARG);
+            }
+            PNP_HIP(hipGetLastError());
+            inT = oT;
+            inS = oS;
+            m = nout;
+            per_win /= G;
+            lg_len += (G == 8 ? 3 : G == 4 ? 2 : 1);
+        }
     }
     std::vector<uint64_t> win((size_t)WW * 24);
-    PNP_HIP(hipMemcpyAsync(win.data(), inT, win.size() * 8, hipMemcpyDeviceToHost, s));
-    PNP_HIP(hipStreamSynchronize(s));
+    if (wk.world == 1) {
+        PNP_HIP(hipMemcpyAsync(win.data(), inT, win.size() * 8, hipMemcpyDeviceToHost, s));
+        PNP_HIP(hipStreamSynchronize(s));
+    } else {
+        // slot r of xbuf = windows [r*per, r*per + per): the gathered buffer is
+        // window-indexed, so one copy brings all WW window sums to the host
+        const uint64_t slot = (uint64_t)per * 24 * 8;
+        if (wk.xbuf_bytes < slot * wk.world) {
+            set_error("msm shard: exchange buffer %llu B < %llu B",
+                      (unsigned long long)wk.xbuf_bytes, (unsigned long long)(slot * wk.world));
+            throw Error(PNP_E_ARG);
+        }
+        if (nown > 0)
+            PNP_HIP(hipMemcpyAsync(wk.xbuf + (uint64_t)v0 * 24, inT, (uint64_t)nown * 24 * 8,
+                                   hipMemcpyDeviceToDevice, s));
+        PNP_HIP(hipStreamSynchronize(s));
+        int rc = wk.allgather(wk.user, slot);
+        if (rc != 0) {
+            set_error("msm shard: all-gather callback failed (%d)", rc);
+            throw Error(PNP_E_DEVICE);
+        }
+        PNP_HIP(hipMemcpyAsync(win.data(), wk.xbuf, win.size() * 8, hipMemcpyDeviceToHost, s));
+        PNP_HIP(hipStreamSynchronize(s));
+    }
     if (wk.timer) wk.timer->collect();
     for (int b = 0; b < B; b++) {
         Xyzz acc = Xyzz::inf();

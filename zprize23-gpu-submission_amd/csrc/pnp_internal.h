@@ -65,12 +65,22 @@ void coset_lde8(NttTables &t, const uint64_t *in, uint64_t *out8, uint32_t lg_n,
 // ---- live per-kernel timing with HIP events on the launching stream ----
 struct KernelTimer {
     bool enabled = false;
-    std::map<std::string, std::pair<double, int>> stats;  // name -> (total ms, launches)
-    std::vector<std::pair<std::string, std::pair<hipEvent_t, hipEvent_t>>> pending;
+    struct Stat {
+        double ms = 0, bytes = 0;
+        int launches = 0;
+    };
+    struct Pending {
+        std::string name;
+        hipEvent_t e0, e1;
+        double bytes;
+    };
+    std::map<std::string, Stat> stats;
+    std::vector<Pending> pending;
     std::vector<hipEvent_t> pool;
     hipEvent_t get();
     void begin(const char *name, hipStream_t s, hipEvent_t &e0);
-    void end(const char *name, hipStream_t s, hipEvent_t e0);
+    // `bytes`: algorithmic bytes credited to this launch
+    void end(const char *name, hipStream_t s, hipEvent_t e0, double bytes = 0);
     void collect();  // call after the stream is synchronized
 };
 
@@ -79,6 +89,12 @@ struct MsmWork {
     DevBuf digits, sorted, counts, offsets, buckets, seg, scal, result;
     size_t cap_n = 0;
     KernelTimer *timer = nullptr;
+    // window sharding across ranks (pnp_set_msm_shard)
+    int rank = 0, world = 1;
+    pnp_allgather_fn allgather = nullptr;
+    void *user = nullptr;
+    uint64_t *xbuf = nullptr;
+    uint64_t xbuf_bytes = 0;
 };
 // sum_i s_i P_i; scalars Montgomery Fr; result written to host as XYZZ Fq (4x6 u64)
 void msm_run(MsmWork &w, const uint64_t *d_points, const uint64_t *d_scalars_mont, uint64_t n,
@@ -100,6 +116,8 @@ void k_poly_eval_multi(const uint64_t *const *polys, int npolys, uint64_t n, con
                        DevBuf &scratch, Fr *out, hipStream_t s);
 void k_poly_div_linear(uint64_t *d, uint64_t n, const Fr &z, DevBuf &scratch, hipStream_t s);
 void k_random_fr(uint64_t *d, uint64_t n, uint64_t seed, hipStream_t s);
+// d[i] = c0 * r^i
+void k_geometric(uint64_t *d, uint64_t n, const Fr &c0, const Fr &r, hipStream_t s);
 void k_srs(uint64_t *d, uint64_t n, const Fr &tau, hipStream_t s);
 void k_coset_consts(uint64_t *vh, uint64_t *x, uint32_t lg_n, hipStream_t s);
 void k_synth_circuit(uint64_t *const w[4], uint64_t *const sel[9], uint64_t *const sigma[4],

@@ -324,6 +324,28 @@ void k_poly_eval(const uint64_t *d, uint64_t n, const Fr &x, DevBuf &scratch, Fr
     k_poly_eval_multi(p, 1, n, x, scratch, out, s);
 }
 
+// ---------------------------------------------------------------- geometric fill
+// d[i] = c0 * r^i — coefficient form of a scaled Lagrange basis polynomial:
+// iNTT(v * e_pos)_j = v n^-1 w^(-pos j), so L1 / PI coefficients need no NTT
+__global__ void k_geometric_(uint64_t *d, uint64_t n, Fr c0, Fr r, uint32_t chunk) {
+    uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    uint64_t lo = t * chunk;
+    if (lo >= n) return;
+    uint64_t hi = lo + chunk < n ? lo + chunk : n;
+    Fr v = c0 * pow_u64(r, lo);
+    for (uint64_t i = lo; i < hi; i++) {
+        store_fr(d, i, v);
+        v = v * r;
+    }
+}
+void k_geometric(uint64_t *d, uint64_t n, const Fr &c0, const Fr &r, hipStream_t s) {
+    if (!n) return;
+    const uint32_t chunk = 16;
+    hipLaunchKernelGGL(k_geometric_, dim3(nblk((n + chunk - 1) / chunk)), dim3(256), 0, s, d, n, c0,
+                       r, chunk);
+    PNP_HIP(hipGetLastError());
+}
+
 // ---------------------------------------------------------------- synthetic inputs
 __device__ __forceinline__ uint64_t splitmix(uint64_t x) {
     x += 0x9e3779b97f4a7c15ULL;

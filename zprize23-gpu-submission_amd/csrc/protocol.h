@@ -22,11 +22,14 @@ struct PermArgs {
     Fr beta, gamma, omega;
 };
 
+// nullptr arrays are known-zero and not read, except z28: nullptr means the
+// lookup-trivial case z2 = 1 with f = t = h1 = h2 = 0, in which every z2 term of
+// the lookup quotient cancels exactly; q_m / q_lookup nullptr = zero selector.
 struct QuotArgs {
-    const uint64_t *w8[4], *z8, *pi8, *f8, *t8, *h18, *h28, *z28, *l1a8, *l18;
+    const uint64_t *w8[4], *z8, *pi8, *f8, *t8, *h18, *h28, *z28, *l18;
     const uint64_t *q_m, *q_l, *q_r, *q_o, *q_4, *q_c, *q_hl, *q_hr, *q_h4, *q_arith, *q_lookup;
     const uint64_t *sig[4], *lin, *vh_inv;
-    Fr alpha, beta, gamma, delta, eps, zeta, lsep;
+    Fr alpha, alpha2, beta, gamma, delta, eps, zeta, lsep;
     Fr bk[4], opd, eopd, sep2, sep3;
 };
 

@@ -169,8 +169,8 @@ __global__ __launch_bounds__(256) void k_quotient_(QuotArgs q, uint64_t N8, uint
     uint64_t nx = i + 8 < N8 ? i + 8 : i + 8 - N8;
     Fr a = load_fr(q.w8[0], i), b = load_fr(q.w8[1], i), c = load_fr(q.w8[2], i), d = load_fr(q.w8[3], i);
     // compute_quotient_i (widget/arithmetic.cu:7-45) + pi
-    Fr acc = a * b * load_fr(q.q_m, i);
-    acc += a * load_fr(q.q_l, i);
+    Fr acc = a * load_fr(q.q_l, i);
+    if (q.q_m) acc += a * b * load_fr(q.q_m, i);
     acc += b * load_fr(q.q_r, i);
     acc += c * load_fr(q.q_o, i);
     acc += d * load_fr(q.q_4, i);
@@ -188,20 +188,26 @@ __global__ __launch_bounds__(256) void k_quotient_(QuotArgs q, uint64_t N8, uint
     Fr pb = (load_fr(q.sig[0], i) * q.beta + a + q.gamma) * (load_fr(q.sig[1], i) * q.beta + b + q.gamma) *
             (load_fr(q.sig[2], i) * q.beta + c + q.gamma) * (load_fr(q.sig[3], i) * q.beta + d + q.gamma);
     pb = pb * zn * q.alpha;
-    num += pa - pb + (zi - Fr::one()) * load_fr(q.l1a8, i);
+    // L1 scaled by alpha^2 (quotient.cu:3-8 LDEs alpha^2 L1; linear, so fold it here)
+    num += pa - pb + (zi - Fr::one()) * (load_fr(q.l18, i) * q.alpha2);
     // _compute_quotient_i (widget/lookup.cu:3-134)
-    Fr f = ld(q.f8, i), tt = ld(q.t8, i), ttn = ld(q.t8, nx);
-    Fr h1 = ld(q.h18, i), h1n = ld(q.h18, nx), h2 = ld(q.h28, i);
-    Fr z2 = load_fr(q.z28, i), z2n = load_fr(q.z28, nx);
-    Fr ct = d;
-    ct = ct * q.zeta + c;
-    ct = ct * q.zeta + b;
-    ct = ct * q.zeta + a;
-    Fr lk = (ct - f) * ld(q.q_lookup, i) * q.lsep;
-    lk += z2 * q.opd * (f + q.eps) * (tt + q.eopd + ttn * q.delta) * q.sep2;
-    lk -= z2n * (h1 + q.eopd + h2 * q.delta) * (h2 + q.eopd + h1n * q.delta) * q.sep2;
-    lk += (z2 - Fr::one()) * (load_fr(q.l18, i) * q.sep3);
-    num += lk;
+    Fr f = ld(q.f8, i);
+    if (q.q_lookup) {
+        Fr ct = d;
+        ct = ct * q.zeta + c;
+        ct = ct * q.zeta + b;
+        ct = ct * q.zeta + a;
+        num += (ct - f) * load_fr(q.q_lookup, i) * q.lsep;
+    }
+    if (q.z28) {
+        Fr tt = ld(q.t8, i), ttn = ld(q.t8, nx);
+        Fr h1 = ld(q.h18, i), h1n = ld(q.h18, nx), h2 = ld(q.h28, i);
+        Fr z2 = load_fr(q.z28, i), z2n = load_fr(q.z28, nx);
+        Fr lk = z2 * q.opd * (f + q.eps) * (tt + q.eopd + ttn * q.delta) * q.sep2;
+        lk -= z2n * (h1 + q.eopd + h2 * q.delta) * (h2 + q.eopd + h1n * q.delta) * q.sep2;
+        lk += (z2 - Fr::one()) * (load_fr(q.l18, i) * q.sep3);
+        num += lk;
+    }
     store_fr(out, i, num * load_fr(q.vh_inv, i));
 }
 void k_quotient(const QuotArgs &q, uint64_t N8, uint64_t *out, hipStream_t s) {

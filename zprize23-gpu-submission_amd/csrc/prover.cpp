@@ -175,12 +175,10 @@ int prove_impl(pnp_ctx *ctx, const CircuitC *cs, int device_ptrs, ProofC *out) {
     PermArgs pa;
     const uint64_t *sigc[4] = {pk.left_sigma_coeffs, pk.right_sigma_coeffs, pk.out_sigma_coeffs,
                                pk.fourth_sigma_coeffs};
+    (void)sigc;
     for (int j = 0; j < 4; j++) {
-        uint64_t *sg = ctx->buf("sig" + std::to_string(j), n);
-        PNP_HIP(hipMemcpyAsync(sg, sigc[j], 32 * n, hipMemcpyDeviceToDevice, s));
-        ntt_run(nt, sg, lg, false, false, s);  // NTT.forward(sigma_polys[j])
         pa.w[j] = wsc[j];
-        pa.sigma[j] = sg;
+        pa.sigma[j] = ctx->pk_sigma_n[j].u64();  // NTT.forward(sigma_polys[j]), cached at key load
     }
     const uint64_t kv[4] = {1, 7, 13, 17};  // K1..K3 (permutation/constants.cu:3-15)
     for (int j = 0; j < 4; j++) pa.bk[j] = beta * fr_from_u64(kv[j]);
@@ -200,24 +198,34 @@ int prove_impl(pnp_ctx *ctx, const CircuitC *cs, int device_ptrs, ProofC *out) {
     append_comm(tr, "z", out->z_comm);
     // lookup grand product (permutation/mod.cu:111-144), h1 = h2 = 0
     uint64_t *z2_poly = ctx->buf("z2_poly", n);
-    k_lookup_nd(num, den, fc, tc, zero_n, zero_n, delta, eps, n, s);
-    k_batch_inverse(den, n, ctx->scratch_a, s);
-    k_mul_inplace(num, den, n, s);
-    k_prefix_product(num, n, ctx->scratch_a, s);
-    PNP_HIP(hipMemcpyAsync(z2_poly, num, 32 * n, hipMemcpyDeviceToDevice, s));
-    ntt_run(nt, z2_poly, lg, true, false, s);
+    // lookup-trivial case (f = t = h1 = h2 = 0): every ratio is
+    // (1+d) e (e(1+d)) / (e(1+d))^2 = 1, so z2 = 1 and its coefficients are [1, 0, ...]
+    const bool z2_one = f_zero && table_zero;
+    if (z2_one) {
+        uint64_t one[4];
+        to_u64_limbs(Fr::one(), one);
+        PNP_HIP(hipMemsetAsync(z2_poly, 0, 32 * n, s));
+        PNP_HIP(hipMemcpyAsync(z2_poly, one, 32, hipMemcpyHostToDevice, s));
+        PNP_HIP(hipStreamSynchronize(s));
+    } else {
+        k_lookup_nd(num, den, fc, tc, zero_n, zero_n, delta, eps, n, s);
+        k_batch_inverse(den, n, ctx->scratch_a, s);
+        k_mul_inplace(num, den, n, s);
+        k_prefix_product(num, n, ctx->scratch_a, s);
+        PNP_HIP(hipMemcpyAsync(z2_poly, num, 32 * n, hipMemcpyDeviceToDevice, s));
+        ntt_run(nt, z2_poly, lg, true, false, s);
+    }
     // z_2_comm is not appended to the transcript (gen_proof.cuh:200-205): its
     // MSM is batched with the quotient chunks in round 4
     // public input poly (pi.cu:11-15)
+    // = iNTT of the evaluations v * e_pos, in closed form: v n^-1 w^(-pos j)
     uint64_t *pi_poly = ctx->buf("pi_poly", n);
-    PNP_HIP(hipMemsetAsync(pi_poly, 0, 32 * n, s));
+    const Fr n_inv = inverse(fr_from_u64(n));
     {
-        uint64_t piv[4];
-        to_u64_limbs(to_mont(from_u64_limbs<FrP>(cs->pi)), piv);
-        PNP_HIP(hipMemcpyAsync(pi_poly + 4 * cs->intended_pi_pos, piv, 32, hipMemcpyHostToDevice, s));
-        PNP_HIP(hipStreamSynchronize(s));
+        Fr v = to_mont(from_u64_limbs<FrP>(cs->pi));
+        Fr w_inv_pos = pow_u64(inverse(root_of_unity(lg)), cs->intended_pi_pos);
+        k_geometric(pi_poly, n, v * n_inv, w_inv_pos, s);
     }
-    ntt_run(nt, pi_poly, lg, true, false, s);
     tm.mark("r3_z2_pi");
 
     // ---------------- round 4: quotient (gen_proof.cuh:209-267, quotient.cu:142-376)
@@ -243,10 +251,13 @@ int prove_impl(pnp_ctx *ctx, const CircuitC *cs, int device_ptrs, ProofC *out) {
     uint64_t *z8 = ctx->buf("z8", N8), *pi8 = ctx->buf("pi8", N8), *z28 = ctx->buf("z28", N8);
     coset_lde8(nt, z_poly, z8, lg, s);
     coset_lde8(nt, pi_poly, pi8, lg, s);
-    coset_lde8(nt, z2_poly, z28, lg, s);
     q.z8 = z8;
     q.pi8 = pi8;
-    q.z28 = z28;
+    q.z28 = nullptr;  // z2 = 1: its quotient terms cancel (protocol.h)
+    if (!z2_one) {
+        coset_lde8(nt, z2_poly, z28, lg, s);
+        q.z28 = z28;
+    }
     q.f8 = q.t8 = nullptr;
     if (!f_zero) {
         uint64_t *f8 = ctx->buf("f8", N8);
@@ -259,28 +270,15 @@ int prove_impl(pnp_ctx *ctx, const CircuitC *cs, int device_ptrs, ProofC *out) {
         q.t8 = t8;
     }
     q.h18 = q.h28 = nullptr;  // h1 = h2 = 0
-    // compute_first_lagrange_poly_scaled(n, alpha^2) and (n, 1) (quotient.cu:3-8)
+    // compute_first_lagrange_poly_scaled(n, alpha^2) and (n, 1) (quotient.cu:3-8):
+    // one LDE of L1 (coefficients n^-1, no iNTT); alpha^2 is applied in the kernel
     Fr alpha2 = alpha * alpha;
-    uint64_t *l1a = ctx->buf("l1a", n), *l1 = ctx->buf("l1", n);
-    uint64_t *l1a8 = ctx->buf("l1a8", N8), *l18 = ctx->buf("l18", N8);
-    {
-        uint64_t v[4];
-        PNP_HIP(hipMemsetAsync(l1a, 0, 32 * n, s));
-        PNP_HIP(hipMemsetAsync(l1, 0, 32 * n, s));
-        to_u64_limbs(alpha2, v);
-        PNP_HIP(hipMemcpyAsync(l1a, v, 32, hipMemcpyHostToDevice, s));
-        PNP_HIP(hipStreamSynchronize(s));
-        to_u64_limbs(Fr::one(), v);
-        PNP_HIP(hipMemcpyAsync(l1, v, 32, hipMemcpyHostToDevice, s));
-        PNP_HIP(hipStreamSynchronize(s));
-    }
-    ntt_run(nt, l1a, lg, true, false, s);
-    ntt_run(nt, l1, lg, true, false, s);
-    coset_lde8(nt, l1a, l1a8, lg, s);
+    uint64_t *l1 = ctx->buf("l1", n), *l18 = ctx->buf("l18", N8);
+    k_geometric(l1, n, n_inv, Fr::one(), s);
     coset_lde8(nt, l1, l18, lg, s);
-    q.l1a8 = l1a8;
     q.l18 = l18;
-    q.q_m = pk.q_m_evals;
+    q.alpha2 = alpha2;
+    q.q_m = ctx->pk_qm_zero ? nullptr : pk.q_m_evals;
     q.q_l = pk.q_l_evals;
     q.q_r = pk.q_r_evals;
     q.q_o = pk.q_o_evals;
@@ -290,7 +288,7 @@ int prove_impl(pnp_ctx *ctx, const CircuitC *cs, int device_ptrs, ProofC *out) {
     q.q_hr = pk.q_hr_evals;
     q.q_h4 = pk.q_h4_evals;
     q.q_arith = pk.q_arith_evals;
-    q.q_lookup = pk.q_lookup_evals;
+    q.q_lookup = ctx->pk_qlookup_zero ? nullptr : pk.q_lookup_evals;
     q.sig[0] = pk.left_sigma_evals;
     q.sig[1] = pk.right_sigma_evals;
     q.sig[2] = pk.out_sigma_evals;
@@ -317,7 +315,17 @@ int prove_impl(pnp_ctx *ctx, const CircuitC *cs, int device_ptrs, ProofC *out) {
     hipEvent_t qe0 = nullptr;
     ctx->ktimer.begin("quotient", s, qe0);
     k_quotient(q, N8, t_poly, s);
-    ctx->ktimer.end("quotient", s, qe0);
+    {
+        // algorithmic bytes: every coset array the kernel reads (nullptr = known
+        // zero, not read) plus t, 32 B per point each
+        const uint64_t *arrs[] = {q.w8[0], q.w8[1], q.w8[2], q.w8[3], q.q_m, q.q_l, q.q_r, q.q_o,
+                                  q.q_4, q.q_c, q.q_hl, q.q_hr, q.q_h4, q.q_arith, q.pi8, q.lin,
+                                  q.z8, q.sig[0], q.sig[1], q.sig[2], q.sig[3], q.f8,
+                                  q.t8, q.h18, q.h28, q.q_lookup, q.z28, q.l18, q.vh_inv};
+        int nread = 0;
+        for (const uint64_t *a : arrs) nread += a != nullptr;
+        ctx->ktimer.end("quotient", s, qe0, 32.0 * (double)N8 * (nread + 1));
+    }
     tm.mark("r4_quotient");
     ctx->ktimer.collect();
     ntt_run(nt, t_poly, lg + 3, true, true, s);  // Intt_coset
@@ -339,8 +347,17 @@ int prove_impl(pnp_ctx *ctx, const CircuitC *cs, int device_ptrs, ProofC *out) {
             sc[nb] = chunk;
             oc[nb++] = tcm[k];
         }
-        sc[nb] = z2_poly;
-        oc[nb++] = &out->z_2_comm;
+        if (z2_one) {
+            // commit([1, 0, ...]) = 1 * powers_of_g[0], already affine
+            uint64_t g0[12];
+            PNP_HIP(hipMemcpyAsync(g0, ctx->ck_dev, sizeof g0, hipMemcpyDeviceToHost, s));
+            PNP_HIP(hipStreamSynchronize(s));
+            memcpy(out->z_2_comm.x, g0, 48);
+            memcpy(out->z_2_comm.y, g0 + 6, 48);
+        } else {
+            sc[nb] = z2_poly;
+            oc[nb++] = &out->z_2_comm;
+        }
         commit_affine_batch(ctx, sc, nb, n, oc);
     }
     const char *tl[8] = {"t_1", "t_2", "t_3", "t_4", "t_5", "t_6", "t_7", "t_8"};
@@ -370,8 +387,8 @@ int prove_impl(pnp_ctx *ctx, const CircuitC *cs, int device_ptrs, ProofC *out) {
         const uint64_t *pw[4] = {z_poly, wpoly[0], wpoly[1], wpoly[3]};
         Fr rw[4];
         k_poly_eval_multi(pw, 4, n, zw, ctx->scratch_a, rw, s);
-        Fr z2n;
-        k_poly_eval(z2_poly, n, zw, ctx->scratch_a, &z2n, s);
+        Fr z2n = Fr::one();
+        if (!z2_one) k_poly_eval(z2_poly, n, zw, ctx->scratch_a, &z2n, s);
         Fr f_eval = Fr::zero(), t_eval = Fr::zero(), t_next = Fr::zero();
         if (!f_zero) k_poly_eval(f_poly, n, zc, ctx->scratch_a, &f_eval, s);
         if (!table_zero) {

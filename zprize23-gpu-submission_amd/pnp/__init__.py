@@ -27,10 +27,14 @@ ERRORS = {-1: "PNP_E_ARG", -2: "PNP_E_DEVICE", -3: "PNP_E_NOKEY", -4: "PNP_E_ENV
 # exported symbols declared by include/pnp_plonk.h (checked by tests/test_abi.py)
 SYMBOLS = ("gen_proof", "pnp_last_error", "pnp_ctx_create", "pnp_ctx_destroy",
            "pnp_load_prover_key", "pnp_load_commit_key", "pnp_prove", "pnp_last_stage_times",
-           "pnp_kernel_timing", "pnp_kernel_stats",
+           "pnp_kernel_timing", "pnp_kernel_stats", "pnp_kernel_bytes", "pnp_set_msm_shard",
            "pnp_sync", "pnp_ntt", "pnp_coset_lde8", "pnp_commit", "pnp_poly_eval",
            "pnp_poly_div_linear", "pnp_prefix_product", "pnp_batch_inverse",
            "pnp_synth_random_fr", "pnp_synth_srs", "pnp_synth_coset_consts", "pnp_synth_circuit")
+
+
+# int allgather(void *user, uint64_t bytes_per_rank) — pnp_set_msm_shard
+ALLGATHER_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_uint64)
 
 
 class PnpError(RuntimeError):
@@ -66,6 +70,8 @@ def load(path: str = LIB_PATH):
     lib.pnp_last_stage_times.argtypes = [vp, C.POINTER(C.c_double), C.POINTER(C.c_char_p), i32]
     lib.pnp_kernel_timing.argtypes = [vp, i32]
     lib.pnp_kernel_stats.argtypes = [vp, C.c_char_p, C.POINTER(C.c_double), C.POINTER(C.c_int)]
+    lib.pnp_kernel_bytes.argtypes = [vp, C.c_char_p, C.POINTER(C.c_double)]
+    lib.pnp_set_msm_shard.argtypes = [vp, i32, i32, ALLGATHER_FN, vp, vp, u64]
     lib.pnp_sync.argtypes = [vp]
     lib.pnp_ntt.argtypes = [vp, vp, C.c_uint32, i32, i32]
     lib.pnp_coset_lde8.argtypes = [vp, vp, vp, C.c_uint32]
@@ -135,6 +141,25 @@ class Context:
 
     def kernel_timing(self, enable: bool):
         check(self.lib.pnp_kernel_timing(self.h, int(enable)), "pnp_kernel_timing")
+
+    def kernel_bytes(self, name: str) -> float:
+        b = C.c_double()
+        check(self.lib.pnp_kernel_bytes(self.h, name.encode(), C.byref(b)), "pnp_kernel_bytes")
+        return b.value
+
+    def set_msm_shard(self, exchange):
+        """Window-sharded MSM across ranks (pnp_set_msm_shard); `exchange` is a
+        pnp.shard.WindowExchange, or None to go back to single-GPU MSMs."""
+        if exchange is None or exchange.world == 1:
+            check(self.lib.pnp_set_msm_shard(self.h, 0, 1, ALLGATHER_FN(), None, None, 0),
+                  "pnp_set_msm_shard")
+            self._exchange = None
+            return
+        cb = exchange.c_callback()
+        check(self.lib.pnp_set_msm_shard(self.h, exchange.rank, exchange.world, cb, None,
+                                         exchange.buf.data_ptr(), exchange.buf.numel() * 8),
+              "pnp_set_msm_shard")
+        self._exchange = (exchange, cb)  # keep the callback alive
 
     def kernel_stats(self, name: str):
         ms, cnt = C.c_double(), C.c_int()
