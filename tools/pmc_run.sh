@@ -1,0 +1,16 @@
+#!/bin/bash
+# PMC passes over one bench proof (one counter group per run, no tracing
+# domains): FETCH_SIZE, WRITE_SIZE, SQ issue/wait breakdown.  Run on the GPU
+# box from the repo root:  bash tools/pmc_run.sh <tag>
+set -e
+R=$(pwd)
+TAG=${1:-pmc}
+RX='k_accumulate|k_dif_pass|k_quotient|k_scatter|k_reduce|k_bitrev_tiles|k_hist'
+cd /tmp && export TMPDIR=/tmp
+i=0
+for P in "FETCH_SIZE" "WRITE_SIZE" "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVES"; do
+  i=$((i+1))
+  timeout -k 10 300 rocprofv3 --pmc $P --kernel-include-regex "$RX" -f csv \
+      -d $R/gpurun_out/$TAG/p$i -o run -- python3 $R/bench.py --steps 1 --warmup 0 --cpu-lg 0 \
+      > $R/gpurun_out/$TAG/p$i.log 2>&1
+done

@@ -185,11 +185,38 @@ __device__ __forceinline__ void mac96x2(uint64_t &acc, uint32_t &acc2, uint32_t 
 // of a*b and of m*p are summed into one 96-bit accumulator; m_k is chosen so
 // the low word of column k (k < N) vanishes; columns N..2N-1 are the result.
 // 2N^2 (mad + addc) + N mul_lo + ~3 movs per column, no CIOS temporaries.
+//   PNP_MONT_VARIANT 0 : one asm statement per product pair (compiler pads
+//                        each statement with an s_nop)
+//   PNP_MONT_VARIANT 1 : the whole product as one asm block, one chain
+//   PNP_MONT_VARIANT 2 : one block, a*b and m*p on two independent chains
+#ifndef PNP_MONT_VARIANT
+#define PNP_MONT_VARIANT 0
+#endif
+#include "mont_asm.inc"
 template <class P>
 __device__ __forceinline__ Fp<P> mont_mul_dev(const Fp<P> &a, const Fp<P> &b) {
     constexpr int N = P::N;
-    uint32_t m[N];
     Fp<P> r;
+#if PNP_MONT_VARIANT == 1 || PNP_MONT_VARIANT == 2
+    uint32_t p[N];
+#pragma unroll
+    for (int i = 0; i < N; i++) p[i] = P::P[i];
+    if constexpr (N == 12) {
+#if PNP_MONT_VARIANT == 1
+        mont_asm12_single(r.v, a.v, b.v, p, P::INV);
+#else
+        mont_asm12_dual(r.v, a.v, b.v, p, P::INV);
+#endif
+    } else {
+        static_assert(N == 8 && P::INV == 0xffffffffu, "Fr expected");
+#if PNP_MONT_VARIANT == 1
+        mont_asm8_single(r.v, a.v, b.v, p);
+#else
+        mont_asm8_dual(r.v, a.v, b.v, p);
+#endif
+    }
+#else
+    uint32_t m[N];
     uint64_t acc = 0;
     uint32_t acc2 = 0;
 #pragma unroll
@@ -210,6 +237,7 @@ __device__ __forceinline__ Fp<P> mont_mul_dev(const Fp<P> &a, const Fp<P> &b) {
         acc = (acc >> 32) | ((uint64_t)acc2 << 32);
         acc2 = 0;
     }
+#endif
     reduce_once(r);  // result < 2P < 2^(32N) for both moduli
     return r;
 }

@@ -193,6 +193,78 @@ __global__ __launch_bounds__(256) void k_accumulate(const uint64_t *points, cons
     store_xyzz(buckets + 24 * t, acc);
 }
 
+// 5'. balanced accumulate: thread t sums exactly the sorted entries
+// [t*S, t*S + S) whatever the bucket boundaries, so every lane of a wave does
+// the same number of mixed additions (one lane per bucket waits for the
+// longest of 64 Poisson-sized runs: ~83% lane efficiency at n/NB = 128).  A
+// bucket lying inside one thread's range is written straight to `buckets`;
+// otherwise its first piece goes to tail[t0] and the pieces of the following
+// threads to head[t], and k_bucket_merge adds them up.
+__device__ __forceinline__ uint32_t bucket_start(const uint32_t *offs, uint64_t u, int nch) {
+    return offs[u * nch];
+}
+__global__ __launch_bounds__(256) void k_accumulate_flat(const uint64_t *points,
+                                                         const uint32_t *sorted,
+                                                         const uint32_t *offs, int nch, uint64_t U,
+                                                         uint32_t S, uint64_t *buckets,
+                                                         uint64_t *head, uint64_t *tail) {
+    uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    const uint32_t total = bucket_start(offs, U, nch);
+    const uint64_t lo64 = t * S;
+    if (lo64 >= total) return;
+    const uint32_t lo = (uint32_t)lo64;
+    const uint32_t hi = lo + S < total ? lo + S : total;
+    // largest u with start(u) <= lo: the (non-empty) bucket containing lo
+    uint64_t a = 0, b = U;  // invariant: start(a) <= lo < start(b)
+    while (b - a > 1) {
+        uint64_t m = (a + b) >> 1;
+        if (bucket_start(offs, m, nch) <= lo) a = m; else b = m;
+    }
+    uint64_t cur = a;
+    bool first = bucket_start(offs, cur, nch) < lo;  // piece continues a bucket begun earlier
+    uint32_t next = bucket_start(offs, cur + 1, nch);
+    Xyzz acc = Xyzz::inf();
+    for (uint32_t k = lo; k < hi; k++) {
+        if (k == next) {  // bucket boundary: emit the finished piece
+            if (first) store_xyzz(head + 24 * t, acc);
+            else store_xyzz(buckets + 24 * cur, acc);
+            first = false;
+            acc = Xyzz::inf();
+            do {  // skip empty buckets
+                cur++;
+                next = bucket_start(offs, cur + 1, nch);
+            } while (next == k);
+        }
+        uint32_t e = sorted[k];
+        const uint64_t *p = points + 12ULL * (e & 0x7FFFFFFFu);
+        Fq x = load_fq(p), y = load_fq(p + 6);
+        if (e >> 31) y = neg(y);
+        acc = madd(acc, x, y);
+    }
+    if (first) store_xyzz(head + 24 * t, acc);
+    else if (next > hi) store_xyzz(tail + 24 * t, acc);
+    else store_xyzz(buckets + 24 * cur, acc);
+}
+
+// bucket u = tail[t0] + head[t0+1] + ... + head[t1] when its entries span
+// threads t0 < t1; empty buckets become infinity
+__global__ __launch_bounds__(256) void k_bucket_merge(const uint32_t *offs, int nch, uint64_t U,
+                                                      uint32_t S, const uint64_t *head,
+                                                      const uint64_t *tail, uint64_t *buckets) {
+    uint64_t u = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    if (u >= U) return;
+    uint32_t s = bucket_start(offs, u, nch), e = bucket_start(offs, u + 1, nch);
+    if (s == e) {
+        store_xyzz(buckets + 24 * u, Xyzz::inf());
+        return;
+    }
+    uint32_t t0 = s / S, t1 = (e - 1) / S;
+    if (t0 == t1) return;
+    Xyzz acc = load_xyzz(tail + 24ULL * t0);
+    for (uint32_t t = t0 + 1; t <= t1; t++) acc = add(acc, load_xyzz(head + 24ULL * t));
+    store_xyzz(buckets + 24 * u, acc);
+}
+
 // ---------------------------------------------------------------- 6. reduce
 // Entry e of a level stands for a contiguous bucket range of length `len`
 // (power of two): T_e = sum_r (r+1) B_r over the range, S_e = sum_r B_r.
@@ -283,8 +355,16 @@ void msm_run_batch(MsmWork &wk, const uint64_t *d_points, const uint64_t *const 
         uint64_t *bk = wk.buckets.u64();
         hipEvent_t ev0 = nullptr;
         if (wk.timer) wk.timer->begin("msm_accumulate", s, ev0);
-        hipLaunchKernelGGL(k_accumulate, dim3((uint32_t)((WB + 255) / 256)), dim3(256), 0, s,
-                           d_points, sorted, counts, g.NB, g.nch, nown, bk);
+        // balanced accumulate: S entries per thread (upper bound nown*n entries)
+        const uint32_t S = 64;
+        const uint64_t nthr = ((uint64_t)nown * n + S - 1) / S;
+        need(wk.seg, nthr * 2 * 24 * 8);
+        uint64_t *head = wk.seg.u64(), *tail = head + nthr * 24;
+        hipLaunchKernelGGL(k_accumulate_flat, dim3((uint32_t)((nthr + 255) / 256)), dim3(256), 0,
+                           s, d_points, sorted, counts, g.nch, WB, S, bk, head, tail);
+        PNP_HIP(hipGetLastError());
+        hipLaunchKernelGGL(k_bucket_merge, dim3((uint32_t)((WB + 255) / 256)), dim3(256), 0, s,
+                           counts, g.nch, WB, S, head, tail, bk);
         PNP_HIP(hipGetLastError());
         // algorithmic bytes: each point (96 B) and scalar (32 B)
         // once per owned window-sweep
