@@ -276,6 +276,12 @@ int pnp_coset_lde8(pnp_ctx *ctx, const uint64_t *d_coeffs, uint64_t *d_out8, uin
 int pnp_commit(pnp_ctx *ctx, const uint64_t *d_points, const uint64_t *d_scalars,
                uint64_t n, CommitmentC *out);
 
+/* KZG commit (kzg10.cu:31-55) against the RESIDENT commit key
+ * (pnp_load_commit_key): sum_{i<n} s_i powers_of_g[i], as gen_proof's
+ * commitments.  Uses the folded fixed-base layout (2^(c k) multiples of the
+ * first n SRS points, built on the first call for this n and kept).  */
+int pnp_commit_ck(pnp_ctx *ctx, const uint64_t *d_scalars, uint64_t n, CommitmentC *out);
+
 /* evaluate (function.cu:162-173): sum_i c_i x^i; x and result Montgomery,
  * host-side scalars.  Synchronous. */
 int pnp_poly_eval(pnp_ctx *ctx, const uint64_t *d_coeffs, uint64_t n,

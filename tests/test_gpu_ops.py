@@ -67,12 +67,24 @@ def _commit_dev(ctx, pts, sc_mont):
     return np.array(list(c.x) + list(c.y), dtype=np.uint64)
 
 
+def _commit_ck(ctx, pts, sc_mont):
+    """Commitment through the resident commit key: the folded fixed-base
+    layout gen_proof uses (table of 2^(c k) multiples built on first use)."""
+    from pnp import abi
+    dp, ds = to_dev(pts), to_dev(sc_mont)
+    ck = abi.CommitKeyC(powers_of_g=abi.ptr(dp.data_ptr()), powers_of_gamma_g=abi.ptr(dp.data_ptr()))
+    ctx.load_commit_key(ck, len(pts), device_ptrs=True)
+    c = ctx.commit_ck(ds.data_ptr(), len(pts))
+    return np.array(list(c.x) + list(c.y), dtype=np.uint64)
+
+
 @pytest.mark.parametrize("n", [1, 2, 3, 17, 64, 257, 1024])
 def test_msm_golden(ctx, n):
     pts = GOLD[f"msm{n}_points"]
     sc = GOLD[f"msm{n}_scalars"].copy()
     oracle().or_fr_vec_to_mont(vp(sc), n)
     assert (_commit_dev(ctx, pts, sc) == GOLD[f"msm{n}_result"]).all()
+    assert (_commit_ck(ctx, pts, sc) == GOLD[f"msm{n}_result"]).all()
 
 
 @pytest.mark.parametrize("n", [5000, 1 << 14, 1 << 16])
@@ -87,6 +99,7 @@ def test_msm_vs_oracle(ctx, n):
     exp = np.zeros(12, dtype=np.uint64)
     lib.or_commit(vp(pts), vp(sc), n, vp(exp))
     assert (_commit_dev(ctx, pts, sc) == exp).all()
+    assert (_commit_ck(ctx, pts, sc) == exp).all()
 
 
 def test_msm_edge_cases(ctx):
@@ -116,6 +129,7 @@ def test_msm_edge_cases(ctx):
         exp = np.zeros(12, dtype=np.uint64)
         lib.or_commit(vp(pts), vp(sc), n, vp(exp))
         assert (_commit_dev(ctx, pts, sc) == exp).all(), name
+        assert (_commit_ck(ctx, pts, sc) == exp).all(), name
 
 
 @pytest.mark.parametrize("n", [1, 31, 32, 33, 1000, 1 << 16])

@@ -39,9 +39,18 @@ void DevBuf::release() {
     bytes = 0;
 }
 
+const uint64_t *commit_table(pnp_ctx *ctx, uint64_t n) {
+    if (ctx->ck_table_n != n) {
+        ctx->ck_table_n = 0;
+        msm_build_table(ctx->ck_table, ctx->ck_dev, n, ctx->stream);
+        ctx->ck_table_n = n;
+    }
+    return ctx->ck_table.u64();
+}
+
 void commit_affine(pnp_ctx *ctx, const uint64_t *d_scalars, uint64_t n, CommitmentC *out) {
     uint64_t xyzz[24], aff[12];
-    msm_run(ctx->msm, ctx->ck_dev, d_scalars, n, xyzz, ctx->stream);
+    msm_run(ctx->msm, ctx->ck_dev, d_scalars, n, xyzz, ctx->stream, commit_table(ctx, n));
     xyzz_to_affine_host(xyzz, aff);
     memcpy(out->x, aff, 48);
     memcpy(out->y, aff + 6, 48);
@@ -85,7 +94,8 @@ void KernelTimer::collect() {
 void commit_affine_batch(pnp_ctx *ctx, const uint64_t *const *d_scalars, int B, uint64_t n,
                          CommitmentC *const *out) {
     std::vector<uint64_t> xyzz((size_t)B * 24);
-    msm_run_batch(ctx->msm, ctx->ck_dev, d_scalars, B, n, xyzz.data(), ctx->stream);
+    msm_run_batch(ctx->msm, ctx->ck_dev, d_scalars, B, n, xyzz.data(), ctx->stream,
+                  commit_table(ctx, n));
     for (int b = 0; b < B; b++) {
         uint64_t aff[12];
         xyzz_to_affine_host(xyzz.data() + 24 * b, aff);
@@ -202,6 +212,20 @@ int pnp_commit(pnp_ctx *ctx, const uint64_t *d_points, const uint64_t *d_scalars
         memcpy(out->x, aff, 48);
         memcpy(out->y, aff + 6, 48);
     });
+}
+
+int pnp_commit_ck(pnp_ctx *ctx, const uint64_t *d_scalars, uint64_t n, CommitmentC *out) {
+    if (!ctx || !out || (n && !d_scalars)) return PNP_E_ARG;
+    if (!ctx->ck_loaded) {
+        set_error("commit key not loaded");
+        return PNP_E_NOKEY;
+    }
+    if (n > ctx->ck_points) {
+        set_error("commit key has %llu points, need %llu", (unsigned long long)ctx->ck_points,
+                  (unsigned long long)n);
+        return PNP_E_ARG;
+    }
+    PNP_TRY(commit_affine(ctx, d_scalars, n, out));
 }
 
 int pnp_poly_eval(pnp_ctx *ctx, const uint64_t *d, uint64_t n, const uint64_t x[4], uint64_t out[4]) {
@@ -359,6 +383,8 @@ int pnp_load_commit_key(pnp_ctx *ctx, const CommitKeyC *ck, uint64_t n_points, i
             ctx->ck_dev = ctx->ck_owned.u64();
         }
         ctx->ck_points = n_points;
+        ctx->ck_table_n = 0;  // rebuilt from the new key on the next commitment
+        ctx->ck_table.release();
         ctx->ck_loaded = true;
     });
 }

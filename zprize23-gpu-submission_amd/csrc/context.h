@@ -25,6 +25,10 @@ struct pnp_ctx {
     uint64_t ck_points = 0;
     pnp::DevBuf ck_owned;
     const uint64_t *ck_dev = nullptr;
+    // folded MSM table of the first ck_table_n SRS points (msm_build_table),
+    // built on the first commitment of that size
+    pnp::DevBuf ck_table;
+    uint64_t ck_table_n = 0;
 
     // ---- per-proof working set (sized on first use, reused) ----
     std::map<std::string, pnp::DevBuf> work;
@@ -37,6 +41,8 @@ struct pnp_ctx {
 };
 
 namespace pnp {
+// commitments over the resident SRS (folded MSM)
+const uint64_t *commit_table(pnp_ctx *ctx, uint64_t n);
 void commit_affine(pnp_ctx *ctx, const uint64_t *d_scalars, uint64_t n, CommitmentC *out);
 // B commitments over the resident SRS in one batched MSM
 void commit_affine_batch(pnp_ctx *ctx, const uint64_t *const *d_scalars, int B, uint64_t n,

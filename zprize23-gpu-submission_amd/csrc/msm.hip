@@ -6,43 +6,38 @@
 // and n scalars (here Montgomery in, canonicalised on the device, as
 // to_base in PLONK/src/arithmetic.cu:3-8).
 //
+// Two layouts of the same pipeline:
+//   * per-window (arbitrary points, pnp_commit): every c-bit window of every
+//     MSM owns NB = 2^(c-1) buckets; window sums meet in a host Horner step.
+//   * folded (the resident SRS, every gen_proof commitment): the commit key is
+//     expanded once into a table T[k*n + i] = 2^(c*k) P_i (W*n affine points,
+//     6 GiB at n = 2^22 — HBM is 288 GB), so digit k of scalar i is a signed
+//     multiple of T[k*n + i] and ALL windows of an MSM share one set of NB
+//     buckets.  Same number of mixed additions, but the bucket reduction is W
+//     times smaller and the result needs no doublings on the host.
+//
 // MI355X design (no cooperative kernels, no CPU bucket fold):
-//   1. k_digits     : signed c-bit digits, |d| <= 2^(c-1), one u16 key per
-//                     (window, point) — key = (|d|-1) | sign<<15, 0xFFFF = 0.
-//   2. k_hist       : one workgroup per (window, chunk of points) builds the
-//                     chunk's bucket histogram in LDS (2^(c-1) u32 <= 128 KiB)
-//                     and stores it bucket-major, chunk-minor.
-//   3. scan         : exclusive scan of those counts = the start of every
-//                     (window, bucket, chunk) run in the sorted index list.
-//   4. k_scatter    : same workgroups place point indices with LDS cursors —
-//                     no global atomics anywhere.
-//   5. k_accumulate : one lane per (window, bucket) walks its run and sums the
-//                     points in XYZZ with mixed additions (8M + 2S).
-//   6. k_reduce     : window sums sum_b b*B_b by a running-sum tree:
-//                     groups of 8 entries merge as T' = sum T + len * sum t*S.
-//   7. host         : Horner over the windows (c doublings each) + affine.
+//   1. k_digits         : signed c-bit digits, |d| <= 2^(c-1), one u16 key per
+//                         (window, point) — key = (|d|-1) | sign<<15, 0xFFFF = 0.
+//   2. k_hist           : one workgroup per (virtual window, chunk of points)
+//                         builds the chunk's bucket histogram in LDS (2^(c-1)
+//                         u32 <= 128 KiB) over all the key rows of its virtual
+//                         window, stored bucket-major, chunk-minor.
+//   3. scan             : exclusive scan of those counts = the start of every
+//                         (window, bucket, chunk) run in the sorted entry list.
+//   4. k_scatter        : same workgroups place entries with LDS cursors — no
+//                         global atomics anywhere.
+//   5. k_accumulate_flat: every lane sums exactly S consecutive sorted entries
+//                         (XYZZ mixed additions, 8M + 2S) across bucket
+//                         boundaries; k_bucket_merge joins split buckets.
+//   6. msm_reduce       : sum_b (b+1) B_b per virtual window (msm_reduce.hip).
+//   7. host             : per-window layout: Horner over the windows; both:
+//                         sum of the ranks' partial results, affine.
 #include <algorithm>
-#include "pnp_internal.h"
+#include "msm_internal.h"
 #include "ec.cuh"
 
 namespace pnp {
-
-struct MsmCfg {
-    int c, W, NB, nch;
-    uint64_t chunk;
-};
-
-static MsmCfg msm_cfg(uint64_t n) {
-    MsmCfg g;
-    int lg = 0;
-    while ((1ULL << lg) < n) lg++;
-    g.c = lg >= 20 ? 16 : (lg - 3 < 4 ? 4 : lg - 3);
-    g.W = (256 + g.c - 1) / g.c;
-    g.NB = 1 << (g.c - 1);
-    g.chunk = n < 8192 ? 8192 : (n >> 4 < 8192 ? 8192 : n >> 4);  // <= 16 chunks per window
-    g.nch = (int)((n + g.chunk - 1) / g.chunk);
-    return g;
-}
 
 // ---------------------------------------------------------------- 1. digits
 __global__ void k_digits(const uint64_t *scalars, uint64_t n, int c, int W, uint16_t *keys) {
@@ -72,28 +67,42 @@ __global__ void k_digits(const uint64_t *scalars, uint64_t n, int c, int W, uint
     }
 }
 
+// Virtual window v reads `rows` key rows starting at row v*vstride + off of
+// the key matrix (row r = keys[r*n .. r*n + n)); the entry of point i in its
+// row j is  i + (id_row0 + j) * id_mul  (id_mul = 0: the point index itself;
+// id_mul = n: the index into the folded table).
+struct KeyRows {
+    uint64_t n;
+    int vstride, off, rows;
+    uint32_t id_row0;
+    uint64_t id_mul;
+};
+
 // ---------------------------------------------------------------- 2. histogram
-__global__ __launch_bounds__(1024) void k_hist(const uint16_t *keys, uint64_t n, int NB,
+__global__ __launch_bounds__(1024) void k_hist(const uint16_t *keys, KeyRows kr, int NB,
                                                uint64_t chunk, int nch, uint32_t *counts) {
     extern __shared__ __attribute__((aligned(16))) uint32_t hist[];
-    const int w = blockIdx.y, ch = blockIdx.x;
+    const int v = blockIdx.y, ch = blockIdx.x;
     for (int b = threadIdx.x; b < NB; b += blockDim.x) hist[b] = 0;
     __syncthreads();
+    const uint64_t n = kr.n;
     uint64_t lo = (uint64_t)ch * chunk, hi = lo + chunk < n ? lo + chunk : n;
-    const uint16_t *k = keys + (uint64_t)w * n;
-    for (uint64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) {
-        uint16_t key = k[i];
-        if (key != 0xFFFF) atomicAdd(&hist[key & 0x7FFF], 1u);
+    const uint16_t *kb = keys + ((uint64_t)v * kr.vstride + kr.off) * n;
+    for (int r = 0; r < kr.rows; r++) {
+        const uint16_t *k = kb + (uint64_t)r * n;
+        for (uint64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) {
+            uint16_t key = k[i];
+            if (key != 0xFFFF) atomicAdd(&hist[key & 0x7FFF], 1u);
+        }
     }
     __syncthreads();
     for (int b = threadIdx.x; b < NB; b += blockDim.x)
-        counts[((uint64_t)w * NB + b) * nch + ch] = hist[b];
+        counts[((uint64_t)v * NB + b) * nch + ch] = hist[b];
 }
 
 // ---------------------------------------------------------------- 3. scan
 // exclusive scan of u32 in place, three phases over 1024-element tiles
 __global__ __launch_bounds__(256) void k_scan_tiles(uint32_t *d, uint64_t n, uint32_t *tile_sums) {
-    __shared__ uint32_t s[1024];
     __shared__ uint32_t wsum[4];
     uint64_t base = (uint64_t)blockIdx.x * 1024;
     uint32_t v[4], loc = 0;
@@ -120,7 +129,6 @@ __global__ __launch_bounds__(256) void k_scan_tiles(uint32_t *d, uint64_t n, uin
         excl += v[k];
     }
     if (threadIdx.x == 255) tile_sums[blockIdx.x] = wpre + x;
-    (void)s;
 }
 __global__ void k_scan_add(uint32_t *d, uint64_t n, const uint32_t *tile_pre) {
     uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
@@ -156,44 +164,30 @@ static void scan_u32(uint32_t *d, uint64_t n, DevBuf &scratch, hipStream_t s) {
 }
 
 // ---------------------------------------------------------------- 4. scatter
-__global__ __launch_bounds__(1024) void k_scatter(const uint16_t *keys, uint64_t n, int NB,
+__global__ __launch_bounds__(1024) void k_scatter(const uint16_t *keys, KeyRows kr, int NB,
                                                   uint64_t chunk, int nch, const uint32_t *offs,
                                                   uint32_t *sorted) {
     extern __shared__ __attribute__((aligned(16))) uint32_t cur[];
-    const int w = blockIdx.y, ch = blockIdx.x;
-    for (int b = threadIdx.x; b < NB; b += blockDim.x) cur[b] = offs[((uint64_t)w * NB + b) * nch + ch];
+    const int v = blockIdx.y, ch = blockIdx.x;
+    for (int b = threadIdx.x; b < NB; b += blockDim.x) cur[b] = offs[((uint64_t)v * NB + b) * nch + ch];
     __syncthreads();
+    const uint64_t n = kr.n;
     uint64_t lo = (uint64_t)ch * chunk, hi = lo + chunk < n ? lo + chunk : n;
-    const uint16_t *k = keys + (uint64_t)w * n;
-    for (uint64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) {
-        uint16_t key = k[i];
-        if (key == 0xFFFF) continue;
-        uint32_t pos = atomicAdd(&cur[key & 0x7FFF], 1u);
-        sorted[pos] = (uint32_t)i | ((uint32_t)(key >> 15) << 31);
+    const uint16_t *kb = keys + ((uint64_t)v * kr.vstride + kr.off) * n;
+    for (int r = 0; r < kr.rows; r++) {
+        const uint16_t *k = kb + (uint64_t)r * n;
+        const uint32_t idb = (uint32_t)((kr.id_row0 + r) * kr.id_mul);
+        for (uint64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) {
+            uint16_t key = k[i];
+            if (key == 0xFFFF) continue;
+            uint32_t pos = atomicAdd(&cur[key & 0x7FFF], 1u);
+            sorted[pos] = (idb + (uint32_t)i) | ((uint32_t)(key >> 15) << 31);
+        }
     }
 }
 
 // ---------------------------------------------------------------- 5. accumulate
-__global__ __launch_bounds__(256) void k_accumulate(const uint64_t *points, const uint32_t *sorted,
-                                                    const uint32_t *offs, int NB, int nch, int W,
-                                                    uint64_t *buckets) {
-    uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
-    if (t >= (uint64_t)W * NB) return;
-    uint32_t start = offs[t * nch];
-    uint32_t end = offs[(t + 1) * nch];  // offs[W*NB*nch] = total (sentinel)
-    Xyzz acc = Xyzz::inf();
-    for (uint32_t k = start; k < end; k++) {
-        uint32_t e = sorted[k];
-        uint32_t idx = e & 0x7FFFFFFFu;
-        const uint64_t *p = points + 12ULL * idx;
-        Fq x = load_fq(p), y = load_fq(p + 6);
-        if (e >> 31) y = neg(y);
-        acc = madd(acc, x, y);
-    }
-    store_xyzz(buckets + 24 * t, acc);
-}
-
-// 5'. balanced accumulate: thread t sums exactly the sorted entries
+// balanced accumulate: thread t sums exactly the sorted entries
 // [t*S, t*S + S) whatever the bucket boundaries, so every lane of a wave does
 // the same number of mixed additions (one lane per bucket waits for the
 // longest of 64 Poisson-sized runs: ~83% lane efficiency at n/NB = 128).  A
@@ -265,75 +259,147 @@ __global__ __launch_bounds__(256) void k_bucket_merge(const uint32_t *offs, int 
     store_xyzz(buckets + 24 * u, acc);
 }
 
-// ---------------------------------------------------------------- 6. reduce
-// Entry e of a level stands for a contiguous bucket range of length `len`
-// (power of two): T_e = sum_r (r+1) B_r over the range, S_e = sum_r B_r.
-// Groups of G entries merge into one: T' = sum_t T_t + len * sum_t t * S_t.
-// Leaves: T = S = B.
-template <int G>
-__global__ __launch_bounds__(256) void k_reduce(const uint64_t *inT, const uint64_t *inS,
-                                                uint64_t nout, uint32_t lg_len, uint64_t *outT,
-                                                uint64_t *outS) {
-    uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
-    if (t >= nout) return;
-    Xyzz sumT = Xyzz::inf(), run = Xyzz::inf(), acc = Xyzz::inf();
+
+// ---------------------------------------------------------------- folded table
+// level k -> k+1: xyzz[i] = 2^c * (x, y)_i
+__global__ __launch_bounds__(256) void k_table_dbl(const uint64_t *src, uint64_t n, int c,
+                                                   uint64_t *xyzz) {
+    uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    Xyzz q = dbl_affine(load_fq(src + 12 * i), load_fq(src + 12 * i + 6));
 #pragma unroll 1
-    for (int k = G - 1; k >= 0; k--) {
-        uint64_t e = t * G + k;
-        Xyzz T = load_xyzz(inT + 24 * e);
-        Xyzz S = load_xyzz(inS + 24 * e);
-        sumT = add(sumT, T);
-        if (k > 0) {
-            run = add(run, S);
-            acc = add(acc, run);  // after the loop: acc = sum_{t>=1} t * S_t
-        } else {
-            run = add(run, S);
-        }
+    for (int k = 1; k < c; k++) q = dbl(q);
+    store_xyzz(xyzz + 24 * i, q);
+}
+// XYZZ -> affine for CH consecutive points per lane, one Fermat inversion per
+// lane (Montgomery's trick over ZZZ; 1/ZZ = (ZZ/ZZZ)^2).  Points of the prime
+// order group are never infinity here.
+__global__ __launch_bounds__(256) void k_table_affine(const uint64_t *xyzz, uint64_t n, uint32_t CH,
+                                                      uint64_t *pre, uint64_t *dst) {
+    uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    uint64_t lo = t * CH;
+    if (lo >= n) return;
+    uint64_t hi = lo + CH < n ? lo + CH : n;
+    Fq acc = Fq::one();
+    for (uint64_t i = lo; i < hi; i++) {
+        Fq z = load_fq(xyzz + 24 * i + 18);
+        if (z.is_zero()) z = Fq::one();
+        acc = acc * z;
+        store_fq(pre + 6 * i, acc);
     }
-    for (uint32_t d = 0; d < lg_len; d++) acc = dbl(acc);
-    store_xyzz(outT + 24 * t, add(sumT, acc));
-    store_xyzz(outS + 24 * t, run);
+    Fq inv = inverse(acc);
+    for (uint64_t i = hi; i-- > lo;) {
+        Fq z = load_fq(xyzz + 24 * i + 18);
+        const bool inf = z.is_zero();
+        if (inf) z = Fq::one();
+        Fq izzz = i > lo ? inv * load_fq(pre + 6 * (i - 1)) : inv;
+        inv = inv * z;
+        Fq w = load_fq(xyzz + 24 * i + 12) * izzz;
+        Fq x = load_fq(xyzz + 24 * i) * (w * w);
+        Fq y = load_fq(xyzz + 24 * i + 6) * izzz;
+        if (inf) x = y = Fq::zero();
+        store_fq(dst + 12 * i, x);
+        store_fq(dst + 12 * i + 6, y);
+    }
 }
 
-// B independent MSMs over the same n points: the B*W windows are treated as
-// one set of "virtual windows" so every stage runs once for the whole batch.
+void msm_build_table(DevBuf &tab, const uint64_t *d_points, uint64_t n, hipStream_t s) {
+    MsmCfg g = msm_cfg(n);
+    tab.alloc((uint64_t)g.W * n * 96);
+    uint64_t *T = tab.u64();
+    PNP_HIP(hipMemcpyAsync(T, d_points, n * 96, hipMemcpyDeviceToDevice, s));
+    if (g.W == 1) return;
+    DevBuf xyzz(n * 192), pre(n * 48);
+    const uint32_t CH = 64;
+    const uint64_t lanes = (n + CH - 1) / CH;
+    for (int k = 1; k < g.W; k++) {
+        hipLaunchKernelGGL(k_table_dbl, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, s,
+                           T + (uint64_t)(k - 1) * n * 12, n, g.c, xyzz.u64());
+        PNP_HIP(hipGetLastError());
+        hipLaunchKernelGGL(k_table_affine, dim3((uint32_t)((lanes + 255) / 256)), dim3(256), 0, s,
+                           xyzz.u64(), n, CH, pre.u64(), T + (uint64_t)k * n * 12);
+        PNP_HIP(hipGetLastError());
+    }
+    PNP_HIP(hipStreamSynchronize(s));
+}
+
+// ---------------------------------------------------------------- driver
+static void put_xyzz(const Xyzz &r, uint64_t *o) {
+    to_u64_limbs(r.x, o);
+    to_u64_limbs(r.y, o + 6);
+    to_u64_limbs(r.zz, o + 12);
+    to_u64_limbs(r.zzz, o + 18);
+}
+static Xyzz get_xyzz(const uint64_t *e) {
+    Xyzz p;
+    p.x = from_u64_limbs<FqP>(e);
+    p.y = from_u64_limbs<FqP>(e + 6);
+    p.zz = from_u64_limbs<FqP>(e + 12);
+    p.zzz = from_u64_limbs<FqP>(e + 18);
+    return p;
+}
+
+// B independent MSMs over the same n points.  Per-window layout: the B*W
+// windows are "virtual windows" of NB buckets each, sharded across ranks.
+// Folded layout (table != nullptr): virtual window b = MSM b with the W key
+// rows of its windows; ranks shard the W windows, every rank reduces B
+// partial sums.
 void msm_run_batch(MsmWork &wk, const uint64_t *d_points, const uint64_t *const *d_scalars, int B,
-                   uint64_t n, uint64_t *h_xyzz, hipStream_t s) {
+                   uint64_t n, uint64_t *h_xyzz, hipStream_t s, const uint64_t *table) {
     if (n == 0 || B == 0) {
-        Xyzz r = Xyzz::inf();
-        for (int b = 0; b < B; b++) {
-            uint64_t *o = h_xyzz + 24 * b;
-            to_u64_limbs(r.x, o); to_u64_limbs(r.y, o + 6); to_u64_limbs(r.zz, o + 12);
-            to_u64_limbs(r.zzz, o + 18);
-        }
+        for (int b = 0; b < B; b++) put_xyzz(Xyzz::inf(), h_xyzz + 24 * b);
         return;
     }
-    MsmCfg g = msm_cfg(n);
-    const int WW = g.W * B;  // virtual windows (c-bit windows x batched MSMs)
-    // window sharding: rank r owns virtual windows [v0, v0 + nown)
-    const int per = (WW + wk.world - 1) / wk.world;
-    const int v0 = std::min(wk.rank * per, WW);
-    const int nown = std::min(v0 + per, WW) - v0;
-    const uint64_t WB = (uint64_t)nown * g.NB;
+    const MsmCfg g = msm_cfg(n);
+    const bool folded = table != nullptr;
+    // units sharded across ranks: windows (folded) or virtual windows
+    const int units = folded ? g.W : g.W * B;
+    const int per = (units + wk.world - 1) / wk.world;
+    const int u0 = std::min(wk.rank * per, units);
+    const int nown = std::min(u0 + per, units) - u0;
+    KeyRows kr;
+    kr.n = n;
+    int nv;  // virtual windows processed on this rank
+    if (folded) {
+        nv = nown > 0 ? B : 0;
+        kr.vstride = g.W;
+        kr.off = u0;
+        kr.rows = nown;
+        kr.id_row0 = (uint32_t)u0;
+        kr.id_mul = n;
+    } else {
+        nv = nown;
+        kr.vstride = 1;
+        kr.off = u0;
+        kr.rows = 1;
+        kr.id_row0 = 0;
+        kr.id_mul = 0;
+    }
+    const uint64_t WB = (uint64_t)nv * g.NB;
+    // points per histogram workgroup: ~512 workgroups in all (two rounds of
+    // one 128 KiB-LDS workgroup per CU), at least 1024 points each
+    const int nch0 = std::max(1, 512 / std::max(nv, 1));
+    const uint64_t chunk = std::max<uint64_t>(1024, (n + nch0 - 1) / nch0);
+    const int nch = (int)((n + chunk - 1) / chunk);
     auto need = [](DevBuf &b, size_t bytes) { if (b.bytes < bytes) b.alloc(bytes); };
-    need(wk.digits, (uint64_t)WW * n * 2);
-    need(wk.counts, (WB * g.nch + 1) * 4);
-    need(wk.sorted, (uint64_t)nown * n * 4);
-    need(wk.buckets, (WB + WB / 2 + 64 * (uint64_t)nown) * 24 * 8);
+    need(wk.digits, (uint64_t)g.W * B * n * 2);
+    need(wk.counts, (WB * nch + 1) * 4);
+    need(wk.sorted, (uint64_t)nv * kr.rows * n * 4 + 4);
+    need(wk.buckets, (WB + WB / 2 + 64 * (uint64_t)nv + 64) * 24 * 8);
     uint16_t *keys = static_cast<uint16_t *>(wk.digits.p);
     uint32_t *counts = static_cast<uint32_t *>(wk.counts.p);
     uint32_t *sorted = static_cast<uint32_t *>(wk.sorted.p);
+    const uint64_t *pts = folded ? table : d_points;
 
-    const uint64_t *inT = nullptr;
-    if (nown > 0) {
+    const uint64_t *res = nullptr;  // nv XYZZ window sums on the device
+    if (nv > 0) {
         for (int b = 0; b < B; b++) {
-            if ((b + 1) * g.W <= v0 || b * g.W >= v0 + nown) continue;  // no owned window
+            if (!folded && ((b + 1) * g.W <= u0 || b * g.W >= u0 + nown)) continue;
             hipLaunchKernelGGL(k_digits, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, s,
                                d_scalars[b], n, g.c, g.W, keys + (uint64_t)b * g.W * n);
             PNP_HIP(hipGetLastError());
         }
-        const uint16_t *own_keys = keys + (uint64_t)v0 * n;
-        dim3 grid((uint32_t)g.nch, (uint32_t)nown);
+        dim3 grid((uint32_t)nch, (uint32_t)nv);
         size_t lds = (size_t)g.NB * 4;
         static bool attr_set = false;
         if (!attr_set) {
@@ -343,118 +409,90 @@ void msm_run_batch(MsmWork &wk, const uint64_t *d_points, const uint64_t *const 
                                         hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
             attr_set = true;
         }
-        hipLaunchKernelGGL(k_hist, grid, dim3(1024), lds, s, own_keys, n, g.NB, g.chunk, g.nch,
-                           counts);
+        hipLaunchKernelGGL(k_hist, grid, dim3(1024), lds, s, keys, kr, g.NB, chunk, nch, counts);
         PNP_HIP(hipGetLastError());
-        const uint64_t ncount = WB * g.nch;
+        const uint64_t ncount = WB * nch;
         PNP_HIP(hipMemsetAsync(counts + ncount, 0, 4, s));
         scan_u32(counts, ncount + 1, wk.offsets, s);  // counts[ncount] = total
-        hipLaunchKernelGGL(k_scatter, grid, dim3(1024), lds, s, own_keys, n, g.NB, g.chunk, g.nch,
-                           counts, sorted);
+        hipLaunchKernelGGL(k_scatter, grid, dim3(1024), lds, s, keys, kr, g.NB, chunk, nch, counts,
+                           sorted);
         PNP_HIP(hipGetLastError());
         uint64_t *bk = wk.buckets.u64();
         hipEvent_t ev0 = nullptr;
         if (wk.timer) wk.timer->begin("msm_accumulate", s, ev0);
-        // balanced accumulate: S entries per thread (upper bound nown*n entries)
+        // balanced accumulate: S entries per thread (upper bound: every entry non-zero)
         const uint32_t S = 64;
-        const uint64_t nthr = ((uint64_t)nown * n + S - 1) / S;
+        const uint64_t nthr = ((uint64_t)nv * kr.rows * n + S - 1) / S;
         need(wk.seg, nthr * 2 * 24 * 8);
         uint64_t *head = wk.seg.u64(), *tail = head + nthr * 24;
         hipLaunchKernelGGL(k_accumulate_flat, dim3((uint32_t)((nthr + 255) / 256)), dim3(256), 0,
-                           s, d_points, sorted, counts, g.nch, WB, S, bk, head, tail);
+                           s, pts, sorted, counts, nch, WB, S, bk, head, tail);
         PNP_HIP(hipGetLastError());
         hipLaunchKernelGGL(k_bucket_merge, dim3((uint32_t)((WB + 255) / 256)), dim3(256), 0, s,
-                           counts, g.nch, WB, S, head, tail, bk);
+                           counts, nch, WB, S, head, tail, bk);
         PNP_HIP(hipGetLastError());
         // algorithmic bytes: each point (96 B) and scalar (32 B)
-        // once per owned window-sweep
+        // once per window sweep
         if (wk.timer)
-            wk.timer->end("msm_accumulate", s, ev0, (double)n * 128.0 * nown / g.W);
-        // running-sum tree: per virtual window NB entries -> 1
-        const uint64_t *inS = bk;
-        inT = bk;
-        uint64_t *free_ptr = bk + WB * 24;
-        uint64_t m = WB;
-        uint32_t lg_len = 0;
-        uint64_t per_win = g.NB;
-        while (per_win > 1) {
-            int G = per_win >= 8 ? 8 : (int)per_win;
-            uint64_t nout = m / G;
-            uint64_t *oT = free_ptr, *oS = free_ptr + nout * 24;
-            free_ptr += 2 * nout * 24;
-            uint32_t blocks = (uint32_t)((nout + 255) / 256);
-            switch (G) {
-                case 8: hipLaunchKernelGGL(k_reduce<8>, dim3(blocks), dim3(256), 0, s, inT, inS, nout, lg_len, oT, oS); break;
-                case 4: hipLaunchKernelGGL(k_reduce<4>, dim3(blocks), dim3(256), 0, s, inT, inS, nout, lg_len, oT, oS); break;
-                case 2: hipLaunchKernelGGL(k_reduce<2>, dim3(blocks), dim3(256), 0, s, inT, inS, nout, lg_len, oT, oS); break;
-                default: set_error("msm reduce"); throw Error(PNP_E_ARG);
-            }
-            PNP_HIP(hipGetLastError());
-            inT = oT;
-            inS = oS;
-            m = nout;
-            per_win /= G;
-            lg_len += (G == 8 ? 3 : G == 4 ? 2 : 1);
-        }
+            wk.timer->end("msm_accumulate", s, ev0, (double)n * 128.0 * nv * kr.rows / g.W);
+        res = msm_reduce(bk, (uint64_t)nv, g.NB, bk + WB * 24, s);
     }
-    std::vector<uint64_t> win((size_t)WW * 24);
+    // gather the window sums of all ranks on the host, slot r = rank r's units
+    const int per_slot = folded ? B : per;  // XYZZ points per rank slot
+    const int total = folded ? B * wk.world : units;
+    std::vector<uint64_t> win((size_t)std::max(total, per_slot * wk.world) * 24);
     if (wk.world == 1) {
-        PNP_HIP(hipMemcpyAsync(win.data(), inT, win.size() * 8, hipMemcpyDeviceToHost, s));
+        PNP_HIP(hipMemcpyAsync(win.data(), res, (size_t)nv * 24 * 8, hipMemcpyDeviceToHost, s));
         PNP_HIP(hipStreamSynchronize(s));
     } else {
-        // slot r of xbuf = windows [r*per, r*per + per): the gathered buffer is
-        // window-indexed, so one copy brings all WW window sums to the host
-        const uint64_t slot = (uint64_t)per * 24 * 8;
+        const uint64_t slot = (uint64_t)per_slot * 24 * 8;
         if (wk.xbuf_bytes < slot * wk.world) {
             set_error("msm shard: exchange buffer %llu B < %llu B",
                       (unsigned long long)wk.xbuf_bytes, (unsigned long long)(slot * wk.world));
             throw Error(PNP_E_ARG);
         }
-        if (nown > 0)
-            PNP_HIP(hipMemcpyAsync(wk.xbuf + (uint64_t)v0 * 24, inT, (uint64_t)nown * 24 * 8,
+        const uint64_t my = folded ? (uint64_t)wk.rank * B : (uint64_t)u0;
+        if (nv > 0)
+            PNP_HIP(hipMemcpyAsync(wk.xbuf + my * 24, res, (uint64_t)nv * 24 * 8,
                                    hipMemcpyDeviceToDevice, s));
+        if (folded && nv == 0) {  // idle rank: its slot holds infinities
+            std::vector<uint64_t> inf((size_t)B * 24);
+            for (int b = 0; b < B; b++) put_xyzz(Xyzz::inf(), inf.data() + 24 * b);
+            PNP_HIP(hipMemcpyAsync(wk.xbuf + my * 24, inf.data(), inf.size() * 8,
+                                   hipMemcpyHostToDevice, s));
+        }
         PNP_HIP(hipStreamSynchronize(s));
         int rc = wk.allgather(wk.user, slot);
         if (rc != 0) {
             set_error("msm shard: all-gather callback failed (%d)", rc);
             throw Error(PNP_E_DEVICE);
         }
-        PNP_HIP(hipMemcpyAsync(win.data(), wk.xbuf, win.size() * 8, hipMemcpyDeviceToHost, s));
+        PNP_HIP(hipMemcpyAsync(win.data(), wk.xbuf, (size_t)total * 24 * 8, hipMemcpyDeviceToHost, s));
         PNP_HIP(hipStreamSynchronize(s));
     }
     if (wk.timer) wk.timer->collect();
     for (int b = 0; b < B; b++) {
         Xyzz acc = Xyzz::inf();
-        for (int w = g.W - 1; w >= 0; w--) {
-            for (int k = 0; k < g.c; k++) acc = dbl(acc);
-            const uint64_t *e = &win[((size_t)b * g.W + w) * 24];
-            Xyzz ww;
-            ww.x = from_u64_limbs<FqP>(e);
-            ww.y = from_u64_limbs<FqP>(e + 6);
-            ww.zz = from_u64_limbs<FqP>(e + 12);
-            ww.zzz = from_u64_limbs<FqP>(e + 18);
-            acc = add(acc, ww);
+        if (folded) {
+            for (int r = 0; r < wk.world; r++) acc = add(acc, get_xyzz(&win[((size_t)r * B + b) * 24]));
+        } else {
+            for (int w = g.W - 1; w >= 0; w--) {
+                for (int k = 0; k < g.c; k++) acc = dbl(acc);
+                acc = add(acc, get_xyzz(&win[((size_t)b * g.W + w) * 24]));
+            }
         }
-        uint64_t *o = h_xyzz + 24 * b;
-        to_u64_limbs(acc.x, o);
-        to_u64_limbs(acc.y, o + 6);
-        to_u64_limbs(acc.zz, o + 12);
-        to_u64_limbs(acc.zzz, o + 18);
+        put_xyzz(acc, h_xyzz + 24 * b);
     }
 }
 
 void msm_run(MsmWork &wk, const uint64_t *d_points, const uint64_t *d_scalars, uint64_t n,
-             uint64_t *h_xyzz, hipStream_t s) {
+             uint64_t *h_xyzz, hipStream_t s, const uint64_t *table) {
     const uint64_t *sc[1] = {d_scalars};
-    msm_run_batch(wk, d_points, sc, 1, n, h_xyzz, s);
+    msm_run_batch(wk, d_points, sc, 1, n, h_xyzz, s, table);
 }
 
 void xyzz_to_affine_host(const uint64_t *xyzz, uint64_t *aff12) {
-    Xyzz p;
-    p.x = from_u64_limbs<FqP>(xyzz);
-    p.y = from_u64_limbs<FqP>(xyzz + 6);
-    p.zz = from_u64_limbs<FqP>(xyzz + 12);
-    p.zzz = from_u64_limbs<FqP>(xyzz + 18);
+    Xyzz p = get_xyzz(xyzz);
     Fq x, y;
     xyzz_to_affine(p, x, y);
     to_u64_limbs(x, aff12);

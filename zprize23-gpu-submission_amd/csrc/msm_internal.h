@@ -1,0 +1,30 @@
+// msm_internal.h — pieces shared by msm.hip (sort + accumulate) and
+// msm_reduce.hip (bucket reduction, compiled with out-of-line Fq products).
+#pragma once
+#include "pnp_internal.h"
+
+namespace pnp {
+
+// Window geometry for an n-point MSM: c-bit signed digits, W windows,
+// NB = 2^(c-1) buckets per window.
+struct MsmCfg {
+    int c, W, NB;
+};
+
+inline MsmCfg msm_cfg(uint64_t n) {
+    MsmCfg g;
+    int lg = 0;
+    while ((1ULL << lg) < n) lg++;
+    g.c = lg >= 20 ? 16 : (lg - 3 < 4 ? 4 : lg - 3);
+    g.W = (256 + g.c - 1) / g.c;
+    g.NB = 1 << (g.c - 1);
+    return g;
+}
+
+// Sum_b (b+1) * B_b for each of `nwin` consecutive groups of NB XYZZ buckets
+// (bk[0 .. nwin*NB)); `scratch` must hold 2*(nwin*NB/7 + 64*nwin) XYZZ points.
+// Returns the device address of the nwin results (XYZZ, 24 u64 each).
+const uint64_t *msm_reduce(const uint64_t *bk, uint64_t nwin, int NB, uint64_t *scratch,
+                           hipStream_t s);
+
+}  // namespace pnp

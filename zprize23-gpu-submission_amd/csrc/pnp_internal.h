@@ -97,10 +97,13 @@ struct MsmWork {
     uint64_t xbuf_bytes = 0;
 };
 // sum_i s_i P_i; scalars Montgomery Fr; result written to host as XYZZ Fq (4x6 u64)
+// `table` (optional): msm_build_table(d_points, n) — the folded layout
 void msm_run(MsmWork &w, const uint64_t *d_points, const uint64_t *d_scalars_mont, uint64_t n,
-             uint64_t *h_xyzz, hipStream_t s);
+             uint64_t *h_xyzz, hipStream_t s, const uint64_t *table = nullptr);
 void msm_run_batch(MsmWork &w, const uint64_t *d_points, const uint64_t *const *d_scalars, int B,
-                   uint64_t n, uint64_t *h_xyzz, hipStream_t s);
+                   uint64_t n, uint64_t *h_xyzz, hipStream_t s, const uint64_t *table = nullptr);
+// T[k*n + i] = 2^(c*k) P_i, k < W (msm_cfg(n)), affine Montgomery, 96 B per point
+void msm_build_table(DevBuf &tab, const uint64_t *d_points, uint64_t n, hipStream_t s);
 // host: XYZZ -> affine Montgomery (inf -> (0, one))
 void xyzz_to_affine_host(const uint64_t *xyzz, uint64_t *aff12);
 

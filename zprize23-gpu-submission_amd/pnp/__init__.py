@@ -28,7 +28,7 @@ ERRORS = {-1: "PNP_E_ARG", -2: "PNP_E_DEVICE", -3: "PNP_E_NOKEY", -4: "PNP_E_ENV
 SYMBOLS = ("gen_proof", "pnp_last_error", "pnp_ctx_create", "pnp_ctx_destroy",
            "pnp_load_prover_key", "pnp_load_commit_key", "pnp_prove", "pnp_last_stage_times",
            "pnp_kernel_timing", "pnp_kernel_stats", "pnp_kernel_bytes", "pnp_set_msm_shard",
-           "pnp_sync", "pnp_ntt", "pnp_coset_lde8", "pnp_commit", "pnp_poly_eval",
+           "pnp_sync", "pnp_ntt", "pnp_coset_lde8", "pnp_commit", "pnp_commit_ck", "pnp_poly_eval",
            "pnp_poly_div_linear", "pnp_prefix_product", "pnp_batch_inverse",
            "pnp_synth_random_fr", "pnp_synth_srs", "pnp_synth_coset_consts", "pnp_synth_circuit")
 
@@ -76,6 +76,7 @@ def load(path: str = LIB_PATH):
     lib.pnp_ntt.argtypes = [vp, vp, C.c_uint32, i32, i32]
     lib.pnp_coset_lde8.argtypes = [vp, vp, vp, C.c_uint32]
     lib.pnp_commit.argtypes = [vp, vp, vp, u64, C.POINTER(abi.CommitmentC)]
+    lib.pnp_commit_ck.argtypes = [vp, vp, u64, C.POINTER(abi.CommitmentC)]
     lib.pnp_poly_eval.argtypes = [vp, vp, u64, vp, vp]
     lib.pnp_poly_div_linear.argtypes = [vp, vp, u64, vp]
     lib.pnp_prefix_product.argtypes = [vp, vp, u64]
@@ -181,6 +182,12 @@ class Context:
         out = abi.CommitmentC()
         check(self.lib.pnp_commit(self.h, C.c_void_p(points), C.c_void_p(scalars), n, C.byref(out)),
               "pnp_commit")
+        return out
+
+    def commit_ck(self, scalars: int, n: int) -> abi.CommitmentC:
+        """Commitment against the resident commit key (folded fixed-base MSM)."""
+        out = abi.CommitmentC()
+        check(self.lib.pnp_commit_ck(self.h, C.c_void_p(scalars), n, C.byref(out)), "pnp_commit_ck")
         return out
 
     def poly_eval(self, addr: int, n: int, x_limbs):
