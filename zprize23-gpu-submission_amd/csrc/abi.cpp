@@ -360,7 +360,37 @@ int pnp_load_prover_key(pnp_ctx *ctx, const ProverKeyC *pk, uint64_t D, int devi
                                    ctx->stream));
             pnp::ntt_run(ctx->ntt, ctx->pk_sigma_n[j].u64(), lg, false, false, ctx->stream);
         }
-        PNP_HIP(hipStreamSynchronize(ctx->stream));
+        // coset constants: v_h^-1 (the reference divides by v_h every proof,
+        // quotient.cu:369-370); when the key's coset arrays are the standard
+        // ones (x_i = 7 w_8n^i, v_h = x^n - 1, as every key built by the
+        // reference's preprocessing), the L1 and PI coset evaluations have the
+        // closed forms of protocol.h and need no LDE per proof
+        const uint64_t N8 = 8 * D;
+        ctx->pk_vh_inv.alloc(32 * N8);
+        PNP_HIP(hipMemcpyAsync(ctx->pk_vh_inv.p, dev.v_h_coset_8n, 32 * N8, hipMemcpyDeviceToDevice,
+                               ctx->stream));
+        pnp::k_batch_inverse(ctx->pk_vh_inv.u64(), N8, ctx->scratch_a, ctx->stream);
+        {
+            pnp::DevBuf vh(32 * N8), x(32 * N8);
+            pnp::k_coset_consts(vh.u64(), x.u64(), lg, ctx->stream);
+            ctx->pk_std_coset =
+                !pnp::k_any_diff(vh.u64(), dev.v_h_coset_8n, 4 * N8, ctx->scratch_b, ctx->stream) &&
+                !pnp::k_any_diff(x.u64(), dev.linear_evaluations, 4 * N8, ctx->scratch_b, ctx->stream);
+            ctx->pk_l1v.release();
+            if (ctx->pk_std_coset) {
+                ctx->pk_l1v.alloc(32 * N8);
+                pnp::k_affine(ctx->pk_l1v.u64(), x.u64(), Fr::one(), pnp::neg(Fr::one()), N8, ctx->stream);
+                pnp::k_batch_inverse(ctx->pk_l1v.u64(), N8, ctx->scratch_a, ctx->stream);
+                Fr nf = Fr::zero();
+                nf.v[0] = (uint32_t)D;
+                nf.v[1] = (uint32_t)(D >> 32);
+                pnp::k_affine(ctx->pk_l1v.u64(), ctx->pk_l1v.u64(), pnp::inverse(pnp::to_mont(nf)),
+                              Fr::zero(), N8, ctx->stream);
+            }
+            ctx->pk_pinv.release();
+            ctx->pk_pinv_pos = ~0ULL;
+            PNP_HIP(hipStreamSynchronize(ctx->stream));
+        }
         ctx->pk_dev = dev;
         ctx->pk_n = D;
         ctx->pk_loaded = true;

@@ -20,6 +20,12 @@ struct pnp_ctx {
     ProverKeyC pk_dev{};                   // HBM pointers for every field
     bool pk_qm_zero = false, pk_qlookup_zero = false;  // all-zero 8n selector evaluations
     pnp::DevBuf pk_sigma_n[4];             // sigma evaluations on the n-domain
+    // proof-independent coset constants, computed at key load
+    pnp::DevBuf pk_vh_inv;                 // v_h_coset_8n^-1 (8n)
+    bool pk_std_coset = false;             // linear_evaluations = 7 w_8n^i, v_h = x^n - 1
+    pnp::DevBuf pk_l1v;                    // n^-1 / (x_i - 1) = L1 / Z_H  (std coset only)
+    pnp::DevBuf pk_pinv;                   // 1 / (x_i - w^pos), for pos = pk_pinv_pos
+    uint64_t pk_pinv_pos = ~0ULL;
     // ---- resident commit key ----
     bool ck_loaded = false;
     uint64_t ck_points = 0;

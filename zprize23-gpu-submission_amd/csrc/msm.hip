@@ -27,9 +27,10 @@
 //                         (window, bucket, chunk) run in the sorted entry list.
 //   4. k_scatter        : same workgroups place entries with LDS cursors — no
 //                         global atomics anywhere.
-//   5. k_accumulate_flat: every lane sums exactly S consecutive sorted entries
-//                         (XYZZ mixed additions, 8M + 2S) across bucket
-//                         boundaries; k_bucket_merge joins split buckets.
+//   5. accumulate       : XYZZ mixed additions (8M + 2S), k_accumulate_flat:
+//                         every lane sums exactly S consecutive sorted entries
+//                         across bucket boundaries; msm_merge_pieces joins the
+//                         pieces of split buckets (msm_reduce.hip).
 //   6. msm_reduce       : sum_b (b+1) B_b per virtual window (msm_reduce.hip).
 //   7. host             : per-window layout: Horner over the windows; both:
 //                         sum of the ranks' partial results, affine.
@@ -193,7 +194,7 @@ __global__ __launch_bounds__(1024) void k_scatter(const uint16_t *keys, KeyRows 
 // longest of 64 Poisson-sized runs: ~83% lane efficiency at n/NB = 128).  A
 // bucket lying inside one thread's range is written straight to `buckets`;
 // otherwise its first piece goes to tail[t0] and the pieces of the following
-// threads to head[t], and k_bucket_merge adds them up.
+// threads to head[t], and msm_merge_pieces adds them up.
 __device__ __forceinline__ uint32_t bucket_start(const uint32_t *offs, uint64_t u, int nch) {
     return offs[u * nch];
 }
@@ -239,26 +240,6 @@ __global__ __launch_bounds__(256) void k_accumulate_flat(const uint64_t *points,
     else if (next > hi) store_xyzz(tail + 24 * t, acc);
     else store_xyzz(buckets + 24 * cur, acc);
 }
-
-// bucket u = tail[t0] + head[t0+1] + ... + head[t1] when its entries span
-// threads t0 < t1; empty buckets become infinity
-__global__ __launch_bounds__(256) void k_bucket_merge(const uint32_t *offs, int nch, uint64_t U,
-                                                      uint32_t S, const uint64_t *head,
-                                                      const uint64_t *tail, uint64_t *buckets) {
-    uint64_t u = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
-    if (u >= U) return;
-    uint32_t s = bucket_start(offs, u, nch), e = bucket_start(offs, u + 1, nch);
-    if (s == e) {
-        store_xyzz(buckets + 24 * u, Xyzz::inf());
-        return;
-    }
-    uint32_t t0 = s / S, t1 = (e - 1) / S;
-    if (t0 == t1) return;
-    Xyzz acc = load_xyzz(tail + 24ULL * t0);
-    for (uint32_t t = t0 + 1; t <= t1; t++) acc = add(acc, load_xyzz(head + 24ULL * t));
-    store_xyzz(buckets + 24 * u, acc);
-}
-
 
 // ---------------------------------------------------------------- folded table
 // level k -> k+1: xyzz[i] = 2^c * (x, y)_i
@@ -385,7 +366,7 @@ void msm_run_batch(MsmWork &wk, const uint64_t *d_points, const uint64_t *const 
     need(wk.digits, (uint64_t)g.W * B * n * 2);
     need(wk.counts, (WB * nch + 1) * 4);
     need(wk.sorted, (uint64_t)nv * kr.rows * n * 4 + 4);
-    need(wk.buckets, (WB + WB / 2 + 64 * (uint64_t)nv + 64) * 24 * 8);
+    need(wk.buckets, (WB * 24 + WB * 72 + 64) * 8);  // buckets + reduction tree scratch
     uint16_t *keys = static_cast<uint16_t *>(wk.digits.p);
     uint32_t *counts = static_cast<uint32_t *>(wk.counts.p);
     uint32_t *sorted = static_cast<uint32_t *>(wk.sorted.p);
@@ -421,16 +402,17 @@ void msm_run_batch(MsmWork &wk, const uint64_t *d_points, const uint64_t *const 
         hipEvent_t ev0 = nullptr;
         if (wk.timer) wk.timer->begin("msm_accumulate", s, ev0);
         // balanced accumulate: S entries per thread (upper bound: every entry non-zero)
-        const uint32_t S = 64;
-        const uint64_t nthr = ((uint64_t)nv * kr.rows * n + S - 1) / S;
+        // (>= 64, or ~2^20 lanes: every bucket piece beyond the first costs an
+        // addition in msm_merge_pieces)
+        const uint64_t nent = (uint64_t)nv * kr.rows * n;
+        const uint32_t S = (uint32_t)std::max<uint64_t>(64, (nent >> 20) & ~7ULL);
+        const uint64_t nthr = (nent + S - 1) / S;
         need(wk.seg, nthr * 2 * 24 * 8);
         uint64_t *head = wk.seg.u64(), *tail = head + nthr * 24;
         hipLaunchKernelGGL(k_accumulate_flat, dim3((uint32_t)((nthr + 255) / 256)), dim3(256), 0,
                            s, pts, sorted, counts, nch, WB, S, bk, head, tail);
         PNP_HIP(hipGetLastError());
-        hipLaunchKernelGGL(k_bucket_merge, dim3((uint32_t)((WB + 255) / 256)), dim3(256), 0, s,
-                           counts, nch, WB, S, head, tail, bk);
-        PNP_HIP(hipGetLastError());
+        msm_merge_pieces(counts, nch, WB, S, (uint32_t)(nent / WB / S + 1), head, tail, bk, s);
         // algorithmic bytes: each point (96 B) and scalar (32 B)
         // once per window sweep
         if (wk.timer)

@@ -21,9 +21,17 @@ inline MsmCfg msm_cfg(uint64_t n) {
     return g;
 }
 
+// Buckets split across accumulate lanes (S entries per lane): bucket u whose
+// sorted run [offs[u*nch], offs[(u+1)*nch]) spans lanes t0 < t1 is
+// tail[t0] + head[t0+1] + ... + head[t1]; empty buckets become infinity.
+// `pieces`: typical lanes per bucket (sets the lanes per merge)
+void msm_merge_pieces(const uint32_t *offs, int nch, uint64_t U, uint32_t S, uint32_t pieces,
+                      const uint64_t *head, const uint64_t *tail, uint64_t *bk, hipStream_t s);
+
 // Sum_b (b+1) * B_b for each of `nwin` consecutive groups of NB XYZZ buckets
-// (bk[0 .. nwin*NB)); `scratch` must hold 2*(nwin*NB/7 + 64*nwin) XYZZ points.
+// (bk[0 .. nwin*NB), NB a power of two); `scratch` must hold 72*nwin*NB u64.
 // Returns the device address of the nwin results (XYZZ, 24 u64 each).
+
 const uint64_t *msm_reduce(const uint64_t *bk, uint64_t nwin, int NB, uint64_t *scratch,
                            hipStream_t s);
 

@@ -3,92 +3,124 @@
 // Replaces the reference's per-window running sum on the GPU plus the CPU
 // fold (sppark_msm/pippenger.cuh:360-468, zkp/cpu/collect.h:326-489).
 //
-// Running-sum tree: entry e of a level stands for a contiguous bucket range
-// of length `len` (a power of two): T_e = sum_r (r+1) B_r over the range and
-// S_e = sum_r B_r.  Groups of G entries merge as T' = sum T_t + len * sum t*S_t;
-// the leaves (T = S = B) take the cheaper running-sum form.
-//
-// These kernels run on few threads (one lane per 8 buckets, then 8x fewer
-// per level), so they are latency-bound: this translation unit calls the Fq
-// product out of line (PNP_FQ_OUTLINE, ec.cuh), keeping every kernel's hot
-// code inside the instruction cache (the inlined XYZZ add is ~150 KB of code;
-// a k_reduce with three inlined adds was 1.3 MB and ran at one wave per SIMD).
-#define PNP_FQ_OUTLINE 1
+// The reduction has little work (a few additions per bucket) and is bound by
+// the LATENCY of dependent XYZZ additions (~22 us each on one lane, measured
+// with tools/ubench_chain.hip), so it is organised for depth, not work:
+// a binary tree over the buckets of each window where a node of height h
+// covering buckets [a, a + 2^h) carries
+//     S = sum B_b,   T = sum (b - a + 1) B_b,   D = 2^h S.
+// Children L, R (height h-1) combine as
+//     S = S_L + S_R,   T = (T_L + T_R) + D_R,   D = 2 (D_L + D_R),
+// four additions and one doubling of depth 2 per level, so a window of 2^15
+// buckets is reduced at depth ~30 instead of the ~150 of running sums whose
+// partial results are scaled by repeated doubling.  The root's T is the window
+// sum.  One launch per level, one lane per node.
 #include "msm_internal.h"
 #include "ec.cuh"
 
 namespace pnp {
 
-// leaves: 8 buckets -> T = sum (r+1) B_r, S = sum B_r (14 additions)
-__global__ __launch_bounds__(256) void k_reduce_leaf(const uint64_t *bk, uint64_t nout,
-                                                     uint64_t *outT, uint64_t *outS) {
+// leaves (h = 1) from bucket pairs: S = B0 + B1, T = S + B1, D = 2 S
+__global__ __launch_bounds__(256) void k_tree_leaf(const uint64_t *bk, uint64_t nout, uint64_t *out) {
     uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
     if (t >= nout) return;
-    Xyzz run = load_xyzz(bk + 24 * (t * 8 + 7));
-    Xyzz acc = run;
-#pragma unroll 1
-    for (int k = 6; k >= 0; k--) {
-        run = add(run, load_xyzz(bk + 24 * (t * 8 + k)));
-        acc = add(acc, run);
-    }
-    store_xyzz(outT + 24 * t, acc);
-    store_xyzz(outS + 24 * t, run);
+    Xyzz b1 = load_xyzz(bk + 24 * (2 * t + 1));
+    Xyzz S = add(load_xyzz(bk + 24 * (2 * t)), b1);
+    uint64_t *o = out + 72 * t;
+    store_xyzz(o, S);
+    store_xyzz(o + 24, add(S, b1));
+    store_xyzz(o + 48, dbl(S));
 }
 
-template <int G>
-__global__ __launch_bounds__(256) void k_reduce(const uint64_t *inT, const uint64_t *inS,
-                                                uint64_t nout, uint32_t lg_len, uint64_t *outT,
-                                                uint64_t *outS) {
-    uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
-    if (t >= nout) return;
-    Xyzz sumT = Xyzz::inf(), run = Xyzz::inf(), acc = Xyzz::inf();
-#pragma unroll 1
-    for (int k = G - 1; k >= 0; k--) {
-        uint64_t e = t * G + k;
-        sumT = add(sumT, load_xyzz(inT + 24 * e));
-        run = add(run, load_xyzz(inS + 24 * e));
-        if (k > 0) acc = add(acc, run);  // after the loop: acc = sum_{t>=1} t * S_t
+// node t from nodes 2t, 2t+1 of the level below; triples (S, T, D) of 72 u64.
+// Three lanes per node (one per component), each at most two operations deep.
+__global__ __launch_bounds__(256) void k_tree_level(const uint64_t *in, uint64_t nout, uint64_t *out) {
+    uint64_t q = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    if (q >= 3 * nout) return;
+    const uint64_t t = q / 3;
+    const int c = (int)(q - 3 * t);
+    const uint64_t *L = in + 144 * t, *R = L + 72;
+    Xyzz r;
+    if (c == 0) {
+        r = add(load_xyzz(L), load_xyzz(R));
+    } else if (c == 1) {
+        r = add(add(load_xyzz(L + 24), load_xyzz(R + 24)), load_xyzz(R + 48));
+    } else {
+        r = dbl(add(load_xyzz(L + 48), load_xyzz(R + 48)));
     }
+    store_xyzz(out + 72 * t + 24 * c, r);
+}
+
+// G lanes per bucket (G | 256, a power of two): lane j sums pieces j, j+G,
+// ... serially, then a log2(G)-step LDS tree.  G is chosen so that every lane
+// adds ~4 pieces: the merge is latency-bound (~22 us per dependent addition).
+__global__ __launch_bounds__(256) void k_merge_pieces(const uint32_t *offs, int nch, uint64_t U,
+                                                      uint32_t S, int G, const uint64_t *head,
+                                                      const uint64_t *tail, uint64_t *bk) {
+    __shared__ uint64_t lds[256 * 24];
+    const uint64_t g = (blockIdx.x * (uint64_t)blockDim.x + threadIdx.x) / G;
+    const int j = threadIdx.x % G;
+    bool live = false;
+    Xyzz acc = Xyzz::inf();
+    if (g < U) {
+        uint32_t s0 = offs[g * nch], e0 = offs[(g + 1) * nch];
+        if (s0 == e0) {
+            if (j == 0) store_xyzz(bk + 24 * g, Xyzz::inf());
+        } else {
+            uint32_t t0 = s0 / S, t1 = (e0 - 1) / S;
+            if (t0 != t1) {
+                live = true;
+                // piece k = tail[t0] (k = 0) or head[t0 + k]
 #pragma unroll 1
-    for (uint32_t d = 0; d < lg_len; d++) acc = dbl(acc);
-    store_xyzz(outT + 24 * t, add(sumT, acc));
-    store_xyzz(outS + 24 * t, run);
+                for (uint32_t k = j; k <= t1 - t0; k += G)
+                    acc = add(acc, load_xyzz(k == 0 ? tail + 24ULL * t0 : head + 24ULL * (t0 + k)));
+            }
+        }
+    }
+    uint64_t *mine = lds + 24 * threadIdx.x;
+    for (int h = G / 2; h >= 1; h /= 2) {
+        store_xyzz(mine, acc);
+        __syncthreads();
+        if (live && j < h) acc = add(acc, load_xyzz(mine + 24 * h));
+        __syncthreads();
+    }
+    if (live && j == 0) store_xyzz(bk + 24 * g, acc);
+}
+
+void msm_merge_pieces(const uint32_t *offs, int nch, uint64_t U, uint32_t S, uint32_t pieces,
+                      const uint64_t *head, const uint64_t *tail, uint64_t *bk, hipStream_t s) {
+    int G = 1;
+    while (G < 8 && (uint32_t)G * 8 <= pieces) G *= 2;
+    const uint64_t blocks = (U * G + 255) / 256;
+    hipLaunchKernelGGL(k_merge_pieces, dim3((uint32_t)blocks), dim3(256), 0, s, offs, nch, U, S, G,
+                       head, tail, bk);
+    PNP_HIP(hipGetLastError());
+}
+
+// ---------------------------------------------------------------- tree
+// the roots' T, packed
+__global__ void k_tree_roots(const uint64_t *in, uint64_t n, uint64_t *out) {
+    uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    if (t < n) store_xyzz(out + 24 * t, load_xyzz(in + 72 * t + 24));
 }
 
 const uint64_t *msm_reduce(const uint64_t *bk, uint64_t nwin, int NB, uint64_t *scratch,
                            hipStream_t s) {
     if (NB == 1) return bk;
-    uint64_t m = nwin * NB;
-    uint64_t per_win = NB;
-    uint32_t lg_len = 0;
-    const uint64_t *inT = bk, *inS = bk;
-    uint64_t *free_ptr = scratch;
-    bool leaf = per_win >= 8;
-    while (per_win > 1) {
-        int G = per_win >= 8 ? 8 : (int)per_win;
-        uint64_t nout = m / G;
-        uint64_t *oT = free_ptr, *oS = free_ptr + nout * 24;
-        free_ptr += 2 * nout * 24;
-        uint32_t blocks = (uint32_t)((nout + 255) / 256);
-        if (leaf) {
-            hipLaunchKernelGGL(k_reduce_leaf, dim3(blocks), dim3(256), 0, s, inT, nout, oT, oS);
-            leaf = false;
-        } else {
-            switch (G) {
-                case 8: hipLaunchKernelGGL(k_reduce<8>, dim3(blocks), dim3(256), 0, s, inT, inS, nout, lg_len, oT, oS); break;
-                case 4: hipLaunchKernelGGL(k_reduce<4>, dim3(blocks), dim3(256), 0, s, inT, inS, nout, lg_len, oT, oS); break;
-                case 2: hipLaunchKernelGGL(k_reduce<2>, dim3(blocks), dim3(256), 0, s, inT, inS, nout, lg_len, oT, oS); break;
-                default: set_error("msm reduce: group %d", G); throw Error(PNP_E_ARG);
-            }
-        }
+    // two ping-pong triple arrays: level sizes nwin*NB/2, /4, ...
+    uint64_t m = nwin * (uint64_t)NB / 2;
+    uint64_t *a = scratch, *b = scratch + 72 * m;
+    hipLaunchKernelGGL(k_tree_leaf, dim3((uint32_t)((m + 255) / 256)), dim3(256), 0, s, bk, m, a);
+    PNP_HIP(hipGetLastError());
+    while (m > nwin) {
+        m /= 2;
+        hipLaunchKernelGGL(k_tree_level, dim3((uint32_t)((3 * m + 255) / 256)), dim3(256), 0, s, a, m, b);
         PNP_HIP(hipGetLastError());
-        inT = oT;
-        inS = oS;
-        m = nout;
-        per_win /= G;
-        lg_len += (G == 8 ? 3 : G == 4 ? 2 : 1);
+        std::swap(a, b);
     }
-    return inT;
+    hipLaunchKernelGGL(k_tree_roots, dim3((uint32_t)((nwin + 255) / 256)), dim3(256), 0, s, a, nwin, b);
+    PNP_HIP(hipGetLastError());
+    return b;
 }
 
 }  // namespace pnp

@@ -29,6 +29,11 @@ struct QuotArgs {
     const uint64_t *w8[4], *z8, *pi8, *f8, *t8, *h18, *h28, *z28, *l18;
     const uint64_t *q_m, *q_l, *q_r, *q_o, *q_4, *q_c, *q_hl, *q_hr, *q_h4, *q_arith, *q_lookup;
     const uint64_t *sig[4], *lin, *vh_inv;
+    // closed forms on the standard coset (pnp_ctx::pk_std_coset), replacing
+    // pi8 / l18: l1v = L1 / Z_H = n^-1 / (x - 1), pinv = 1 / (x - w^pos),
+    // PI / Z_H = c_pi * pinv with c_pi = pi * w^pos / n
+    const uint64_t *l1v, *pinv;
+    Fr c_pi;
     Fr alpha, alpha2, beta, gamma, delta, eps, zeta, lsep;
     Fr bk[4], opd, eopd, sep2, sep3;
 };
@@ -50,6 +55,10 @@ void k_lookup_nd(uint64_t *num, uint64_t *den, const uint64_t *f, const uint64_t
                  hipStream_t s);
 void k_mul_inplace(uint64_t *a, const uint64_t *b, uint64_t n, hipStream_t s);
 bool k_any_nonzero(const uint64_t *v, uint64_t words, DevBuf &scratch, hipStream_t s);
+// any word of a differs from b
+bool k_any_diff(const uint64_t *a, const uint64_t *b, uint64_t words, DevBuf &scratch, hipStream_t s);
+// out_i = a * in_i + b
+void k_affine(uint64_t *out, const uint64_t *in, const Fr &a, const Fr &b, uint64_t n, hipStream_t s);
 void k_quotient(const QuotArgs &q, uint64_t N8, uint64_t *out, hipStream_t s);
 void k_lincomb(const LinArgs &a, uint64_t n, uint64_t *out, hipStream_t s);
 

@@ -154,6 +154,37 @@ bool k_any_nonzero(const uint64_t *v, uint64_t words, DevBuf &scratch, hipStream
     return h != 0;
 }
 
+__global__ void k_any_diff_(const uint64_t *a, const uint64_t *b, uint64_t words, unsigned *flag) {
+    uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    uint64_t acc = 0;
+    for (; i < words; i += stride) acc |= a[i] ^ b[i];
+    if (__any(acc != 0) && (threadIdx.x & 63) == 0) atomicOr(flag, 1u);
+}
+bool k_any_diff(const uint64_t *a, const uint64_t *b, uint64_t words, DevBuf &scratch, hipStream_t s) {
+    if (!words) return false;
+    if (scratch.bytes < 16) scratch.alloc(16);
+    unsigned *flag = static_cast<unsigned *>(scratch.p);
+    PNP_HIP(hipMemsetAsync(flag, 0, 4, s));
+    uint64_t blocks = (words + 255) / 256;
+    if (blocks > 4096) blocks = 4096;
+    hipLaunchKernelGGL(k_any_diff_, dim3((uint32_t)blocks), dim3(256), 0, s, a, b, words, flag);
+    PNP_HIP(hipGetLastError());
+    unsigned h = 0;
+    PNP_HIP(hipMemcpyAsync(&h, flag, 4, hipMemcpyDeviceToHost, s));
+    PNP_HIP(hipStreamSynchronize(s));
+    return h != 0;
+}
+
+__global__ void k_affine_(uint64_t *out, const uint64_t *in, Fr a, Fr b, uint64_t n) {
+    uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    if (i < n) store_fr(out, i, load_fr(in, i) * a + b);
+}
+void k_affine(uint64_t *out, const uint64_t *in, const Fr &a, const Fr &b, uint64_t n, hipStream_t s) {
+    hipLaunchKernelGGL(k_affine_, dim3(nblk(n)), dim3(256), 0, s, out, in, a, b, n);
+    PNP_HIP(hipGetLastError());
+}
+
 // ---------------------------------------------------------------- quotient
 __device__ __forceinline__ Fr ld(const uint64_t *p, uint64_t i) {
     return p ? load_fr(p, i) : Fr::zero();
@@ -178,7 +209,7 @@ __global__ __launch_bounds__(256) void k_quotient_(QuotArgs q, uint64_t N8, uint
     acc += pow5(b) * load_fr(q.q_hr, i);
     acc += pow5(d) * load_fr(q.q_h4, i);
     acc += load_fr(q.q_c, i);
-    Fr num = acc * load_fr(q.q_arith, i) + ld(q.pi8, i);
+    Fr num = acc * load_fr(q.q_arith, i) + ld(q.pi8, i);  // pi8 = nullptr: closed form below
     // permutation_compute_quotient (proof_system/permutation.cu:267-296)
     Fr x = load_fr(q.lin, i);
     Fr zi = load_fr(q.z8, i), zn = load_fr(q.z8, nx);
@@ -189,7 +220,9 @@ __global__ __launch_bounds__(256) void k_quotient_(QuotArgs q, uint64_t N8, uint
             (load_fr(q.sig[2], i) * q.beta + c + q.gamma) * (load_fr(q.sig[3], i) * q.beta + d + q.gamma);
     pb = pb * zn * q.alpha;
     // L1 scaled by alpha^2 (quotient.cu:3-8 LDEs alpha^2 L1; linear, so fold it here)
-    num += pa - pb + (zi - Fr::one()) * (load_fr(q.l18, i) * q.alpha2);
+    num += pa - pb;
+    // terms carrying L1, over Z_H (closed form) or not (LDE of L1)
+    Fr l1t = (zi - Fr::one()) * q.alpha2;
     // _compute_quotient_i (widget/lookup.cu:3-134)
     Fr f = ld(q.f8, i);
     if (q.q_lookup) {
@@ -205,10 +238,16 @@ __global__ __launch_bounds__(256) void k_quotient_(QuotArgs q, uint64_t N8, uint
         Fr z2 = load_fr(q.z28, i), z2n = load_fr(q.z28, nx);
         Fr lk = z2 * q.opd * (f + q.eps) * (tt + q.eopd + ttn * q.delta) * q.sep2;
         lk -= z2n * (h1 + q.eopd + h2 * q.delta) * (h2 + q.eopd + h1n * q.delta) * q.sep2;
-        lk += (z2 - Fr::one()) * (load_fr(q.l18, i) * q.sep3);
+        l1t += (z2 - Fr::one()) * q.sep3;
         num += lk;
     }
-    store_fr(out, i, num * load_fr(q.vh_inv, i));
+    if (q.l1v) {
+        Fr r = num * load_fr(q.vh_inv, i) + l1t * load_fr(q.l1v, i);
+        if (q.pinv) r += q.c_pi * load_fr(q.pinv, i);
+        store_fr(out, i, r);
+    } else {
+        store_fr(out, i, (num + l1t * load_fr(q.l18, i)) * load_fr(q.vh_inv, i));
+    }
 }
 void k_quotient(const QuotArgs &q, uint64_t N8, uint64_t *out, hipStream_t s) {
     hipLaunchKernelGGL(k_quotient_, dim3(nblk(N8)), dim3(256), 0, s, q, N8, out);

@@ -219,12 +219,22 @@ int prove_impl(pnp_ctx *ctx, const CircuitC *cs, int device_ptrs, ProofC *out) {
     // MSM is batched with the quotient chunks in round 4
     // public input poly (pi.cu:11-15)
     // = iNTT of the evaluations v * e_pos, in closed form: v n^-1 w^(-pos j)
-    uint64_t *pi_poly = ctx->buf("pi_poly", n);
     const Fr n_inv = inverse(fr_from_u64(n));
-    {
-        Fr v = to_mont(from_u64_limbs<FrP>(cs->pi));
+    const Fr pi_v = to_mont(from_u64_limbs<FrP>(cs->pi));
+    const bool closed = ctx->pk_std_coset;  // L1, PI on the coset in closed form
+    uint64_t *pi_poly = nullptr;
+    if (!closed) {
+        pi_poly = ctx->buf("pi_poly", n);
         Fr w_inv_pos = pow_u64(inverse(root_of_unity(lg)), cs->intended_pi_pos);
-        k_geometric(pi_poly, n, v * n_inv, w_inv_pos, s);
+        k_geometric(pi_poly, n, pi_v * n_inv, w_inv_pos, s);
+    } else if (ctx->pk_pinv_pos != cs->intended_pi_pos) {
+        // 1 / (x_i - w^pos), kept across proofs with the same PI position
+        ctx->pk_pinv_pos = ~0ULL;
+        if (!ctx->pk_pinv.p) ctx->pk_pinv.alloc(32 * N8);
+        Fr wpos = pow_u64(root_of_unity(lg), cs->intended_pi_pos);
+        k_affine(ctx->pk_pinv.u64(), pk.linear_evaluations, Fr::one(), neg(wpos), N8, s);
+        k_batch_inverse(ctx->pk_pinv.u64(), N8, ctx->scratch_a, s);
+        ctx->pk_pinv_pos = cs->intended_pi_pos;
     }
     tm.mark("r3_z2_pi");
 
@@ -248,11 +258,20 @@ int prove_impl(pnp_ctx *ctx, const CircuitC *cs, int device_ptrs, ProofC *out) {
         coset_lde8(nt, wpoly[j], w8, lg, s);
         q.w8[j] = w8;
     }
-    uint64_t *z8 = ctx->buf("z8", N8), *pi8 = ctx->buf("pi8", N8), *z28 = ctx->buf("z28", N8);
+    uint64_t *z8 = ctx->buf("z8", N8), *z28 = ctx->buf("z28", N8);
     coset_lde8(nt, z_poly, z8, lg, s);
-    coset_lde8(nt, pi_poly, pi8, lg, s);
     q.z8 = z8;
-    q.pi8 = pi8;
+    q.pi8 = nullptr;
+    q.l18 = q.l1v = q.pinv = nullptr;
+    if (closed) {
+        q.l1v = ctx->pk_l1v.u64();
+        q.pinv = ctx->pk_pinv.u64();
+        q.c_pi = pi_v * pow_u64(root_of_unity(lg), cs->intended_pi_pos) * n_inv;
+    } else {
+        uint64_t *pi8 = ctx->buf("pi8", N8);
+        coset_lde8(nt, pi_poly, pi8, lg, s);
+        q.pi8 = pi8;
+    }
     q.z28 = nullptr;  // z2 = 1: its quotient terms cancel (protocol.h)
     if (!z2_one) {
         coset_lde8(nt, z2_poly, z28, lg, s);
@@ -273,10 +292,12 @@ int prove_impl(pnp_ctx *ctx, const CircuitC *cs, int device_ptrs, ProofC *out) {
     // compute_first_lagrange_poly_scaled(n, alpha^2) and (n, 1) (quotient.cu:3-8):
     // one LDE of L1 (coefficients n^-1, no iNTT); alpha^2 is applied in the kernel
     Fr alpha2 = alpha * alpha;
-    uint64_t *l1 = ctx->buf("l1", n), *l18 = ctx->buf("l18", N8);
-    k_geometric(l1, n, n_inv, Fr::one(), s);
-    coset_lde8(nt, l1, l18, lg, s);
-    q.l18 = l18;
+    if (!closed) {
+        uint64_t *l1 = ctx->buf("l1", n), *l18 = ctx->buf("l18", N8);
+        k_geometric(l1, n, n_inv, Fr::one(), s);
+        coset_lde8(nt, l1, l18, lg, s);
+        q.l18 = l18;
+    }
     q.alpha2 = alpha2;
     q.q_m = ctx->pk_qm_zero ? nullptr : pk.q_m_evals;
     q.q_l = pk.q_l_evals;
@@ -294,10 +315,7 @@ int prove_impl(pnp_ctx *ctx, const CircuitC *cs, int device_ptrs, ProofC *out) {
     q.sig[2] = pk.out_sigma_evals;
     q.sig[3] = pk.fourth_sigma_evals;
     q.lin = pk.linear_evaluations;
-    uint64_t *vh_inv = ctx->buf("vh_inv", N8);
-    PNP_HIP(hipMemcpyAsync(vh_inv, pk.v_h_coset_8n, 32 * N8, hipMemcpyDeviceToDevice, s));
-    k_batch_inverse(vh_inv, N8, ctx->scratch_a, s);
-    q.vh_inv = vh_inv;
+    q.vh_inv = ctx->pk_vh_inv.u64();  // v_h^-1, computed at key load
     q.alpha = alpha;
     q.beta = beta;
     q.gamma = gamma;
@@ -321,7 +339,7 @@ int prove_impl(pnp_ctx *ctx, const CircuitC *cs, int device_ptrs, ProofC *out) {
         const uint64_t *arrs[] = {q.w8[0], q.w8[1], q.w8[2], q.w8[3], q.q_m, q.q_l, q.q_r, q.q_o,
                                   q.q_4, q.q_c, q.q_hl, q.q_hr, q.q_h4, q.q_arith, q.pi8, q.lin,
                                   q.z8, q.sig[0], q.sig[1], q.sig[2], q.sig[3], q.f8,
-                                  q.t8, q.h18, q.h28, q.q_lookup, q.z28, q.l18, q.vh_inv};
+                                  q.t8, q.h18, q.h28, q.q_lookup, q.z28, q.l18, q.vh_inv, q.l1v, q.pinv};
         int nread = 0;
         for (const uint64_t *a : arrs) nread += a != nullptr;
         ctx->ktimer.end("quotient", s, qe0, 32.0 * (double)N8 * (nread + 1));
