@@ -79,26 +79,46 @@ struct KeyRows {
     uint64_t id_mul;
 };
 
-// ---------------------------------------------------------------- 2. histogram
-__global__ __launch_bounds__(1024) void k_hist(const uint16_t *keys, KeyRows kr, int NB,
-                                               uint64_t chunk, int nch, uint32_t *counts) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t hist[];
+// ---------------------------------------------------------------- 2. coarse pass
+// Two-pass bucket sort.  Pass A sorts the entries by the top CB bits of the
+// bucket (NBc <= 128 coarse bins), pass B sorts each coarse bin (~2^19 entries
+// of a 2^22 MSM) by the remaining FB bits in one workgroup.  Few bins keep the
+// write fronts few; pass A also counting-sorts 4096-key tiles in LDS so each
+// bin's entries leave as one run (a one-pass scatter straight to 2^15 buckets
+// wrote ~8x its payload to HBM).  Keys, fine keys and entries are read four
+// per lane (8 / 4 / 16-byte loads).
+constexpr int SORT_CB = 7;
+__global__ __launch_bounds__(1024) void k_coarse_hist(const uint16_t *keys, KeyRows kr, int fb,
+                                                      int NBc, uint64_t chunk, int nch,
+                                                      uint32_t *counts) {
+    __shared__ uint32_t hist[1 << SORT_CB];
     const int v = blockIdx.y, ch = blockIdx.x;
-    for (int b = threadIdx.x; b < NB; b += blockDim.x) hist[b] = 0;
+    for (int b = threadIdx.x; b < NBc; b += blockDim.x) hist[b] = 0;
     __syncthreads();
     const uint64_t n = kr.n;
     uint64_t lo = (uint64_t)ch * chunk, hi = lo + chunk < n ? lo + chunk : n;
     const uint16_t *kb = keys + ((uint64_t)v * kr.vstride + kr.off) * n;
+    const bool vec = ((n | chunk) & 3) == 0;  // four keys per 8-byte load
     for (int r = 0; r < kr.rows; r++) {
         const uint16_t *k = kb + (uint64_t)r * n;
-        for (uint64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) {
-            uint16_t key = k[i];
-            if (key != 0xFFFF) atomicAdd(&hist[key & 0x7FFF], 1u);
+        if (vec) {
+            for (uint64_t i = lo + 4 * threadIdx.x; i < hi; i += 4 * blockDim.x) {
+                uint2 q = *reinterpret_cast<const uint2 *>(k + i);
+                uint32_t w[4] = {q.x & 0xFFFF, q.x >> 16, q.y & 0xFFFF, q.y >> 16};
+#pragma unroll
+                for (int j = 0; j < 4; j++)
+                    if (w[j] != 0xFFFF) atomicAdd(&hist[(w[j] & 0x7FFF) >> fb], 1u);
+            }
+        } else {
+            for (uint64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) {
+                uint16_t key = k[i];
+                if (key != 0xFFFF) atomicAdd(&hist[(key & 0x7FFF) >> fb], 1u);
+            }
         }
     }
     __syncthreads();
-    for (int b = threadIdx.x; b < NB; b += blockDim.x)
-        counts[((uint64_t)v * NB + b) * nch + ch] = hist[b];
+    for (int b = threadIdx.x; b < NBc; b += blockDim.x)
+        counts[((uint64_t)v * NBc + b) * nch + ch] = hist[b];
 }
 
 // ---------------------------------------------------------------- 3. scan
@@ -164,26 +184,169 @@ static void scan_u32(uint32_t *d, uint64_t n, DevBuf &scratch, hipStream_t s) {
     }
 }
 
-// ---------------------------------------------------------------- 4. scatter
-__global__ __launch_bounds__(1024) void k_scatter(const uint16_t *keys, KeyRows kr, int NB,
-                                                  uint64_t chunk, int nch, const uint32_t *offs,
-                                                  uint32_t *sorted) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t cur[];
+// ---------------------------------------------------------------- 4. scatters
+// pass A: entry (table index | sign << 31) and its fine key, grouped by coarse
+// bin.  Tiles of 4096 keys are counting-sorted in LDS first, so each bin's
+// entries of a tile leave as one contiguous run (coalesced stores).
+constexpr int TILE_K = 4096;
+__device__ __forceinline__ void tile_scan(uint32_t *lh, uint32_t *lofs, int nb) {
+    // exclusive scan of lh[0..nb) into lofs by wave 0 (nb <= 256)
+    if (threadIdx.x < 64) {
+        const int per = (nb + 63) / 64, b0 = threadIdx.x * per;
+        uint32_t loc = 0;
+        for (int b = b0; b < b0 + per && b < nb; b++) loc += lh[b];
+        uint32_t x = loc;
+        for (int off = 1; off < 64; off <<= 1) {
+            uint32_t y = __shfl_up(x, off, 64);
+            if ((int)threadIdx.x >= off) x += y;
+        }
+        uint32_t run = x - loc;
+        for (int b = b0; b < b0 + per && b < nb; b++) {
+            lofs[b] = run;
+            run += lh[b];
+        }
+    }
+}
+
+__global__ __launch_bounds__(1024) void k_coarse_scatter(const uint16_t *keys, KeyRows kr, int fb,
+                                                         int NBc, uint64_t chunk, int nch,
+                                                         const uint32_t *offs, uint32_t *ent,
+                                                         uint8_t *fk) {
+    __shared__ uint32_t cur[1 << SORT_CB], lh[1 << SORT_CB], lofs[1 << SORT_CB];
+    __shared__ uint32_t st_e[TILE_K];
+    __shared__ uint16_t st_m[TILE_K];
     const int v = blockIdx.y, ch = blockIdx.x;
-    for (int b = threadIdx.x; b < NB; b += blockDim.x) cur[b] = offs[((uint64_t)v * NB + b) * nch + ch];
+    for (int b = threadIdx.x; b < NBc; b += blockDim.x) {
+        cur[b] = offs[((uint64_t)v * NBc + b) * nch + ch];
+        lh[b] = 0;
+    }
     __syncthreads();
     const uint64_t n = kr.n;
+    const uint32_t fmask = (1u << fb) - 1;
     uint64_t lo = (uint64_t)ch * chunk, hi = lo + chunk < n ? lo + chunk : n;
     const uint16_t *kb = keys + ((uint64_t)v * kr.vstride + kr.off) * n;
+    const bool vec = ((n | chunk) & 3) == 0;
     for (int r = 0; r < kr.rows; r++) {
         const uint16_t *k = kb + (uint64_t)r * n;
         const uint32_t idb = (uint32_t)((kr.id_row0 + r) * kr.id_mul);
-        for (uint64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) {
-            uint16_t key = k[i];
-            if (key == 0xFFFF) continue;
-            uint32_t pos = atomicAdd(&cur[key & 0x7FFF], 1u);
-            sorted[pos] = (idb + (uint32_t)i) | ((uint32_t)(key >> 15) << 31);
+        for (uint64_t tb = lo; tb < hi; tb += TILE_K) {
+            const uint64_t i0 = tb + 4 * threadIdx.x;
+            uint32_t key[4], rank[4];
+            if (vec && i0 + 4 <= hi) {
+                uint2 q = *reinterpret_cast<const uint2 *>(k + i0);
+                key[0] = q.x & 0xFFFF; key[1] = q.x >> 16; key[2] = q.y & 0xFFFF; key[3] = q.y >> 16;
+            } else {
+#pragma unroll
+                for (int j = 0; j < 4; j++) key[j] = i0 + j < hi ? k[i0 + j] : 0xFFFF;
+            }
+#pragma unroll
+            for (int j = 0; j < 4; j++)
+                if (key[j] != 0xFFFF) rank[j] = atomicAdd(&lh[(key[j] & 0x7FFF) >> fb], 1u);
+            __syncthreads();
+            tile_scan(lh, lofs, NBc);
+            __syncthreads();
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                if (key[j] == 0xFFFF) continue;
+                uint32_t mag = key[j] & 0x7FFF, at = lofs[mag >> fb] + rank[j];
+                st_e[at] = (idb + (uint32_t)(i0 + j)) | ((key[j] >> 15) << 31);
+                st_m[at] = (uint16_t)mag;
+            }
+            __syncthreads();
+            const uint32_t total = lofs[NBc - 1] + lh[NBc - 1];
+            for (uint32_t x = threadIdx.x; x < total; x += blockDim.x) {
+                uint32_t mag = st_m[x], bn = mag >> fb;
+                uint32_t pos = cur[bn] + x - lofs[bn];
+                ent[pos] = st_e[x];
+                fk[pos] = (uint8_t)(mag & fmask);
+            }
+            __syncthreads();
+            for (int b = threadIdx.x; b < NBc; b += blockDim.x) {
+                cur[b] += lh[b];
+                lh[b] = 0;
+            }
+            __syncthreads();
         }
+    }
+}
+
+// pass B: one workgroup per (virtual window, coarse bin) = bucket range
+// [p << fb, (p + 1) << fb); writes every bucket's start and the sorted entries
+// Histogram first (bucket starts), then tiles of 8192 entries counting-sorted
+// in LDS and written out one run per fine bin (~32 entries at 2^22).
+constexpr int TILE_F = 8192;
+__global__ __launch_bounds__(1024) void k_fine_sort(const uint32_t *ent, const uint8_t *fk,
+                                                    const uint32_t *coffs, int nch, int fb,
+                                                    uint32_t *bstart, uint32_t *sorted) {
+    __shared__ uint32_t h[256], lh[256], lofs[256];
+    __shared__ uint32_t st_e[TILE_F];
+    __shared__ uint8_t st_f[TILE_F];
+    const uint64_t p = blockIdx.x;
+    const uint32_t ps = coffs[p * nch], pe = coffs[(p + 1) * nch];
+    const int NF = 1 << fb;
+    for (int f = threadIdx.x; f < NF; f += blockDim.x) h[f] = lh[f] = 0;
+    __syncthreads();
+    // [a, b): 4-aligned body read as uchar4; the rest one by one
+    const uint32_t a = std::min((ps + 3) & ~3u, pe), b = std::max(pe & ~3u, a);
+    for (uint32_t k = a + 4 * threadIdx.x; k < b; k += 4 * blockDim.x) {
+        uint32_t q = *reinterpret_cast<const uint32_t *>(fk + k);
+        atomicAdd(&h[q & 0xFF], 1u);
+        atomicAdd(&h[(q >> 8) & 0xFF], 1u);
+        atomicAdd(&h[(q >> 16) & 0xFF], 1u);
+        atomicAdd(&h[q >> 24], 1u);
+    }
+    for (uint32_t k = ps + threadIdx.x; k < a; k += blockDim.x) atomicAdd(&h[fk[k]], 1u);
+    for (uint32_t k = b + threadIdx.x; k < pe; k += blockDim.x) atomicAdd(&h[fk[k]], 1u);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t run = ps;
+        for (int f = 0; f < NF; f++) {
+            uint32_t c = h[f];
+            h[f] = run;  // h becomes the global cursor of bin f
+            run += c;
+        }
+    }
+    __syncthreads();
+    for (int f = threadIdx.x; f < NF; f += blockDim.x) bstart[p * NF + f] = h[f];
+    constexpr int PER = TILE_F / 1024;
+    for (uint32_t tb = ps; tb < pe; tb += TILE_F) {
+        uint32_t e[PER], rank[PER];
+        uint8_t f[PER];
+#pragma unroll
+        for (int j = 0; j < PER; j++) {
+            uint32_t k = tb + threadIdx.x + j * 1024;  // coalesced, one entry per lane per step
+            f[j] = 0;
+            e[j] = 0xFFFFFFFFu;
+            if (k < pe) {
+                f[j] = fk[k];
+                e[j] = ent[k];
+                rank[j] = atomicAdd(&lh[f[j]], 1u);
+            }
+        }
+        __syncthreads();
+        tile_scan(lh, lofs, NF);
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < PER; j++) {
+            uint32_t k = tb + threadIdx.x + j * 1024;
+            if (k < pe) {
+                uint32_t at = lofs[f[j]] + rank[j];
+                st_e[at] = e[j];
+                st_f[at] = f[j];
+            }
+        }
+        __syncthreads();
+        const uint32_t total = pe - tb < (uint32_t)TILE_F ? pe - tb : (uint32_t)TILE_F;
+        for (uint32_t x = threadIdx.x; x < total; x += blockDim.x) {
+            uint32_t bn = st_f[x];
+            sorted[h[bn] + x - lofs[bn]] = st_e[x];
+        }
+        __syncthreads();
+        for (int q = threadIdx.x; q < NF; q += blockDim.x) {
+            h[q] += lh[q];
+            lh[q] = 0;
+        }
+        __syncthreads();
     }
 }
 
@@ -357,18 +520,24 @@ void msm_run_batch(MsmWork &wk, const uint64_t *d_points, const uint64_t *const 
         kr.id_mul = 0;
     }
     const uint64_t WB = (uint64_t)nv * g.NB;
-    // points per histogram workgroup: ~512 workgroups in all (two rounds of
-    // one 128 KiB-LDS workgroup per CU), at least 1024 points each
+    // points per coarse-pass workgroup: ~512 workgroups in all, >= 1024 points each
     const int nch0 = std::max(1, 512 / std::max(nv, 1));
     const uint64_t chunk = std::max<uint64_t>(1024, (n + nch0 - 1) / nch0);
     const int nch = (int)((n + chunk - 1) / chunk);
     auto need = [](DevBuf &b, size_t bytes) { if (b.bytes < bytes) b.alloc(bytes); };
     need(wk.digits, (uint64_t)g.W * B * n * 2);
-    need(wk.counts, (WB * nch + 1) * 4);
-    need(wk.sorted, (uint64_t)nv * kr.rows * n * 4 + 4);
+    const int cb = std::min(SORT_CB, g.c - 1), fb = g.c - 1 - cb, NBc = 1 << cb;
+    const uint64_t nbins = (uint64_t)nv * NBc;
+    const uint64_t nent = (uint64_t)nv * kr.rows * n;  // upper bound (zero digits drop out)
+    need(wk.counts, (nbins * nch + 1) * 4);
+    need(wk.offsets, (WB + 1) * 4);
+    need(wk.ent, nent * 4 + 4);
+    need(wk.fkey, nent + 4);
+    need(wk.sorted, nent * 4 + 4);
     need(wk.buckets, (WB * 24 + WB * 72 + 64) * 8);  // buckets + reduction tree scratch
     uint16_t *keys = static_cast<uint16_t *>(wk.digits.p);
     uint32_t *counts = static_cast<uint32_t *>(wk.counts.p);
+    uint32_t *bstart = static_cast<uint32_t *>(wk.offsets.p);
     uint32_t *sorted = static_cast<uint32_t *>(wk.sorted.p);
     const uint64_t *pts = folded ? table : d_points;
 
@@ -381,38 +550,34 @@ void msm_run_batch(MsmWork &wk, const uint64_t *d_points, const uint64_t *const 
             PNP_HIP(hipGetLastError());
         }
         dim3 grid((uint32_t)nch, (uint32_t)nv);
-        size_t lds = (size_t)g.NB * 4;
-        static bool attr_set = false;
-        if (!attr_set) {
-            PNP_HIP(hipFuncSetAttribute((const void *)k_hist,
-                                        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-            PNP_HIP(hipFuncSetAttribute((const void *)k_scatter,
-                                        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-            attr_set = true;
-        }
-        hipLaunchKernelGGL(k_hist, grid, dim3(1024), lds, s, keys, kr, g.NB, chunk, nch, counts);
+        hipLaunchKernelGGL(k_coarse_hist, grid, dim3(1024), 0, s, keys, kr, fb, NBc, chunk, nch,
+                           counts);
         PNP_HIP(hipGetLastError());
-        const uint64_t ncount = WB * nch;
+        const uint64_t ncount = nbins * nch;
         PNP_HIP(hipMemsetAsync(counts + ncount, 0, 4, s));
-        scan_u32(counts, ncount + 1, wk.offsets, s);  // counts[ncount] = total
-        hipLaunchKernelGGL(k_scatter, grid, dim3(1024), lds, s, keys, kr, g.NB, chunk, nch, counts,
-                           sorted);
+        scan_u32(counts, ncount + 1, wk.scan_tmp, s);  // counts[ncount] = total
+        uint32_t *ent = static_cast<uint32_t *>(wk.ent.p);
+        uint8_t *fk = static_cast<uint8_t *>(wk.fkey.p);
+        hipLaunchKernelGGL(k_coarse_scatter, grid, dim3(1024), 0, s, keys, kr, fb, NBc, chunk, nch,
+                           counts, ent, fk);
         PNP_HIP(hipGetLastError());
+        hipLaunchKernelGGL(k_fine_sort, dim3((uint32_t)nbins), dim3(1024), 0, s, ent, fk, counts,
+                           nch, fb, bstart, sorted);
+        PNP_HIP(hipGetLastError());
+        PNP_HIP(hipMemcpyAsync(bstart + WB, counts + ncount, 4, hipMemcpyDeviceToDevice, s));
         uint64_t *bk = wk.buckets.u64();
         hipEvent_t ev0 = nullptr;
         if (wk.timer) wk.timer->begin("msm_accumulate", s, ev0);
-        // balanced accumulate: S entries per thread (upper bound: every entry non-zero)
-        // (>= 64, or ~2^20 lanes: every bucket piece beyond the first costs an
-        // addition in msm_merge_pieces)
-        const uint64_t nent = (uint64_t)nv * kr.rows * n;
+        // balanced accumulate: S entries per thread, S >= 64 or ~2^20 lanes (every
+        // bucket piece beyond the first costs an addition in msm_merge_pieces)
         const uint32_t S = (uint32_t)std::max<uint64_t>(64, (nent >> 20) & ~7ULL);
         const uint64_t nthr = (nent + S - 1) / S;
         need(wk.seg, nthr * 2 * 24 * 8);
         uint64_t *head = wk.seg.u64(), *tail = head + nthr * 24;
         hipLaunchKernelGGL(k_accumulate_flat, dim3((uint32_t)((nthr + 255) / 256)), dim3(256), 0,
-                           s, pts, sorted, counts, nch, WB, S, bk, head, tail);
+                           s, pts, sorted, bstart, 1, WB, S, bk, head, tail);
         PNP_HIP(hipGetLastError());
-        msm_merge_pieces(counts, nch, WB, S, (uint32_t)(nent / WB / S + 1), head, tail, bk, s);
+        msm_merge_pieces(bstart, 1, WB, S, (uint32_t)(nent / WB / S + 1), head, tail, bk, s);
         // algorithmic bytes: each point (96 B) and scalar (32 B)
         // once per window sweep
         if (wk.timer)

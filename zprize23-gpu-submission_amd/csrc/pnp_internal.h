@@ -86,7 +86,11 @@ struct KernelTimer {
 
 // ---- MSM (msm.hip) ----
 struct MsmWork {
-    DevBuf digits, sorted, counts, offsets, buckets, seg, scal, result;
+    // digits: u16 keys; counts: coarse-bin counts -> offsets (scan, scan_tmp);
+    // ent/fkey: pass-A entries and fine keys; offsets: bucket starts;
+    // sorted: entries by bucket; buckets: XYZZ buckets + reduction tree;
+    // seg: split-bucket pieces
+    DevBuf digits, sorted, counts, offsets, scan_tmp, ent, fkey, buckets, seg;
     size_t cap_n = 0;
     KernelTimer *timer = nullptr;
     // window sharding across ranks (pnp_set_msm_shard)
