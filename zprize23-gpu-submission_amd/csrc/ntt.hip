@@ -287,11 +287,16 @@ __global__ void k_pad_coset(const uint64_t *in, uint64_t *out, uint64_t n, uint6
     store_fr(out, i, x);
 }
 
-static void dif(NttTables &t, uint64_t *d, uint32_t lg, bool inverse, hipStream_t s) {
+// DIF of size 2^lg on each of the 2^(lg_total - lg) consecutive blocks of d
+static void dif(NttTables &t, uint64_t *d, uint32_t lg, bool inverse, hipStream_t s,
+                uint32_t lg_total = 0) {
+    if (lg_total < lg) lg_total = lg;
     const uint64_t *tw = ntt_twiddles(t, lg, inverse, s);
-    if (lg <= 10) {
-        hipLaunchKernelGGL(k_dif_small, dim3(1), dim3(NTT_THREADS), 0, s, d, tw, lg);
-        PNP_HIP(hipGetLastError());
+    if (lg_total < 10 || (lg <= 10 && lg_total == lg)) {
+        for (uint64_t b = 0; b < (1ULL << (lg_total - lg)); b++) {
+            hipLaunchKernelGGL(k_dif_small, dim3(1), dim3(NTT_THREADS), 0, s, d + 4 * (b << lg), tw, lg);
+            PNP_HIP(hipGetLastError());
+        }
         return;
     }
     // split lg into passes of at most 10 levels (balanced), top levels first
@@ -302,7 +307,7 @@ static void dif(NttTables &t, uint64_t *d, uint32_t lg, bool inverse, hipStream_
         int k = (rem + (npass - p) - 1) / (npass - p);
         rem -= k;
         uint32_t lg_hlo = top - k;  // smallest half size of this pass = 2^(top-k)
-        uint64_t groups = (1ULL << lg) >> k;
+        uint64_t groups = (1ULL << lg_total) >> k;
         uint32_t blocks = (uint32_t)(groups / (TILE >> k));
         switch (k) {
 #define PNP_CASE(KK)                                                                          \
@@ -354,13 +359,48 @@ void ntt_run(NttTables &t, uint64_t *d, uint32_t lg, bool inverse, bool coset, h
     bitrev(d, lg, sc, s);
 }
 
+// out[b n + j] = in[j] * T[b n + j],  T[b n + j] = (g w_8n^rev3(b))^j
+__global__ void k_lde_twist(const uint64_t *in, const uint64_t *T, uint64_t *out, uint64_t n,
+                            uint64_t N) {
+    uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    if (i >= N) return;
+    store_fr(out, i, load_fr(in, i & (n - 1)) * load_fr(T, i));
+}
+
+static const uint64_t *lde_twist_table(NttTables &t, uint32_t lg_n, hipStream_t s) {
+    auto it = t.lde_twist.find(lg_n);
+    if (it != t.lde_twist.end()) return it->second.u64();
+    const uint64_t n = 1ULL << lg_n;
+    DevBuf buf(8 * n * 32);
+    const Fr w8n = host_root(lg_n + 3), g = host_gen();
+    const uint32_t chunk = 64;
+    const uint64_t threads = (n + chunk - 1) / chunk;
+    for (uint32_t b = 0; b < 8; b++) {
+        uint32_t m = ((b & 1) << 2) | (b & 2) | ((b >> 2) & 1);  // rev3(b)
+        Fr base = g * pow_u64(w8n, m);
+        hipLaunchKernelGGL(k_powers_table, dim3((uint32_t)((threads + 255) / 256)), dim3(256), 0, s,
+                           buf.u64() + 4 * b * n, n, base, chunk);
+        PNP_HIP(hipGetLastError());
+    }
+    const uint64_t *p = buf.u64();
+    t.lde_twist.emplace(lg_n, std::move(buf));
+    return p;
+}
+
+// Ntt_coset::forward of the zero-padded n-coefficient polynomial on 8n points.
+// The top three DIF levels of a length-8n transform whose upper 7n inputs are
+// zero only copy and twist: afterwards block b (of 8, length n) holds
+// c_j g^j w_8n^(j rev3(b)).  So: one twist pass from a key-independent table,
+// then 22 (not 25) DIF levels as 8 independent size-n transforms (their
+// twiddle table is 8x smaller and stays in the MALL), then the usual 8n
+// bit reversal to natural order.
 void coset_lde8(NttTables &t, const uint64_t *in, uint64_t *out8, uint32_t lg_n, hipStream_t s) {
-    ntt_prepare_coset(t, s);
     uint64_t n = 1ULL << lg_n, N = n << 3;
-    hipLaunchKernelGGL(k_pad_coset, dim3((uint32_t)((N + 255) / 256)), dim3(256), 0, s, in, out8, n,
-                       N, t.coset_hi.u64(), t.coset_lo.u64());
+    const uint64_t *T = lde_twist_table(t, lg_n, s);
+    hipLaunchKernelGGL(k_lde_twist, dim3((uint32_t)((N + 255) / 256)), dim3(256), 0, s, in, T, out8,
+                       n, N);
     PNP_HIP(hipGetLastError());
-    dif(t, out8, lg_n + 3, false, s);
+    if (lg_n > 0) dif(t, out8, lg_n, false, s, lg_n + 3);
     Scale sc{0, Fr::one(), nullptr, nullptr};
     bitrev(out8, lg_n + 3, sc, s);
 }

@@ -54,6 +54,8 @@ struct NttTables {
     DevBuf coset_hi, coset_lo;        // g^(4096 k), g^k
     DevBuf coset_inv_hi, coset_inv_lo;  // g^-(4096 k), g^-k
     bool coset_ready = false;
+    // coset LDE twist per lg_n: (g w_8n^rev3(b))^j for block b, j < n
+    std::map<uint32_t, DevBuf> lde_twist;
 };
 const uint64_t *ntt_twiddles(NttTables &t, uint32_t lg, bool inverse, hipStream_t s);
 void ntt_prepare_coset(NttTables &t, hipStream_t s);
