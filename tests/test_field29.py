@@ -1,0 +1,164 @@
+"""CPU model of the radix-2^29 Fq arithmetic of csrc/field29.cuh (the MSM
+bucket accumulation): the limb-level Montgomery product and lifted-offset
+subtraction restated in Python, checked for exactness and for the bounds the
+kernel relies on (64-bit column accumulators never overflow, limbs stay
+< 2^29, XYZZ coordinates stay below the subtraction offsets) over long chains
+of mixed additions, against affine arithmetic on BLS12-381 G1."""
+import os
+import random
+import re
+
+import pytest
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+INC = os.path.join(HERE, "..", "zprize23-gpu-submission_amd", "csrc", "f29_consts.inc")
+Q = 0x1a0111ea397fe69a4b1ba7b6434bacd764774b84f38512bf6730d2a0f6b0f6241eabfffeb153ffffb9feffffffffaaab
+M29 = (1 << 29) - 1
+
+
+def _consts():
+    txt = open(INC).read()
+    arrs = {m.group(1): [int(x.rstrip("u"), 16) for x in m.group(2).split(",")]
+            for m in re.finditer(r"(F29_\w+)\[14\] = \{([^}]*)\}", txt)}
+    qinv = int(re.search(r"F29_QINV = (0x[0-9a-f]+)u", txt).group(1), 16)
+    return arrs, qinv
+
+
+C, QINV = _consts()
+
+
+def val(l):
+    return sum(x << (29 * i) for i, x in enumerate(l))
+
+
+def limbs(v):
+    return [(v >> (29 * i)) & M29 for i in range(13)] + [v >> (29 * 13)]
+
+
+def mul29(a, b):
+    """mul29 of field29.cuh, limb for limb."""
+    assert all(x < 2**29 for x in a + b)
+    q = C["F29_Q"]
+    m, r, acc = [0] * 14, [0] * 14, 0
+    for k in range(27):
+        for i in range(max(0, k - 13), min(k, 13) + 1):
+            acc += a[i] * b[k - i]
+        for i in range(max(0, k - 13), min(k, 14)):
+            acc += m[i] * q[k - i]
+        if k < 14:
+            m[k] = ((acc & 0xFFFFFFFF) * QINV) & M29
+            acc += m[k] * q[0]
+            assert acc & M29 == 0
+        else:
+            r[k - 14] = acc & M29
+        assert acc < 2**64
+        acc >>= 29
+    r[13] = acc
+    assert acc < 2**29
+    return r
+
+
+def sub29(a, b, K):
+    r, c = [0] * 14, 0
+    for i in range(13):
+        t = a[i] + K[i] - b[i] + c
+        assert 0 <= t < 2**32
+        r[i], c = t & M29, t >> 29
+    r[13] = a[13] + K[13] - b[13] + c
+    assert r[13] >= 0
+    return r
+
+
+R406 = 1 << 406
+
+
+def to_m(v):  # integer -> R406 Montgomery limbs
+    return limbs(v * R406 % Q)
+
+
+def from_m(l):
+    return val(l) * pow(R406, -1, Q) % Q
+
+
+def test_constants():
+    assert val(C["F29_Q"]) == Q
+    assert (QINV * Q) % 2**29 == 2**29 - 1
+    assert val(C["F29_ONE"]) == R406 % Q
+    assert val(C["F29_C384"]) == 2**384 % Q and val(C["F29_C428"]) == 2**428 % Q
+    for k, lo in (("F29_KA", 386), ("F29_KB", 389)):
+        v = val(C[k])
+        assert v % Q == 0 and 2**lo <= v < 2**(lo + 1)
+        assert all(2**29 <= x < 2**30 for x in C[k][:13])
+
+
+def test_mul_exact_and_bounded():
+    rnd = random.Random(1)
+    for _ in range(300):
+        a, b = rnd.randrange(2**391), rnd.randrange(2**391)
+        r = mul29(limbs(a), limbs(b))
+        assert val(r) % Q == a * b * pow(R406, -1, Q) % Q
+        assert val(r) < 2**382
+
+
+# ---- G1 (y^2 = x^3 + 4) affine reference
+G1X = 0x17f1d3a73197d7942695638c4fa9ac0fc3688c4f9774b905a14e3a3f171bac586c55e83ff97a1aeffb3af00adb22c6bb
+G1Y = 0x08b3f481e3aaa0f1a09e30ed741d8ae4fcf5e095d5d00af600db18cb2c04b3edd03cc744a2888ae40caa232946c5e7e1
+
+
+def aff_add(p, q):
+    (x1, y1), (x2, y2) = p, q
+    lam = (y2 - y1) * pow(x2 - x1, -1, Q) % Q
+    x3 = (lam * lam - x1 - x2) % Q
+    return x3, (lam * (x1 - x3) - y1) % Q
+
+
+def madd29(p, x2, y2):
+    """madd29 of msm.hip with the bounds of field29.cuh asserted."""
+    KA, KB = C["F29_KA"], C["F29_KB"]
+    X, Y, ZZ, ZZZ = p
+    for v in (X, Y):
+        assert val(v) < 2**389
+    u2, s2 = mul29(x2, ZZ), mul29(y2, ZZZ)
+    P, R = sub29(u2, X, KB), sub29(s2, Y, KB)
+    assert val(P) < 2**391 and val(R) < 2**391
+    pp = mul29(P, P)
+    ppp = mul29(P, pp)
+    q = mul29(X, pp)
+    x3 = sub29(sub29(sub29(mul29(R, R), ppp, KA), q, KA), q, KA)
+    assert val(x3) < 2**389
+    t = sub29(q, x3, KB)
+    assert val(t) < 2**391
+    y3 = sub29(mul29(R, t), mul29(Y, ppp), KA)
+    return x3, y3, mul29(ZZ, pp), mul29(ZZZ, ppp)
+
+
+@pytest.mark.parametrize("seed", [3, 4])
+def test_madd_chain(seed):
+    rnd = random.Random(seed)
+    pts, P = [], (G1X, G1Y)
+    for _ in range(24):  # distinct multiples of G
+        k = rnd.randrange(1, 2**64)
+        acc = None
+        base, e = P, k
+        while e:
+            if e & 1:
+                acc = base if acc is None else aff_add(acc, base)
+            x, y = base
+            lam = 3 * x * x * pow(2 * y, -1, Q) % Q
+            x3 = (lam * lam - 2 * x) % Q
+            base = (x3, (lam * (x - x3) - y) % Q)
+            e >>= 1
+        pts.append(acc)
+    ref = pts[0]
+    acc = (to_m(pts[0][0]), to_m(pts[0][1]), to_m(1), to_m(1))
+    for x, y in pts[1:]:
+        neg = rnd.random() < 0.5
+        ym = to_m(y)
+        if neg:
+            ym = sub29([0] * 14, ym, C["F29_KA"])
+            y = (-y) % Q
+        acc = madd29(acc, to_m(x), ym)
+        ref = aff_add(ref, (x, y))
+    X, Y, ZZ, ZZZ = (from_m(v) for v in acc)
+    assert X * pow(ZZ, -1, Q) % Q == ref[0]
+    assert Y * pow(ZZZ, -1, Q) % Q == ref[1]

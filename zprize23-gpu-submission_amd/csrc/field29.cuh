@@ -1,0 +1,122 @@
+// field29.cuh — BLS12-381 Fq in radix 2^29 (14 limbs), for the MSM bucket
+// accumulation on gfx950.
+//
+// Why: the 32-bit-limb Montgomery product (field.cuh) spends one
+// v_addc_co_u32 per v_mad_u64_u32 to carry the 96-bit column sums, and on
+// gfx950 both cost ~4.3 cycles per wave64 instruction (tools/ubench_ops.hip).
+// With 29-bit limbs every product is < 2^58 and a whole column (<= 28
+// products + carry) fits a 64-bit accumulator, so the product is 392 bare
+// v_mad_u64_u32 plus a shift/mask per column: ~25% fewer issue cycles.
+//
+// Representation: value V = sum l_i 2^(29 i), every limb < 2^29, Montgomery
+// with R = 2^406, NOT reduced: a product of inputs < 2^391 is < 2^382, and the
+// subtractions add a multiple of q (F29_KA ~ 2^386 > any product, F29_KB ~
+// 2^389 > any stored coordinate) whose limbs are "lifted" into [2^29, 2^30),
+// so no limb ever borrows and no conditional reduction is needed.  The bounds
+// are tracked per formula in madd29 (ec29 below) and checked by
+// tests/test_field29.py against a Python model.  Zero tests need a canonical
+// value and are done once per bucket piece (to_fq32).
+#pragma once
+#include "field.cuh"
+#include "f29_consts.inc"
+
+namespace pnp {
+
+struct F29 {
+    uint32_t l[14];
+};
+
+#define F29_M 0x1FFFFFFFu
+
+// Montgomery product a b 2^-406 (product scanning, one 64-bit accumulator)
+__device__ __forceinline__ F29 mul29(const F29 &a, const F29 &b) {
+    uint32_t m[14];
+    F29 r;
+    uint64_t acc = 0;
+#pragma unroll
+    for (int k = 0; k < 27; k++) {
+#pragma unroll
+        for (int i = (k > 13 ? k - 13 : 0); i <= (k < 13 ? k : 13); i++) acc += (uint64_t)a.l[i] * b.l[k - i];
+#pragma unroll
+        for (int i = (k > 13 ? k - 13 : 0); i < (k < 14 ? k : 14); i++) acc += (uint64_t)m[i] * F29_Q[k - i];
+        if (k < 14) {
+            m[k] = ((uint32_t)acc * F29_QINV) & F29_M;
+            acc += (uint64_t)m[k] * F29_Q[0];
+        } else {
+            r.l[k - 14] = (uint32_t)acc & F29_M;
+        }
+        acc >>= 29;
+    }
+    r.l[13] = (uint32_t)acc;
+    return r;
+}
+
+// a + K - b (K = F29_KA or F29_KB, b < K), carries normalised
+__device__ __forceinline__ F29 sub29(const F29 &a, const F29 &b, const uint32_t *K) {
+    F29 r;
+    uint32_t c = 0;
+#pragma unroll
+    for (int i = 0; i < 13; i++) {
+        uint32_t t = a.l[i] + K[i] - b.l[i] + c;
+        r.l[i] = t & F29_M;
+        c = t >> 29;
+    }
+    r.l[13] = a.l[13] + K[13] - b.l[13] + c;
+    return r;
+}
+
+// K - b
+__device__ __forceinline__ F29 neg29(const F29 &b, const uint32_t *K) {
+    F29 r;
+    uint32_t c = 0;
+#pragma unroll
+    for (int i = 0; i < 13; i++) {
+        uint32_t t = K[i] - b.l[i] + c;
+        r.l[i] = t & F29_M;
+        c = t >> 29;
+    }
+    r.l[13] = K[13] - b.l[13] + c;
+    return r;
+}
+
+__device__ __forceinline__ F29 const29(const uint32_t *c) {
+    F29 r;
+#pragma unroll
+    for (int i = 0; i < 14; i++) r.l[i] = c[i];
+    return r;
+}
+
+// 12 x 32-bit limbs -> 14 x 29-bit limbs (same integer)
+__device__ __forceinline__ F29 repack29(const uint32_t *v) {
+    F29 r;
+#pragma unroll
+    for (int j = 0; j < 14; j++) {
+        const int bit = 29 * j, w = bit >> 5, sh = bit & 31;
+        uint64_t x = v[w];
+        if (w + 1 < 12) x |= (uint64_t)v[w + 1] << 32;
+        r.l[j] = (uint32_t)(x >> sh) & F29_M;
+    }
+    return r;
+}
+
+// integer < 2q (limbs normalised, < 2^384) -> canonical Fq (12 x 32-bit limbs)
+__device__ __forceinline__ Fq unpack29(const F29 &a) {
+    Fq r;
+#pragma unroll
+    for (int w = 0; w < 12; w++) {
+        const int bit = 32 * w, j = bit / 29, sh = bit % 29;
+        uint64_t x = (uint64_t)a.l[j] >> sh;
+        if (j + 1 < 14) x |= (uint64_t)a.l[j + 1] << (29 - sh);
+        if (j + 2 < 14 && 58 - sh < 32) x |= (uint64_t)a.l[j + 2] << (58 - sh);
+        r.v[w] = (uint32_t)x;
+    }
+    reduce_once(r);
+    return r;
+}
+
+// R406-form F29 -> R384-form canonical Fq
+__device__ __forceinline__ Fq to_fq32(const F29 &a) { return unpack29(mul29(a, const29(F29_C384))); }
+// R384-form Fq (canonical) -> R406-form F29 (< 2q)
+__device__ __forceinline__ F29 from_fq32(const Fq &a) { return mul29(repack29(a.v), const29(F29_C428)); }
+
+}  // namespace pnp

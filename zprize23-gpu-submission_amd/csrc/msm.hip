@@ -37,6 +37,7 @@
 #include <algorithm>
 #include "msm_internal.h"
 #include "ec.cuh"
+#include "field29.cuh"
 
 namespace pnp {
 
@@ -361,12 +362,12 @@ __global__ __launch_bounds__(1024) void k_fine_sort(const uint32_t *ent, const u
 __device__ __forceinline__ uint32_t bucket_start(const uint32_t *offs, uint64_t u, int nch) {
     return offs[u * nch];
 }
-__global__ __launch_bounds__(256) void k_accumulate_flat(const uint64_t *points,
-                                                         const uint32_t *sorted,
-                                                         const uint32_t *offs, int nch, uint64_t U,
-                                                         uint32_t S, uint64_t *buckets,
-                                                         uint64_t *head, uint64_t *tail) {
-    uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+// The segment walk shared by the exact kernels; `ld(e)` yields the affine
+// point of sorted entry e (sign bit stripped by the caller).
+template <class LoadPt>
+__device__ __forceinline__ void segment32(uint64_t t, LoadPt ld, const uint32_t *sorted,
+                                          const uint32_t *offs, int nch, uint64_t U, uint32_t S,
+                                          uint64_t *buckets, uint64_t *head, uint64_t *tail) {
     const uint32_t total = bucket_start(offs, U, nch);
     const uint64_t lo64 = t * S;
     if (lo64 >= total) return;
@@ -394,14 +395,134 @@ __global__ __launch_bounds__(256) void k_accumulate_flat(const uint64_t *points,
             } while (next == k);
         }
         uint32_t e = sorted[k];
-        const uint64_t *p = points + 12ULL * (e & 0x7FFFFFFFu);
-        Fq x = load_fq(p), y = load_fq(p + 6);
+        Fq x, y;
+        ld(e & 0x7FFFFFFFu, x, y);
         if (e >> 31) y = neg(y);
         acc = madd(acc, x, y);
     }
     if (first) store_xyzz(head + 24 * t, acc);
     else if (next > hi) store_xyzz(tail + 24 * t, acc);
     else store_xyzz(buckets + 24 * cur, acc);
+}
+
+__global__ __launch_bounds__(256) void k_accumulate_flat(const uint64_t *points,
+                                                         const uint32_t *sorted,
+                                                         const uint32_t *offs, int nch, uint64_t U,
+                                                         uint32_t S, uint64_t *buckets,
+                                                         uint64_t *head, uint64_t *tail) {
+    uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    auto ld = [points](uint32_t i, Fq &x, Fq &y) {
+        x = load_fq(points + 12ULL * i);
+        y = load_fq(points + 12ULL * i + 6);
+    };
+    segment32(t, ld, sorted, offs, nch, U, S, buckets, head, tail);
+}
+
+// ---- radix-2^29 accumulation (field29.cuh) over the folded table in F29 form
+// (28 u32 per point: x, y in R = 2^406 Montgomery, < 2q)
+__device__ __forceinline__ F29 load29(const uint32_t *p) {
+    const uint4 *q = reinterpret_cast<const uint4 *>(p);
+    uint4 a = q[0], b = q[1], c = q[2];
+    uint2 d = *reinterpret_cast<const uint2 *>(p + 12);
+    F29 r;
+    r.l[0] = a.x; r.l[1] = a.y; r.l[2] = a.z; r.l[3] = a.w;
+    r.l[4] = b.x; r.l[5] = b.y; r.l[6] = b.z; r.l[7] = b.w;
+    r.l[8] = c.x; r.l[9] = c.y; r.l[10] = c.z; r.l[11] = c.w;
+    r.l[12] = d.x; r.l[13] = d.y;
+    return r;
+}
+struct Xyzz29 {
+    F29 x, y, zz, zzz;
+};
+// P += (x2, y2), madd-2008-s.  Bounds (see field29.cuh): products < 2^382,
+// stored coordinates < 2^389, every product input < 2^391.  No equal /
+// opposite / infinity cases: those make ZZ = 0 mod q, detected per piece.
+__device__ __forceinline__ void madd29(Xyzz29 &p, const F29 &x2, const F29 &y2) {
+    F29 u2 = mul29(x2, p.zz);
+    F29 s2 = mul29(y2, p.zzz);
+    F29 P = sub29(u2, p.x, F29_KB);
+    F29 R = sub29(s2, p.y, F29_KB);
+    F29 pp = mul29(P, P);
+    F29 ppp = mul29(P, pp);
+    F29 q = mul29(p.x, pp);
+    F29 x3 = sub29(sub29(sub29(mul29(R, R), ppp, F29_KA), q, F29_KA), q, F29_KA);
+    F29 y3 = sub29(mul29(R, sub29(q, x3, F29_KB)), mul29(p.y, ppp), F29_KA);
+    p.zz = mul29(p.zz, pp);
+    p.zzz = mul29(p.zzz, ppp);
+    p.x = x3;
+    p.y = y3;
+}
+// store as canonical R384 XYZZ; false when ZZ = 0 (a degenerate step)
+__device__ __forceinline__ bool store29(uint64_t *dst, const Xyzz29 &p) {
+    Fq zz = to_fq32(p.zz);
+    store_fq(dst, to_fq32(p.x));
+    store_fq(dst + 6, to_fq32(p.y));
+    store_fq(dst + 12, zz);
+    store_fq(dst + 18, to_fq32(p.zzz));
+    return !zz.is_zero();
+}
+
+__global__ __launch_bounds__(256) void k_accumulate29(const uint32_t *pts29, const uint32_t *sorted,
+                                                      const uint32_t *offs, uint64_t U, uint32_t S,
+                                                      uint64_t *buckets, uint64_t *head,
+                                                      uint64_t *tail, uint32_t *redo,
+                                                      uint32_t *nredo) {
+    uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    const uint32_t total = offs[U];
+    const uint64_t lo64 = t * S;
+    if (lo64 >= total) return;
+    const uint32_t lo = (uint32_t)lo64;
+    const uint32_t hi = lo + S < total ? lo + S : total;
+    uint64_t a = 0, b = U;  // start(a) <= lo < start(b)
+    while (b - a > 1) {
+        uint64_t m = (a + b) >> 1;
+        if (offs[m] <= lo) a = m; else b = m;
+    }
+    uint64_t cur = a;
+    bool first = offs[cur] < lo;
+    uint32_t next = offs[cur + 1];
+    bool ok = true, fresh = true;
+    Xyzz29 acc;
+    for (uint32_t k = lo; k < hi; k++) {
+        if (k == next) {
+            ok &= store29(first ? head + 24 * t : buckets + 24 * cur, acc);
+            first = false;
+            fresh = true;
+            do {
+                cur++;
+                next = offs[cur + 1];
+            } while (next == k);
+        }
+        uint32_t e = sorted[k];
+        const uint32_t *p = pts29 + 28ULL * (e & 0x7FFFFFFFu);
+        F29 x = load29(p), y = load29(p + 14);
+        if (e >> 31) y = neg29(y, F29_KA);
+        if (fresh) {
+            acc.x = x;
+            acc.y = y;
+            acc.zz = acc.zzz = const29(F29_ONE);
+            fresh = false;
+        } else {
+            madd29(acc, x, y);
+        }
+    }
+    ok &= store29(first ? head + 24 * t : (next > hi ? tail + 24 * t : buckets + 24 * cur), acc);
+    if (!ok) redo[atomicAdd(nredo, 1u)] = (uint32_t)t;
+}
+
+// exact 32-bit recomputation of the segments k_accumulate29 flagged
+__global__ __launch_bounds__(64) void k_accumulate_redo(const uint32_t *pts29, const uint32_t *sorted,
+                                                        const uint32_t *offs, uint64_t U, uint32_t S,
+                                                        uint64_t *buckets, uint64_t *head,
+                                                        uint64_t *tail, const uint32_t *redo,
+                                                        uint32_t nredo) {
+    uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= nredo) return;
+    auto ld = [pts29](uint32_t i, Fq &x, Fq &y) {
+        x = to_fq32(load29(pts29 + 28ULL * i));
+        y = to_fq32(load29(pts29 + 28ULL * i + 14));
+    };
+    segment32(redo[r], ld, sorted, offs, 1, U, S, buckets, head, tail);
 }
 
 // ---------------------------------------------------------------- folded table
@@ -447,23 +568,42 @@ __global__ __launch_bounds__(256) void k_table_affine(const uint64_t *xyzz, uint
     }
 }
 
+__global__ void k_table_to29(const uint64_t *T, uint64_t count, uint32_t *T29) {
+    uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    if (i >= count) return;
+    F29 x = from_fq32(load_fq(T + 12 * i)), y = from_fq32(load_fq(T + 12 * i + 6));
+    uint32_t *o = T29 + 28 * i;
+#pragma unroll
+    for (int j = 0; j < 14; j++) {
+        o[j] = x.l[j];
+        o[14 + j] = y.l[j];
+    }
+}
+
 void msm_build_table(DevBuf &tab, const uint64_t *d_points, uint64_t n, hipStream_t s) {
     MsmCfg g = msm_cfg(n);
-    tab.alloc((uint64_t)g.W * n * 96);
-    uint64_t *T = tab.u64();
+    DevBuf t32((uint64_t)g.W * n * 96);
+    uint64_t *T = t32.u64();
     PNP_HIP(hipMemcpyAsync(T, d_points, n * 96, hipMemcpyDeviceToDevice, s));
-    if (g.W == 1) return;
-    DevBuf xyzz(n * 192), pre(n * 48);
-    const uint32_t CH = 64;
-    const uint64_t lanes = (n + CH - 1) / CH;
-    for (int k = 1; k < g.W; k++) {
-        hipLaunchKernelGGL(k_table_dbl, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, s,
-                           T + (uint64_t)(k - 1) * n * 12, n, g.c, xyzz.u64());
-        PNP_HIP(hipGetLastError());
-        hipLaunchKernelGGL(k_table_affine, dim3((uint32_t)((lanes + 255) / 256)), dim3(256), 0, s,
-                           xyzz.u64(), n, CH, pre.u64(), T + (uint64_t)k * n * 12);
-        PNP_HIP(hipGetLastError());
+    if (g.W > 1) {
+        DevBuf xyzz(n * 192), pre(n * 48);
+        const uint32_t CH = 64;
+        const uint64_t lanes = (n + CH - 1) / CH;
+        for (int k = 1; k < g.W; k++) {
+            hipLaunchKernelGGL(k_table_dbl, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, s,
+                               T + (uint64_t)(k - 1) * n * 12, n, g.c, xyzz.u64());
+            PNP_HIP(hipGetLastError());
+            hipLaunchKernelGGL(k_table_affine, dim3((uint32_t)((lanes + 255) / 256)), dim3(256), 0, s,
+                               xyzz.u64(), n, CH, pre.u64(), T + (uint64_t)k * n * 12);
+            PNP_HIP(hipGetLastError());
+        }
+        PNP_HIP(hipStreamSynchronize(s));
     }
+    const uint64_t count = (uint64_t)g.W * n;
+    tab.alloc(count * 112);
+    hipLaunchKernelGGL(k_table_to29, dim3((uint32_t)((count + 255) / 256)), dim3(256), 0, s, T, count,
+                       static_cast<uint32_t *>(tab.p));
+    PNP_HIP(hipGetLastError());
     PNP_HIP(hipStreamSynchronize(s));
 }
 
@@ -574,9 +714,27 @@ void msm_run_batch(MsmWork &wk, const uint64_t *d_points, const uint64_t *const 
         const uint64_t nthr = (nent + S - 1) / S;
         need(wk.seg, nthr * 2 * 24 * 8);
         uint64_t *head = wk.seg.u64(), *tail = head + nthr * 24;
-        hipLaunchKernelGGL(k_accumulate_flat, dim3((uint32_t)((nthr + 255) / 256)), dim3(256), 0,
-                           s, pts, sorted, bstart, 1, WB, S, bk, head, tail);
-        PNP_HIP(hipGetLastError());
+        if (folded) {
+            need(wk.redo, nthr * 4 + 16);
+            uint32_t *nredo = static_cast<uint32_t *>(wk.redo.p), *redo = nredo + 4;
+            PNP_HIP(hipMemsetAsync(nredo, 0, 4, s));
+            const uint32_t *t29 = reinterpret_cast<const uint32_t *>(table);
+            hipLaunchKernelGGL(k_accumulate29, dim3((uint32_t)((nthr + 255) / 256)), dim3(256), 0,
+                               s, t29, sorted, bstart, WB, S, bk, head, tail, redo, nredo);
+            PNP_HIP(hipGetLastError());
+            uint32_t h_redo = 0;
+            PNP_HIP(hipMemcpyAsync(&h_redo, nredo, 4, hipMemcpyDeviceToHost, s));
+            PNP_HIP(hipStreamSynchronize(s));
+            if (h_redo) {  // equal / opposite points or infinity inside a piece
+                hipLaunchKernelGGL(k_accumulate_redo, dim3((h_redo + 63) / 64), dim3(64), 0, s, t29,
+                                   sorted, bstart, WB, S, bk, head, tail, redo, h_redo);
+                PNP_HIP(hipGetLastError());
+            }
+        } else {
+            hipLaunchKernelGGL(k_accumulate_flat, dim3((uint32_t)((nthr + 255) / 256)), dim3(256), 0,
+                               s, pts, sorted, bstart, 1, WB, S, bk, head, tail);
+            PNP_HIP(hipGetLastError());
+        }
         msm_merge_pieces(bstart, 1, WB, S, (uint32_t)(nent / WB / S + 1), head, tail, bk, s);
         // algorithmic bytes: each point (96 B) and scalar (32 B)
         // once per window sweep

@@ -92,7 +92,8 @@ struct MsmWork {
     // ent/fkey: pass-A entries and fine keys; offsets: bucket starts;
     // sorted: entries by bucket; buckets: XYZZ buckets + reduction tree;
     // seg: split-bucket pieces
-    DevBuf digits, sorted, counts, offsets, scan_tmp, ent, fkey, buckets, seg;
+    // redo: segments the radix-2^29 accumulation hands back to the exact path
+    DevBuf digits, sorted, counts, offsets, scan_tmp, ent, fkey, buckets, seg, redo;
     size_t cap_n = 0;
     KernelTimer *timer = nullptr;
     // window sharding across ranks (pnp_set_msm_shard)
@@ -108,7 +109,8 @@ void msm_run(MsmWork &w, const uint64_t *d_points, const uint64_t *d_scalars_mon
              uint64_t *h_xyzz, hipStream_t s, const uint64_t *table = nullptr);
 void msm_run_batch(MsmWork &w, const uint64_t *d_points, const uint64_t *const *d_scalars, int B,
                    uint64_t n, uint64_t *h_xyzz, hipStream_t s, const uint64_t *table = nullptr);
-// T[k*n + i] = 2^(c*k) P_i, k < W (msm_cfg(n)), affine Montgomery, 96 B per point
+// T[k*n + i] = 2^(c*k) P_i, k < W (msm_cfg(n)), affine, in the radix-2^29
+// form of field29.cuh (x, y: 14 u32 each, 112 B per point)
 void msm_build_table(DevBuf &tab, const uint64_t *d_points, uint64_t n, hipStream_t s);
 // host: XYZZ -> affine Montgomery (inf -> (0, one))
 void xyzz_to_affine_host(const uint64_t *xyzz, uint64_t *aff12);
