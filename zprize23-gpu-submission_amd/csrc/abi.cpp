@@ -39,11 +39,17 @@ void DevBuf::release() {
     bytes = 0;
 }
 
+// folded table of this rank's point range (msm_point_range) of the first n
+// SRS points, rebuilt when n or the sharding changes
 const uint64_t *commit_table(pnp_ctx *ctx, uint64_t n) {
-    if (ctx->ck_table_n != n) {
+    uint64_t p0, p1;
+    msm_point_range(n, ctx->msm.rank, ctx->msm.world, p0, p1);
+    if (ctx->ck_table_n != n || ctx->ck_table_p0 != p0 || ctx->ck_table_p1 != p1) {
         ctx->ck_table_n = 0;
-        msm_build_table(ctx->ck_table, ctx->ck_dev, n, ctx->stream);
+        msm_build_table(ctx->ck_table, ctx->ck_dev + 12 * p0, p1 - p0, ctx->msm.fold_c, ctx->stream);
         ctx->ck_table_n = n;
+        ctx->ck_table_p0 = p0;
+        ctx->ck_table_p1 = p1;
     }
     return ctx->ck_table.u64();
 }
@@ -134,6 +140,7 @@ int pnp_ctx_create(int device, pnp_ctx **out) {
     pnp_ctx *c = new pnp_ctx();
     try {
         c->device = device;
+        if (const char *e = getenv("PNP_FOLD_C")) c->msm.fold_c = atoi(e);  // experiments
         PNP_HIP(hipSetDevice(device));
         PNP_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     } catch (const Error &e) {

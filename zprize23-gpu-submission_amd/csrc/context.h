@@ -34,7 +34,7 @@ struct pnp_ctx {
     // folded MSM table of the first ck_table_n SRS points (msm_build_table),
     // built on the first commitment of that size
     pnp::DevBuf ck_table;
-    uint64_t ck_table_n = 0;
+    uint64_t ck_table_n = 0, ck_table_p0 = 0, ck_table_p1 = 0;
 
     // ---- per-proof working set (sized on first use, reused) ----
     std::map<std::string, pnp::DevBuf> work;

@@ -18,7 +18,8 @@
 //
 // MI355X design (no cooperative kernels, no CPU bucket fold):
 //   1. k_digits         : signed c-bit digits, |d| <= 2^(c-1), one u16 key per
-//                         (window, point) — key = (|d|-1) | sign<<15, 0xFFFF = 0.
+//                         (window, point) — u32 key = (|d|-1) | sign<<31,
+//                         KEY_ZERO for d = 0.
 //   2. k_hist           : one workgroup per (virtual window, chunk of points)
 //                         builds the chunk's bucket histogram in LDS (2^(c-1)
 //                         u32 <= 128 KiB) over all the key rows of its virtual
@@ -42,7 +43,8 @@
 namespace pnp {
 
 // ---------------------------------------------------------------- 1. digits
-__global__ void k_digits(const uint64_t *scalars, uint64_t n, int c, int W, uint16_t *keys) {
+constexpr uint32_t KEY_ZERO = 0xFFFFFFFFu;
+__global__ void k_digits(const uint64_t *scalars, uint64_t n, int c, int W, uint32_t *keys) {
     uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
     if (i >= n) return;
     Fr s = from_mont(load_fr(scalars, i));
@@ -55,16 +57,16 @@ __global__ void k_digits(const uint64_t *scalars, uint64_t n, int c, int W, uint
         if (li + 1 < 8) word |= (uint64_t)s.v[li + 1] << 32;
         uint32_t raw = (uint32_t)(word >> sh) & ((1u << c) - 1);
         raw += carry;
-        uint16_t key = 0xFFFF;
+        uint32_t key = KEY_ZERO;
         if (raw > NB) {
             uint32_t mag = (NB << 1) - raw;  // |raw - 2^c|, 0 when raw = 2^c
             carry = 1;
-            if (mag) key = (uint16_t)((mag - 1) | 0x8000u);
+            if (mag) key = (mag - 1) | 0x80000000u;
         } else {
             carry = 0;
-            if (raw) key = (uint16_t)(raw - 1);
+            if (raw) key = raw - 1;
         }
-        // for c = 16 the top window never carries (scalars < 2^255)
+        // the top window never carries: W c >= 255 + 1 for the configured c (scalars < 2^255)
         keys[(uint64_t)w * n + i] = key;
     }
 }
@@ -88,8 +90,9 @@ struct KeyRows {
 // bin's entries leave as one run (a one-pass scatter straight to 2^15 buckets
 // wrote ~8x its payload to HBM).  Keys, fine keys and entries are read four
 // per lane (8 / 4 / 16-byte loads).
-constexpr int SORT_CB = 7;
-__global__ __launch_bounds__(1024) void k_coarse_hist(const uint16_t *keys, KeyRows kr, int fb,
+constexpr int SORT_CB = 8;
+constexpr int SORT_FB_MAX = 11;
+__global__ __launch_bounds__(1024) void k_coarse_hist(const uint32_t *keys, KeyRows kr, int fb,
                                                       int NBc, uint64_t chunk, int nch,
                                                       uint32_t *counts) {
     __shared__ uint32_t hist[1 << SORT_CB];
@@ -98,22 +101,22 @@ __global__ __launch_bounds__(1024) void k_coarse_hist(const uint16_t *keys, KeyR
     __syncthreads();
     const uint64_t n = kr.n;
     uint64_t lo = (uint64_t)ch * chunk, hi = lo + chunk < n ? lo + chunk : n;
-    const uint16_t *kb = keys + ((uint64_t)v * kr.vstride + kr.off) * n;
-    const bool vec = ((n | chunk) & 3) == 0;  // four keys per 8-byte load
+    const uint32_t *kb = keys + ((uint64_t)v * kr.vstride + kr.off) * n;
+    const bool vec = ((n | chunk) & 3) == 0;  // four keys per 16-byte load
     for (int r = 0; r < kr.rows; r++) {
-        const uint16_t *k = kb + (uint64_t)r * n;
+        const uint32_t *k = kb + (uint64_t)r * n;
         if (vec) {
             for (uint64_t i = lo + 4 * threadIdx.x; i < hi; i += 4 * blockDim.x) {
-                uint2 q = *reinterpret_cast<const uint2 *>(k + i);
-                uint32_t w[4] = {q.x & 0xFFFF, q.x >> 16, q.y & 0xFFFF, q.y >> 16};
+                uint4 q = *reinterpret_cast<const uint4 *>(k + i);
+                uint32_t w[4] = {q.x, q.y, q.z, q.w};
 #pragma unroll
                 for (int j = 0; j < 4; j++)
-                    if (w[j] != 0xFFFF) atomicAdd(&hist[(w[j] & 0x7FFF) >> fb], 1u);
+                    if (w[j] != KEY_ZERO) atomicAdd(&hist[(w[j] & 0x7FFFFFFFu) >> fb], 1u);
             }
         } else {
             for (uint64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) {
-                uint16_t key = k[i];
-                if (key != 0xFFFF) atomicAdd(&hist[(key & 0x7FFF) >> fb], 1u);
+                uint32_t key = k[i];
+                if (key != KEY_ZERO) atomicAdd(&hist[(key & 0x7FFFFFFFu) >> fb], 1u);
             }
         }
     }
@@ -209,13 +212,13 @@ __device__ __forceinline__ void tile_scan(uint32_t *lh, uint32_t *lofs, int nb) 
     }
 }
 
-__global__ __launch_bounds__(1024) void k_coarse_scatter(const uint16_t *keys, KeyRows kr, int fb,
+__global__ __launch_bounds__(1024) void k_coarse_scatter(const uint32_t *keys, KeyRows kr, int fb,
                                                          int NBc, uint64_t chunk, int nch,
                                                          const uint32_t *offs, uint32_t *ent,
-                                                         uint8_t *fk) {
+                                                         uint16_t *fk) {
     __shared__ uint32_t cur[1 << SORT_CB], lh[1 << SORT_CB], lofs[1 << SORT_CB];
     __shared__ uint32_t st_e[TILE_K];
-    __shared__ uint16_t st_m[TILE_K];
+    __shared__ uint32_t st_m[TILE_K];
     const int v = blockIdx.y, ch = blockIdx.x;
     for (int b = threadIdx.x; b < NBc; b += blockDim.x) {
         cur[b] = offs[((uint64_t)v * NBc + b) * nch + ch];
@@ -225,33 +228,33 @@ __global__ __launch_bounds__(1024) void k_coarse_scatter(const uint16_t *keys, K
     const uint64_t n = kr.n;
     const uint32_t fmask = (1u << fb) - 1;
     uint64_t lo = (uint64_t)ch * chunk, hi = lo + chunk < n ? lo + chunk : n;
-    const uint16_t *kb = keys + ((uint64_t)v * kr.vstride + kr.off) * n;
+    const uint32_t *kb = keys + ((uint64_t)v * kr.vstride + kr.off) * n;
     const bool vec = ((n | chunk) & 3) == 0;
     for (int r = 0; r < kr.rows; r++) {
-        const uint16_t *k = kb + (uint64_t)r * n;
+        const uint32_t *k = kb + (uint64_t)r * n;
         const uint32_t idb = (uint32_t)((kr.id_row0 + r) * kr.id_mul);
         for (uint64_t tb = lo; tb < hi; tb += TILE_K) {
             const uint64_t i0 = tb + 4 * threadIdx.x;
             uint32_t key[4], rank[4];
             if (vec && i0 + 4 <= hi) {
-                uint2 q = *reinterpret_cast<const uint2 *>(k + i0);
-                key[0] = q.x & 0xFFFF; key[1] = q.x >> 16; key[2] = q.y & 0xFFFF; key[3] = q.y >> 16;
+                uint4 q = *reinterpret_cast<const uint4 *>(k + i0);
+                key[0] = q.x; key[1] = q.y; key[2] = q.z; key[3] = q.w;
             } else {
 #pragma unroll
-                for (int j = 0; j < 4; j++) key[j] = i0 + j < hi ? k[i0 + j] : 0xFFFF;
+                for (int j = 0; j < 4; j++) key[j] = i0 + j < hi ? k[i0 + j] : KEY_ZERO;
             }
 #pragma unroll
             for (int j = 0; j < 4; j++)
-                if (key[j] != 0xFFFF) rank[j] = atomicAdd(&lh[(key[j] & 0x7FFF) >> fb], 1u);
+                if (key[j] != KEY_ZERO) rank[j] = atomicAdd(&lh[(key[j] & 0x7FFFFFFFu) >> fb], 1u);
             __syncthreads();
             tile_scan(lh, lofs, NBc);
             __syncthreads();
 #pragma unroll
             for (int j = 0; j < 4; j++) {
-                if (key[j] == 0xFFFF) continue;
-                uint32_t mag = key[j] & 0x7FFF, at = lofs[mag >> fb] + rank[j];
-                st_e[at] = (idb + (uint32_t)(i0 + j)) | ((key[j] >> 15) << 31);
-                st_m[at] = (uint16_t)mag;
+                if (key[j] == KEY_ZERO) continue;
+                uint32_t mag = key[j] & 0x7FFFFFFFu, at = lofs[mag >> fb] + rank[j];
+                st_e[at] = (idb + (uint32_t)(i0 + j)) | (key[j] & 0x80000000u);
+                st_m[at] = mag;
             }
             __syncthreads();
             const uint32_t total = lofs[NBc - 1] + lh[NBc - 1];
@@ -259,7 +262,7 @@ __global__ __launch_bounds__(1024) void k_coarse_scatter(const uint16_t *keys, K
                 uint32_t mag = st_m[x], bn = mag >> fb;
                 uint32_t pos = cur[bn] + x - lofs[bn];
                 ent[pos] = st_e[x];
-                fk[pos] = (uint8_t)(mag & fmask);
+                fk[pos] = (uint16_t)(mag & fmask);
             }
             __syncthreads();
             for (int b = threadIdx.x; b < NBc; b += blockDim.x) {
@@ -276,43 +279,38 @@ __global__ __launch_bounds__(1024) void k_coarse_scatter(const uint16_t *keys, K
 // Histogram first (bucket starts), then tiles of 8192 entries counting-sorted
 // in LDS and written out one run per fine bin (~32 entries at 2^22).
 constexpr int TILE_F = 8192;
-__global__ __launch_bounds__(1024) void k_fine_sort(const uint32_t *ent, const uint8_t *fk,
+__global__ __launch_bounds__(1024) void k_fine_sort(const uint32_t *ent, const uint16_t *fk,
                                                     const uint32_t *coffs, int nch, int fb,
                                                     uint32_t *bstart, uint32_t *sorted) {
-    __shared__ uint32_t h[256], lh[256], lofs[256];
+    __shared__ uint32_t h[1 << SORT_FB_MAX], lh[1 << SORT_FB_MAX], lofs[1 << SORT_FB_MAX];
     __shared__ uint32_t st_e[TILE_F];
-    __shared__ uint8_t st_f[TILE_F];
+    __shared__ uint16_t st_f[TILE_F];
     const uint64_t p = blockIdx.x;
     const uint32_t ps = coffs[p * nch], pe = coffs[(p + 1) * nch];
     const int NF = 1 << fb;
     for (int f = threadIdx.x; f < NF; f += blockDim.x) h[f] = lh[f] = 0;
     __syncthreads();
-    // [a, b): 4-aligned body read as uchar4; the rest one by one
+    // [a, b): 4-aligned body read as 4 x u16; the rest one by one
     const uint32_t a = std::min((ps + 3) & ~3u, pe), b = std::max(pe & ~3u, a);
     for (uint32_t k = a + 4 * threadIdx.x; k < b; k += 4 * blockDim.x) {
-        uint32_t q = *reinterpret_cast<const uint32_t *>(fk + k);
-        atomicAdd(&h[q & 0xFF], 1u);
-        atomicAdd(&h[(q >> 8) & 0xFF], 1u);
-        atomicAdd(&h[(q >> 16) & 0xFF], 1u);
-        atomicAdd(&h[q >> 24], 1u);
+        uint2 q = *reinterpret_cast<const uint2 *>(fk + k);
+        atomicAdd(&h[q.x & 0xFFFF], 1u);
+        atomicAdd(&h[q.x >> 16], 1u);
+        atomicAdd(&h[q.y & 0xFFFF], 1u);
+        atomicAdd(&h[q.y >> 16], 1u);
     }
     for (uint32_t k = ps + threadIdx.x; k < a; k += blockDim.x) atomicAdd(&h[fk[k]], 1u);
     for (uint32_t k = b + threadIdx.x; k < pe; k += blockDim.x) atomicAdd(&h[fk[k]], 1u);
     __syncthreads();
-    if (threadIdx.x == 0) {
-        uint32_t run = ps;
-        for (int f = 0; f < NF; f++) {
-            uint32_t c = h[f];
-            h[f] = run;  // h becomes the global cursor of bin f
-            run += c;
-        }
-    }
+    tile_scan(h, lofs, NF);
+    __syncthreads();
+    for (int f = threadIdx.x; f < NF; f += blockDim.x) h[f] = ps + lofs[f];  // cursor of fine bin f
     __syncthreads();
     for (int f = threadIdx.x; f < NF; f += blockDim.x) bstart[p * NF + f] = h[f];
     constexpr int PER = TILE_F / 1024;
     for (uint32_t tb = ps; tb < pe; tb += TILE_F) {
         uint32_t e[PER], rank[PER];
-        uint8_t f[PER];
+        uint32_t f[PER];
 #pragma unroll
         for (int j = 0; j < PER; j++) {
             uint32_t k = tb + threadIdx.x + j * 1024;  // coalesced, one entry per lane per step
@@ -580,8 +578,8 @@ __global__ void k_table_to29(const uint64_t *T, uint64_t count, uint32_t *T29) {
     }
 }
 
-void msm_build_table(DevBuf &tab, const uint64_t *d_points, uint64_t n, hipStream_t s) {
-    MsmCfg g = msm_cfg(n);
+void msm_build_table(DevBuf &tab, const uint64_t *d_points, uint64_t n, int c, hipStream_t s) {
+    MsmCfg g = msm_cfg(n, c);
     DevBuf t32((uint64_t)g.W * n * 96);
     uint64_t *T = t32.u64();
     PNP_HIP(hipMemcpyAsync(T, d_points, n * 96, hipMemcpyDeviceToDevice, s));
@@ -623,38 +621,31 @@ static Xyzz get_xyzz(const uint64_t *e) {
     return p;
 }
 
-// B independent MSMs over the same n points.  Per-window layout: the B*W
-// windows are "virtual windows" of NB buckets each, sharded across ranks.
-// Folded layout (table != nullptr): virtual window b = MSM b with the W key
-// rows of its windows; ranks shard the W windows, every rank reduces B
-// partial sums.
-void msm_run_batch(MsmWork &wk, const uint64_t *d_points, const uint64_t *const *d_scalars, int B,
-                   uint64_t n, uint64_t *h_xyzz, hipStream_t s, const uint64_t *table) {
+// B independent MSMs over the same n points, on this GPU only; the B results
+// (XYZZ) land in h_xyzz.  Per-window layout: the B*W windows are "virtual
+// windows" of NB buckets each.  Folded layout (table != nullptr): virtual
+// window b = MSM b with the W key rows of its windows, one bucket set.
+static void msm_local_batch(MsmWork &wk, const uint64_t *d_points, const uint64_t *const *d_scalars,
+                            int B, uint64_t n, uint64_t *h_xyzz, hipStream_t s,
+                            const uint64_t *table) {
     if (n == 0 || B == 0) {
         for (int b = 0; b < B; b++) put_xyzz(Xyzz::inf(), h_xyzz + 24 * b);
         return;
     }
-    const MsmCfg g = msm_cfg(n);
     const bool folded = table != nullptr;
-    // units sharded across ranks: windows (folded) or virtual windows
-    const int units = folded ? g.W : g.W * B;
-    const int per = (units + wk.world - 1) / wk.world;
-    const int u0 = std::min(wk.rank * per, units);
-    const int nown = std::min(u0 + per, units) - u0;
+    const MsmCfg g = msm_cfg(n, folded ? wk.fold_c : 0);
     KeyRows kr;
     kr.n = n;
-    int nv;  // virtual windows processed on this rank
+    const int nv = folded ? B : B * g.W;  // virtual windows
     if (folded) {
-        nv = nown > 0 ? B : 0;
         kr.vstride = g.W;
-        kr.off = u0;
-        kr.rows = nown;
-        kr.id_row0 = (uint32_t)u0;
+        kr.off = 0;
+        kr.rows = g.W;
+        kr.id_row0 = 0;
         kr.id_mul = n;
     } else {
-        nv = nown;
         kr.vstride = 1;
-        kr.off = u0;
+        kr.off = 0;
         kr.rows = 1;
         kr.id_row0 = 0;
         kr.id_mul = 0;
@@ -665,26 +656,29 @@ void msm_run_batch(MsmWork &wk, const uint64_t *d_points, const uint64_t *const 
     const uint64_t chunk = std::max<uint64_t>(1024, (n + nch0 - 1) / nch0);
     const int nch = (int)((n + chunk - 1) / chunk);
     auto need = [](DevBuf &b, size_t bytes) { if (b.bytes < bytes) b.alloc(bytes); };
-    need(wk.digits, (uint64_t)g.W * B * n * 2);
+    need(wk.digits, (uint64_t)g.W * B * n * 4);
     const int cb = std::min(SORT_CB, g.c - 1), fb = g.c - 1 - cb, NBc = 1 << cb;
+    if (fb > SORT_FB_MAX) {
+        set_error("msm: window of %d bits exceeds the sort's %d", g.c, SORT_CB + SORT_FB_MAX + 1);
+        throw Error(PNP_E_ARG);
+    }
     const uint64_t nbins = (uint64_t)nv * NBc;
     const uint64_t nent = (uint64_t)nv * kr.rows * n;  // upper bound (zero digits drop out)
     need(wk.counts, (nbins * nch + 1) * 4);
     need(wk.offsets, (WB + 1) * 4);
     need(wk.ent, nent * 4 + 4);
-    need(wk.fkey, nent + 4);
+    need(wk.fkey, nent * 2 + 8);
     need(wk.sorted, nent * 4 + 4);
     need(wk.buckets, (WB * 24 + WB * 72 + 64) * 8);  // buckets + reduction tree scratch
-    uint16_t *keys = static_cast<uint16_t *>(wk.digits.p);
+    uint32_t *keys = static_cast<uint32_t *>(wk.digits.p);
     uint32_t *counts = static_cast<uint32_t *>(wk.counts.p);
     uint32_t *bstart = static_cast<uint32_t *>(wk.offsets.p);
     uint32_t *sorted = static_cast<uint32_t *>(wk.sorted.p);
     const uint64_t *pts = folded ? table : d_points;
 
     const uint64_t *res = nullptr;  // nv XYZZ window sums on the device
-    if (nv > 0) {
+    {
         for (int b = 0; b < B; b++) {
-            if (!folded && ((b + 1) * g.W <= u0 || b * g.W >= u0 + nown)) continue;
             hipLaunchKernelGGL(k_digits, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, s,
                                d_scalars[b], n, g.c, g.W, keys + (uint64_t)b * g.W * n);
             PNP_HIP(hipGetLastError());
@@ -697,7 +691,7 @@ void msm_run_batch(MsmWork &wk, const uint64_t *d_points, const uint64_t *const 
         PNP_HIP(hipMemsetAsync(counts + ncount, 0, 4, s));
         scan_u32(counts, ncount + 1, wk.scan_tmp, s);  // counts[ncount] = total
         uint32_t *ent = static_cast<uint32_t *>(wk.ent.p);
-        uint8_t *fk = static_cast<uint8_t *>(wk.fkey.p);
+        uint16_t *fk = static_cast<uint16_t *>(wk.fkey.p);
         hipLaunchKernelGGL(k_coarse_scatter, grid, dim3(1024), 0, s, keys, kr, fb, NBc, chunk, nch,
                            counts, ent, fk);
         PNP_HIP(hipGetLastError());
@@ -742,50 +736,65 @@ void msm_run_batch(MsmWork &wk, const uint64_t *d_points, const uint64_t *const 
             wk.timer->end("msm_accumulate", s, ev0, (double)n * 128.0 * nv * kr.rows / g.W);
         res = msm_reduce(bk, (uint64_t)nv, g.NB, bk + WB * 24, s);
     }
-    // gather the window sums of all ranks on the host, slot r = rank r's units
-    const int per_slot = folded ? B : per;  // XYZZ points per rank slot
-    const int total = folded ? B * wk.world : units;
-    std::vector<uint64_t> win((size_t)std::max(total, per_slot * wk.world) * 24);
-    if (wk.world == 1) {
-        PNP_HIP(hipMemcpyAsync(win.data(), res, (size_t)nv * 24 * 8, hipMemcpyDeviceToHost, s));
-        PNP_HIP(hipStreamSynchronize(s));
-    } else {
-        const uint64_t slot = (uint64_t)per_slot * 24 * 8;
-        if (wk.xbuf_bytes < slot * wk.world) {
-            set_error("msm shard: exchange buffer %llu B < %llu B",
-                      (unsigned long long)wk.xbuf_bytes, (unsigned long long)(slot * wk.world));
-            throw Error(PNP_E_ARG);
-        }
-        const uint64_t my = folded ? (uint64_t)wk.rank * B : (uint64_t)u0;
-        if (nv > 0)
-            PNP_HIP(hipMemcpyAsync(wk.xbuf + my * 24, res, (uint64_t)nv * 24 * 8,
-                                   hipMemcpyDeviceToDevice, s));
-        if (folded && nv == 0) {  // idle rank: its slot holds infinities
-            std::vector<uint64_t> inf((size_t)B * 24);
-            for (int b = 0; b < B; b++) put_xyzz(Xyzz::inf(), inf.data() + 24 * b);
-            PNP_HIP(hipMemcpyAsync(wk.xbuf + my * 24, inf.data(), inf.size() * 8,
-                                   hipMemcpyHostToDevice, s));
-        }
-        PNP_HIP(hipStreamSynchronize(s));
-        int rc = wk.allgather(wk.user, slot);
-        if (rc != 0) {
-            set_error("msm shard: all-gather callback failed (%d)", rc);
-            throw Error(PNP_E_DEVICE);
-        }
-        PNP_HIP(hipMemcpyAsync(win.data(), wk.xbuf, (size_t)total * 24 * 8, hipMemcpyDeviceToHost, s));
-        PNP_HIP(hipStreamSynchronize(s));
-    }
+    std::vector<uint64_t> win((size_t)nv * 24);
+    PNP_HIP(hipMemcpyAsync(win.data(), res, win.size() * 8, hipMemcpyDeviceToHost, s));
+    PNP_HIP(hipStreamSynchronize(s));
     if (wk.timer) wk.timer->collect();
     for (int b = 0; b < B; b++) {
         Xyzz acc = Xyzz::inf();
         if (folded) {
-            for (int r = 0; r < wk.world; r++) acc = add(acc, get_xyzz(&win[((size_t)r * B + b) * 24]));
+            acc = get_xyzz(&win[(size_t)b * 24]);
         } else {
             for (int w = g.W - 1; w >= 0; w--) {
                 for (int k = 0; k < g.c; k++) acc = dbl(acc);
                 acc = add(acc, get_xyzz(&win[((size_t)b * g.W + w) * 24]));
             }
         }
+        put_xyzz(acc, h_xyzz + 24 * b);
+    }
+}
+
+void msm_point_range(uint64_t n, int rank, int world, uint64_t &p0, uint64_t &p1) {
+    const uint64_t per = (n + world - 1) / world;
+    p0 = std::min<uint64_t>((uint64_t)rank * per, n);
+    p1 = std::min<uint64_t>(p0 + per, n);
+}
+
+// Multi-GPU: rank r takes the points [p0, p1) of msm_point_range (every
+// window; the folded table passed in covers that range), the B partial sums
+// meet in one all-gather of B XYZZ points per rank and are added on the host.
+void msm_run_batch(MsmWork &wk, const uint64_t *d_points, const uint64_t *const *d_scalars, int B,
+                   uint64_t n, uint64_t *h_xyzz, hipStream_t s, const uint64_t *table) {
+    if (wk.world == 1) {
+        msm_local_batch(wk, d_points, d_scalars, B, n, h_xyzz, s, table);
+        return;
+    }
+    uint64_t p0, p1;
+    msm_point_range(n, wk.rank, wk.world, p0, p1);
+    std::vector<const uint64_t *> sc(B);
+    for (int b = 0; b < B; b++) sc[b] = d_scalars[b] + 4 * p0;
+    std::vector<uint64_t> part((size_t)B * 24);
+    msm_local_batch(wk, d_points + 12 * p0, sc.data(), B, p1 - p0, part.data(), s, table);
+    const uint64_t slot = (uint64_t)B * 24 * 8;
+    if (wk.xbuf_bytes < slot * wk.world) {
+        set_error("msm shard: exchange buffer %llu B < %llu B", (unsigned long long)wk.xbuf_bytes,
+                  (unsigned long long)(slot * wk.world));
+        throw Error(PNP_E_ARG);
+    }
+    PNP_HIP(hipMemcpyAsync(wk.xbuf + (uint64_t)wk.rank * B * 24, part.data(), slot,
+                           hipMemcpyHostToDevice, s));
+    PNP_HIP(hipStreamSynchronize(s));
+    int rc = wk.allgather(wk.user, slot);
+    if (rc != 0) {
+        set_error("msm shard: all-gather callback failed (%d)", rc);
+        throw Error(PNP_E_DEVICE);
+    }
+    std::vector<uint64_t> all((size_t)wk.world * B * 24);
+    PNP_HIP(hipMemcpyAsync(all.data(), wk.xbuf, all.size() * 8, hipMemcpyDeviceToHost, s));
+    PNP_HIP(hipStreamSynchronize(s));
+    for (int b = 0; b < B; b++) {
+        Xyzz acc = Xyzz::inf();
+        for (int r = 0; r < wk.world; r++) acc = add(acc, get_xyzz(&all[((size_t)r * B + b) * 24]));
         put_xyzz(acc, h_xyzz + 24 * b);
     }
 }

@@ -11,11 +11,14 @@ struct MsmCfg {
     int c, W, NB;
 };
 
-inline MsmCfg msm_cfg(uint64_t n) {
+// c = 0: the default for n; W c >= 256 so the top window of a scalar < 2^255
+// never carries out of its signed digit
+inline MsmCfg msm_cfg(uint64_t n, int c = 0) {
     MsmCfg g;
     int lg = 0;
     while ((1ULL << lg) < n) lg++;
     g.c = lg >= 20 ? 16 : (lg - 3 < 4 ? 4 : lg - 3);
+    if (c > 0) g.c = c;
     g.W = (256 + g.c - 1) / g.c;
     g.NB = 1 << (g.c - 1);
     return g;

@@ -96,7 +96,9 @@ struct MsmWork {
     DevBuf digits, sorted, counts, offsets, scan_tmp, ent, fkey, buckets, seg, redo;
     size_t cap_n = 0;
     KernelTimer *timer = nullptr;
-    // window sharding across ranks (pnp_set_msm_shard)
+    // point-range sharding across ranks (pnp_set_msm_shard)
+    // window bits of the folded layout (msm_cfg default when 0; PNP_FOLD_C)
+    int fold_c = 0;
     int rank = 0, world = 1;
     pnp_allgather_fn allgather = nullptr;
     void *user = nullptr;
@@ -109,9 +111,11 @@ void msm_run(MsmWork &w, const uint64_t *d_points, const uint64_t *d_scalars_mon
              uint64_t *h_xyzz, hipStream_t s, const uint64_t *table = nullptr);
 void msm_run_batch(MsmWork &w, const uint64_t *d_points, const uint64_t *const *d_scalars, int B,
                    uint64_t n, uint64_t *h_xyzz, hipStream_t s, const uint64_t *table = nullptr);
+// multi-GPU MSMs: the points [p0, p1) rank `rank` of `world` takes
+void msm_point_range(uint64_t n, int rank, int world, uint64_t &p0, uint64_t &p1);
 // T[k*n + i] = 2^(c*k) P_i, k < W (msm_cfg(n)), affine, in the radix-2^29
 // form of field29.cuh (x, y: 14 u32 each, 112 B per point)
-void msm_build_table(DevBuf &tab, const uint64_t *d_points, uint64_t n, hipStream_t s);
+void msm_build_table(DevBuf &tab, const uint64_t *d_points, uint64_t n, int c, hipStream_t s);
 // host: XYZZ -> affine Montgomery (inf -> (0, one))
 void xyzz_to_affine_host(const uint64_t *xyzz, uint64_t *aff12);
 
