@@ -173,9 +173,10 @@ def main():
     ctx = pnp.Context(local)
     gates = min(args.gates, 1 << args.lg)
     t0 = time.perf_counter()
-    if world > 1:  # window-sharded MSMs, exchange over RCCL (one in-place all-gather per batch)
-        from pnp.shard import WindowExchange
-        ctx.set_msm_shard(WindowExchange(rank, world, device=torch.device("cuda", local)))
+    if world > 1:  # sharded MSMs + distributed round 4, exchanges over RCCL
+        from pnp.shard import WindowExchange, a2a_bytes_for
+        ctx.set_msm_shard(WindowExchange(rank, world, device=torch.device("cuda", local),
+                                         a2a_bytes=a2a_bytes_for(args.lg, world)))
     syn = Synthetic(ctx, args.lg, gates, seed=1)  # same instance on every rank
     ctx.load_prover_key(syn.pk, syn.n, device_ptrs=True)
     ctx.load_commit_key(syn.ck, syn.n, device_ptrs=True)

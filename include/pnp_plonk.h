@@ -240,19 +240,34 @@ int pnp_kernel_stats(pnp_ctx *ctx, const char *name, double *total_ms, int *laun
  * windows it processed). */
 int pnp_kernel_bytes(pnp_ctx *ctx, const char *name, double *bytes);
 
-/* Multi-GPU: window-sharded MSM (one process per GPU, every rank runs
- * pnp_prove on the same inputs).  Each MSM batch's virtual windows (c-bit
- * windows x batched MSMs) are split into `world` contiguous slices of
- * ceil(WW/world); rank r accumulates and reduces slice r only.  The library
- * then writes its slice's window sums (XYZZ, 192 B each) to
- * d_xbuf + r * bytes_per_rank, synchronizes its stream and calls
- * allgather(user, bytes_per_rank), which must leave every rank's slice at its
- * offset in d_xbuf on every rank (an in-place all-gather, e.g. RCCL) and
- * return 0 once the data is visible to the device.  All other work is
- * replicated, so every rank returns the same ProofC.  world = 1 disables. */
+/* Multi-GPU (one process per GPU, every rank runs pnp_prove on the same
+ * inputs and returns the same ProofC).
+ *
+ * pnp_set_msm_shard: MSMs are sharded by point range — rank r takes points
+ * [r*ceil(n/world), ...) over every window (with the folded table of that
+ * range) and writes its B partial sums (XYZZ, 192 B each) to
+ * d_xbuf + r * bytes_per_rank; after synchronizing its stream the library
+ * calls allgather(user, bytes_per_rank), which must leave every rank's slot at
+ * its offset in d_xbuf on every rank (an in-place all-gather, e.g. RCCL) and
+ * return 0 once the data is visible to the device.  The same exchange carries
+ * a few scalars per rank (split polynomial divisions, chunk flags).
+ * world = 1 disables.
+ *
+ * pnp_set_exchange_a2a (optional, before pnp_load_prover_key; world must
+ * divide 8): distributes gen_proof's round 4 — rank r owns blocks
+ * [r*8/world, (r+1)*8/world) of the 8n coset (residues i mod 8) for the LDEs
+ * and the quotient, and coefficient range r of the quotient chunks, the
+ * linearisation and the opening witnesses.  One all-to-all moves the inverse
+ * block transforms: the library fills world slots of bytes_per_peer at
+ * d_a2a (slot s for rank s) and calls alltoall(user, bytes_per_peer), which
+ * must leave the slot rank s sent to this rank at
+ * d_a2a + (world + s) * bytes_per_peer. */
 typedef int (*pnp_allgather_fn)(void *user, uint64_t bytes_per_rank);
+typedef int (*pnp_alltoall_fn)(void *user, uint64_t bytes_per_peer);
 int pnp_set_msm_shard(pnp_ctx *ctx, int rank, int world, pnp_allgather_fn allgather,
                       void *user, uint64_t *d_xbuf, uint64_t xbuf_bytes);
+int pnp_set_exchange_a2a(pnp_ctx *ctx, pnp_alltoall_fn alltoall, void *user, uint64_t *d_a2a,
+                         uint64_t a2a_bytes);
 
 /* ------------------------------------------------------------------ */
 /* 3. Operator API on HBM pointers (mirrors PLONK/utils/function.cuh) */

@@ -4,9 +4,10 @@
         python shard_worker.py {cpu|gpu} OUT_PREFIX [lg seed]
 
 cpu: exercises pnp.shard.WindowExchange over gloo with host tensors.
-gpu: every rank proves the same seeded instance on cuda:0 with window-sharded
-     MSMs (gloo exchange through host memory, since the ranks share one GPU)
-     and writes its ProofC bytes to OUT_PREFIX.<rank>."""
+gpu: every rank proves the same seeded instance on cuda:0 with point-range
+     sharded MSMs and, when world divides 8, the distributed round 4 (gloo
+     exchanges through host memory, since the ranks share one GPU) and writes
+     its ProofC bytes to OUT_PREFIX.<rank>."""
 import os
 import sys
 
@@ -31,6 +32,15 @@ def main():
             exp = torch.cat([torch.arange(w) + 1000 * (r + 1) for r in range(world)])
             assert torch.equal(ex.buf[:w * world], exp), (w, ex.buf[:w * world])
             assert int(ex.buf[w * world:].abs().sum()) == 0
+        # all-to-all: slot s of rank r carries (r, s); afterwards receive slot s
+        # holds what rank s sent to this rank
+        ex2 = WindowExchange(rank, world, capacity_bytes=1 << 12, a2a_bytes=2 * world * 5 * 8)
+        for s in range(world):
+            ex2.a2a[5 * s:5 * s + 5] = torch.arange(5) + 100 * rank + 10 * s
+        ex2.alltoall(5 * 8)
+        for s in range(world):
+            got = ex2.a2a[5 * (world + s):5 * (world + s) + 5]
+            assert torch.equal(got, torch.arange(5) + 100 * s + 10 * rank), (s, got)
         cb = ex.c_callback()
         assert cb(None, 24 * 8) == 0 and ex.calls == 4
         assert cb(None, 1 << 20) == 1 and ex.error is not None  # oversize slot -> error code
@@ -43,12 +53,14 @@ def main():
         from pnp_testlib import Inputs
         inp = Inputs(lg, seed)
         ctx = pnp.Context(0)
-        ex = WindowExchange(rank, world, device="cuda")
+        from pnp.shard import a2a_bytes_for
+        ex = WindowExchange(rank, world, device="cuda", a2a_bytes=a2a_bytes_for(lg, world))
         ctx.set_msm_shard(ex)
         ctx.load_prover_key(inp.pk, inp.n, device_ptrs=False)
         ctx.load_commit_key(inp.ck, inp.n, device_ptrs=False)
         proof = ctx.prove(inp.circuit, device_ptrs=False)
         assert ex.calls > 0
+        assert (ex.a2a_calls > 0) == (8 % world == 0)
         with open(f"{out}.{rank}", "wb") as f:
             f.write(abi.proof_to_bytes(proof))
         ctx.close()

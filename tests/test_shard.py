@@ -1,9 +1,12 @@
-"""Multi-rank paths: window-sharded MSM exchange.
+"""Multi-rank paths: point-range sharded MSMs and the
+distributed round 4.
 
-CPU: world_size-2 gloo ranks exercise the in-place slot all-gather.
-GPU: 2 and 3 ranks share the one GPU (gloo exchange through host memory) and
-must each return the oracle's ProofC byte for byte — the 3-rank case splits
-the virtual windows unevenly."""
+CPU: world_size-2 gloo ranks exercise the in-place slot all-gather and the
+all-to-all.
+GPU: 2, 3 and 4 ranks share the one GPU (gloo exchanges through host memory)
+and must each return the oracle's ProofC byte for byte — 2 and 4 ranks run the
+distributed quotient (blocks + coefficient ranges + one all-to-all), 3 ranks
+(does not divide 8) only shard the MSMs, with uneven point ranges."""
 import os
 import socket
 import subprocess
@@ -50,7 +53,7 @@ def test_window_exchange_gloo_world2(tmp_path):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 4])
 def test_sharded_gen_proof_parity(tmp_path, world):
     from pnp_testlib import Inputs
     from pnp import abi

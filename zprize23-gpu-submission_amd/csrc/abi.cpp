@@ -98,10 +98,10 @@ void KernelTimer::collect() {
 }
 
 void commit_affine_batch(pnp_ctx *ctx, const uint64_t *const *d_scalars, int B, uint64_t n,
-                         CommitmentC *const *out) {
+                         CommitmentC *const *out, bool local) {
     std::vector<uint64_t> xyzz((size_t)B * 24);
     msm_run_batch(ctx->msm, ctx->ck_dev, d_scalars, B, n, xyzz.data(), ctx->stream,
-                  commit_table(ctx, n));
+                  commit_table(ctx, n), local);
     for (int b = 0; b < B; b++) {
         uint64_t aff[12];
         xyzz_to_affine_host(xyzz.data() + 24 * b, aff);
@@ -192,6 +192,16 @@ int pnp_set_msm_shard(pnp_ctx *ctx, int rank, int world, pnp_allgather_fn allgat
     ctx->msm.user = user;
     ctx->msm.xbuf = world > 1 ? d_xbuf : nullptr;
     ctx->msm.xbuf_bytes = world > 1 ? xbuf_bytes : 0;
+    return PNP_OK;
+}
+
+int pnp_set_exchange_a2a(pnp_ctx *ctx, pnp_alltoall_fn alltoall, void *user, uint64_t *d_a2a,
+                         uint64_t a2a_bytes) {
+    if (!ctx || (alltoall && !d_a2a)) return PNP_E_ARG;
+    ctx->msm.alltoall = alltoall;
+    ctx->msm.a2a_user = user;
+    ctx->msm.a2a = alltoall ? d_a2a : nullptr;
+    ctx->msm.a2a_bytes = alltoall ? a2a_bytes : 0;
     return PNP_OK;
 }
 
@@ -373,31 +383,64 @@ int pnp_load_prover_key(pnp_ctx *ctx, const ProverKeyC *pk, uint64_t D, int devi
         // reference's preprocessing), the L1 and PI coset evaluations have the
         // closed forms of protocol.h and need no LDE per proof
         const uint64_t N8 = 8 * D;
-        ctx->pk_vh_inv.alloc(32 * N8);
-        PNP_HIP(hipMemcpyAsync(ctx->pk_vh_inv.p, dev.v_h_coset_8n, 32 * N8, hipMemcpyDeviceToDevice,
+        pnp::DevBuf vh_inv(32 * N8), l1v;
+        PNP_HIP(hipMemcpyAsync(vh_inv.p, dev.v_h_coset_8n, 32 * N8, hipMemcpyDeviceToDevice,
                                ctx->stream));
-        pnp::k_batch_inverse(ctx->pk_vh_inv.u64(), N8, ctx->scratch_a, ctx->stream);
+        pnp::k_batch_inverse(vh_inv.u64(), N8, ctx->scratch_a, ctx->stream);
         {
             pnp::DevBuf vh(32 * N8), x(32 * N8);
             pnp::k_coset_consts(vh.u64(), x.u64(), lg, ctx->stream);
             ctx->pk_std_coset =
                 !pnp::k_any_diff(vh.u64(), dev.v_h_coset_8n, 4 * N8, ctx->scratch_b, ctx->stream) &&
                 !pnp::k_any_diff(x.u64(), dev.linear_evaluations, 4 * N8, ctx->scratch_b, ctx->stream);
-            ctx->pk_l1v.release();
             if (ctx->pk_std_coset) {
-                ctx->pk_l1v.alloc(32 * N8);
-                pnp::k_affine(ctx->pk_l1v.u64(), x.u64(), Fr::one(), pnp::neg(Fr::one()), N8, ctx->stream);
-                pnp::k_batch_inverse(ctx->pk_l1v.u64(), N8, ctx->scratch_a, ctx->stream);
+                l1v.alloc(32 * N8);
+                pnp::k_affine(l1v.u64(), x.u64(), Fr::one(), pnp::neg(Fr::one()), N8, ctx->stream);
+                pnp::k_batch_inverse(l1v.u64(), N8, ctx->scratch_a, ctx->stream);
                 Fr nf = Fr::zero();
                 nf.v[0] = (uint32_t)D;
                 nf.v[1] = (uint32_t)(D >> 32);
-                pnp::k_affine(ctx->pk_l1v.u64(), ctx->pk_l1v.u64(), pnp::inverse(pnp::to_mont(nf)),
-                              Fr::zero(), N8, ctx->stream);
+                pnp::k_affine(l1v.u64(), l1v.u64(), pnp::inverse(pnp::to_mont(nf)), Fr::zero(), N8,
+                              ctx->stream);
             }
-            ctx->pk_pinv.release();
-            ctx->pk_pinv_pos = ~0ULL;
             PNP_HIP(hipStreamSynchronize(ctx->stream));
         }
+        // The quotient's 8n arrays in block layout (point 8j + m -> block m,
+        // index j), only the blocks this rank owns: all 8 on one GPU; 8/world
+        // when the round-4 pipeline is distributed (pnp_set_exchange_a2a)
+        const int world = ctx->msm.world;
+        const bool split = world > 1 && 8 % world == 0 && ctx->msm.alltoall;
+        ctx->pk_nb = split ? 8 / world : 8;
+        ctx->pk_mb0 = split ? ctx->msm.rank * ctx->pk_nb : 0;
+        ctx->pk_blk.clear();
+        auto blk = [&](const char *name, const uint64_t *src) {
+            auto &b = ctx->pk_blk[name];
+            b.alloc(32 * (uint64_t)ctx->pk_nb * D);
+            pnp::to_blocks(src, b.u64(), lg, ctx->pk_mb0, ctx->pk_nb, ctx->stream);
+        };
+        if (!ctx->pk_qm_zero) blk("q_m", dev.q_m_evals);
+        if (!ctx->pk_qlookup_zero) blk("q_lookup", dev.q_lookup_evals);
+        blk("q_l", dev.q_l_evals);
+        blk("q_r", dev.q_r_evals);
+        blk("q_o", dev.q_o_evals);
+        blk("q_4", dev.q_4_evals);
+        blk("q_c", dev.q_c_evals);
+        blk("q_hl", dev.q_hl_evals);
+        blk("q_hr", dev.q_hr_evals);
+        blk("q_h4", dev.q_h4_evals);
+        blk("q_arith", dev.q_arith_evals);
+        blk("sig0", dev.left_sigma_evals);
+        blk("sig1", dev.right_sigma_evals);
+        blk("sig2", dev.out_sigma_evals);
+        blk("sig3", dev.fourth_sigma_evals);
+        blk("lin", dev.linear_evaluations);
+        blk("vh_inv", vh_inv.u64());
+        if (ctx->pk_std_coset) blk("l1v", l1v.u64());
+        ctx->pk_blk_rank = ctx->msm.rank;
+        ctx->pk_blk_world = world;
+        ctx->pk_pinv.release();
+        ctx->pk_pinv_pos = ~0ULL;
+        PNP_HIP(hipStreamSynchronize(ctx->stream));
         ctx->pk_dev = dev;
         ctx->pk_n = D;
         ctx->pk_loaded = true;

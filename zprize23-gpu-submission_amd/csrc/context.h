@@ -20,12 +20,21 @@ struct pnp_ctx {
     ProverKeyC pk_dev{};                   // HBM pointers for every field
     bool pk_qm_zero = false, pk_qlookup_zero = false;  // all-zero 8n selector evaluations
     pnp::DevBuf pk_sigma_n[4];             // sigma evaluations on the n-domain
-    // proof-independent coset constants, computed at key load
-    pnp::DevBuf pk_vh_inv;                 // v_h_coset_8n^-1 (8n)
-    bool pk_std_coset = false;             // linear_evaluations = 7 w_8n^i, v_h = x^n - 1
-    pnp::DevBuf pk_l1v;                    // n^-1 / (x_i - 1) = L1 / Z_H  (std coset only)
-    pnp::DevBuf pk_pinv;                   // 1 / (x_i - w^pos), for pos = pk_pinv_pos
+    // The quotient's 8n-point arrays in block layout (ntt.hip: point 8j + m
+    // -> block m, index j), blocks pk_mb0 .. pk_mb0 + pk_nb - 1 only:
+    // q_* selectors, sig0..3, lin (coset points) and the proof-independent
+    // coset constants computed at key load: vh_inv = v_h^-1 and, when
+    // pk_std_coset (linear_evaluations = 7 w_8n^i, v_h = x^n - 1),
+    // l1v = n^-1 / (x - 1) = L1 / Z_H
+    std::map<std::string, pnp::DevBuf> pk_blk;
+    int pk_mb0 = 0, pk_nb = 8, pk_blk_rank = 0, pk_blk_world = 1;
+    bool pk_std_coset = false;
+    pnp::DevBuf pk_pinv;                   // 1 / (x - w^pos) (block layout), pos = pk_pinv_pos
     uint64_t pk_pinv_pos = ~0ULL;
+    const uint64_t *blk(const char *name) const {
+        auto it = pk_blk.find(name);
+        return it == pk_blk.end() ? nullptr : it->second.u64();
+    }
     // ---- resident commit key ----
     bool ck_loaded = false;
     uint64_t ck_points = 0;
@@ -51,7 +60,8 @@ namespace pnp {
 const uint64_t *commit_table(pnp_ctx *ctx, uint64_t n);
 void commit_affine(pnp_ctx *ctx, const uint64_t *d_scalars, uint64_t n, CommitmentC *out);
 // B commitments over the resident SRS in one batched MSM
+// local: on a multi-GPU run the scalars hold only this rank's point range
 void commit_affine_batch(pnp_ctx *ctx, const uint64_t *const *d_scalars, int B, uint64_t n,
-                         CommitmentC *const *out);
+                         CommitmentC *const *out, bool local = false);
 int prove_impl(pnp_ctx *ctx, const CircuitC *cs, int device_ptrs, ProofC *out);
 }  // namespace pnp

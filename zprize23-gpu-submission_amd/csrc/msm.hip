@@ -764,7 +764,8 @@ void msm_point_range(uint64_t n, int rank, int world, uint64_t &p0, uint64_t &p1
 // window; the folded table passed in covers that range), the B partial sums
 // meet in one all-gather of B XYZZ points per rank and are added on the host.
 void msm_run_batch(MsmWork &wk, const uint64_t *d_points, const uint64_t *const *d_scalars, int B,
-                   uint64_t n, uint64_t *h_xyzz, hipStream_t s, const uint64_t *table) {
+                   uint64_t n, uint64_t *h_xyzz, hipStream_t s, const uint64_t *table,
+                   bool scalars_local) {
     if (wk.world == 1) {
         msm_local_batch(wk, d_points, d_scalars, B, n, h_xyzz, s, table);
         return;
@@ -772,7 +773,7 @@ void msm_run_batch(MsmWork &wk, const uint64_t *d_points, const uint64_t *const 
     uint64_t p0, p1;
     msm_point_range(n, wk.rank, wk.world, p0, p1);
     std::vector<const uint64_t *> sc(B);
-    for (int b = 0; b < B; b++) sc[b] = d_scalars[b] + 4 * p0;
+    for (int b = 0; b < B; b++) sc[b] = scalars_local ? d_scalars[b] : d_scalars[b] + 4 * p0;
     std::vector<uint64_t> part((size_t)B * 24);
     msm_local_batch(wk, d_points + 12 * p0, sc.data(), B, p1 - p0, part.data(), s, table);
     const uint64_t slot = (uint64_t)B * 24 * 8;

@@ -208,6 +208,7 @@ __device__ __forceinline__ Fr apply_scale(const Scale &s, Fr x, uint64_t i) {
 // lg >= 10: index = hi5 | mid | lo5; tile(mid) <-> tile(rev(mid)) transposed.
 __global__ __launch_bounds__(256) void k_bitrev_tiles(uint64_t *data, uint32_t lg, Scale sc) {
     __shared__ uint4 t0l[32 * 33], t0h[32 * 33], t1l[32 * 33], t1h[32 * 33];
+    data += ((uint64_t)blockIdx.y << lg) * 4;  // independent transforms of 2^lg side by side
     const uint32_t midbits = lg - 10;
     const uint32_t mid = blockIdx.x;
     const uint32_t rmid = midbits ? brev(mid, midbits) : 0;
@@ -253,6 +254,7 @@ __global__ __launch_bounds__(256) void k_bitrev_tiles(uint64_t *data, uint32_t l
 // lg < 10: single workgroup, via LDS
 __global__ __launch_bounds__(256) void k_bitrev_small(uint64_t *data, uint32_t lg, Scale sc) {
     __shared__ uint4 tl[1024], th[1024];
+    data += ((uint64_t)blockIdx.y << lg) * 4;
     const uint32_t n = 1u << lg;
     for (uint32_t e = threadIdx.x; e < n; e += 256) {
         const uint4 *s = reinterpret_cast<const uint4 *>(data + 4 * (uint64_t)e);
@@ -327,11 +329,11 @@ static void dif(NttTables &t, uint64_t *d, uint32_t lg, bool inverse, hipStream_
     }
 }
 
-static void bitrev(uint64_t *d, uint32_t lg, const Scale &sc, hipStream_t s) {
+static void bitrev(uint64_t *d, uint32_t lg, const Scale &sc, hipStream_t s, uint32_t nblocks = 1) {
     if (lg < 10) {
-        hipLaunchKernelGGL(k_bitrev_small, dim3(1), dim3(256), 0, s, d, lg, sc);
+        hipLaunchKernelGGL(k_bitrev_small, dim3(1, nblocks), dim3(256), 0, s, d, lg, sc);
     } else {
-        hipLaunchKernelGGL(k_bitrev_tiles, dim3(1u << (lg - 10)), dim3(256), 0, s, d, lg, sc);
+        hipLaunchKernelGGL(k_bitrev_tiles, dim3(1u << (lg - 10), nblocks), dim3(256), 0, s, d, lg, sc);
     }
     PNP_HIP(hipGetLastError());
 }
@@ -403,6 +405,149 @@ void coset_lde8(NttTables &t, const uint64_t *in, uint64_t *out8, uint32_t lg_n,
     if (lg_n > 0) dif(t, out8, lg_n, false, s, lg_n + 3);
     Scale sc{0, Fr::one(), nullptr, nullptr};
     bitrev(out8, lg_n + 3, sc, s);
+}
+
+// ---------------------------------------------------------------- block layout
+// gen_proof round 4 keeps the 8n coset in "block layout": point
+// x_i = g w_8n^i, i = 8 j + m, lives in block m at index j, so each residue
+// class m is the size-n domain coset g w_8n^m <w_n> and every block is an
+// independent size-n transform (and a unit of multi-GPU work).
+static const uint64_t *block_twist_table(NttTables &t, uint32_t lg_n, bool inverse, hipStream_t s) {
+    auto &tabs = inverse ? t.blk_twist_inv : t.blk_twist;
+    auto it = tabs.find(lg_n);
+    if (it != tabs.end()) return it->second.u64();
+    const uint64_t n = 1ULL << lg_n;
+    DevBuf buf(8 * n * 32);
+    const Fr w8n = host_root(lg_n + 3), g = host_gen();
+    const uint32_t chunk = 64;
+    const uint64_t threads = (n + chunk - 1) / chunk;
+    for (uint32_t m = 0; m < 8; m++) {
+        // forward: (g w_8n^m)^j;  inverse: w_8n^(-m j)
+        Fr base = inverse ? pnp::inverse(pow_u64(w8n, m)) : g * pow_u64(w8n, m);
+        hipLaunchKernelGGL(k_powers_table, dim3((uint32_t)((threads + 255) / 256)), dim3(256), 0, s,
+                           buf.u64() + 4 * m * n, n, base, chunk);
+        PNP_HIP(hipGetLastError());
+    }
+    const uint64_t *p = buf.u64();
+    tabs.emplace(lg_n, std::move(buf));
+    return p;
+}
+
+static uint32_t lg_blocks(int nb) {
+    uint32_t l = 0;
+    while ((1 << l) < nb) l++;
+    if ((1 << l) != nb) {
+        set_error("block count %d is not a power of two", nb);
+        throw Error(PNP_E_ARG);
+    }
+    return l;
+}
+
+// out[b n + j] = f(g w_8n^(8 j + m0 + b)), b < nb, for the n coefficients `in`
+void lde_blocks(NttTables &t, const uint64_t *in, uint64_t *out, uint32_t lg_n, int m0, int nb,
+                hipStream_t s) {
+    const uint64_t n = 1ULL << lg_n, N = n * nb;
+    const uint64_t *T = block_twist_table(t, lg_n, false, s) + 4 * (uint64_t)m0 * n;
+    hipLaunchKernelGGL(k_lde_twist, dim3((uint32_t)((N + 255) / 256)), dim3(256), 0, s, in, T, out, n, N);
+    PNP_HIP(hipGetLastError());
+    if (lg_n > 0) dif(t, out, lg_n, false, s, lg_n + lg_blocks(nb));
+    Scale sc{0, Fr::one(), nullptr, nullptr};
+    bitrev(out, lg_n, sc, s, nb);
+}
+
+__global__ void k_mul_table(uint64_t *d, const uint64_t *T, uint64_t N) {
+    uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    if (i < N) store_fr(d, i, load_fr(d, i) * load_fr(T, i));
+}
+
+// in place, block b < nb holding residue m = m0 + b:
+//   Y_m[u] = w_8n^(-m u) sum_j d[b n + j] w_n^(-j u)      (no 1/n scaling)
+void intt_blocks(NttTables &t, uint64_t *d, uint32_t lg_n, int m0, int nb, hipStream_t s) {
+    const uint64_t n = 1ULL << lg_n, N = n * nb;
+    if (lg_n > 0) dif(t, d, lg_n, true, s, lg_n + lg_blocks(nb));
+    Scale sc{0, Fr::one(), nullptr, nullptr};
+    bitrev(d, lg_n, sc, s, nb);
+    const uint64_t *T = block_twist_table(t, lg_n, true, s) + 4 * (uint64_t)m0 * n;
+    hipLaunchKernelGGL(k_mul_table, dim3((uint32_t)((N + 255) / 256)), dim3(256), 0, s, d, T, N);
+    PNP_HIP(hipGetLastError());
+}
+
+// Coefficients of the 8n-point coset interpolant from the 8 twisted block
+// transforms Y_m (block-major, `len` entries each, covering u in [q0, q0+len)):
+//   c_(u + n m1) = g^-(u + n m1) / (8n) sum_m w_8^(-m m1) Y_m[u]
+// -> out[m1 len + (u - q0)]: radix-2 8-point inverse DFT per u.
+__global__ void k_t_combine(const uint64_t *Y, uint64_t len, uint64_t q0, uint64_t *out, Fr w1, Fr w2,
+                            Fr w3, Fr inv8n, const uint64_t *chi, const uint64_t *clo, Fr gn0, Fr gn1,
+                            Fr gn2, Fr gn3, Fr gn4, Fr gn5, Fr gn6, Fr gn7) {
+    uint64_t u = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    if (u >= len) return;
+    Fr y[8];
+#pragma unroll
+    for (int m = 0; m < 8; m++) y[m] = load_fr(Y, m * len + u);
+    // DIF stage h = 4 (twiddles w^k), h = 2 (w^2k), h = 1; output bit-reversed
+    const Fr wk[4] = {Fr::one(), w1, w2, w3};
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        Fr a = y[k], b = y[k + 4];
+        y[k] = a + b;
+        y[k + 4] = k ? (a - b) * wk[k] : a - b;
+    }
+#pragma unroll
+    for (int base = 0; base < 8; base += 4) {
+        Fr a = y[base], b = y[base + 2];
+        y[base] = a + b;
+        y[base + 2] = a - b;
+        a = y[base + 1];
+        b = y[base + 3];
+        y[base + 1] = a + b;
+        y[base + 3] = (a - b) * w2;
+    }
+#pragma unroll
+    for (int base = 0; base < 8; base += 2) {
+        Fr a = y[base], b = y[base + 1];
+        y[base] = a + b;
+        y[base + 1] = a - b;
+    }
+    const Fr s0 = coset_pow(chi, clo, q0 + u) * inv8n;  // g^-u / (8n)
+    const Fr gn[8] = {gn0, gn1, gn2, gn3, gn4, gn5, gn6, gn7};
+    const int rev[8] = {0, 4, 2, 6, 1, 5, 3, 7};
+#pragma unroll
+    for (int p = 0; p < 8; p++) {
+        const int m1 = rev[p];
+        store_fr(out, m1 * len + u, y[p] * (s0 * gn[m1]));
+    }
+}
+
+void t_combine(NttTables &t, const uint64_t *Y, uint64_t len, uint64_t q0, uint64_t *out,
+               uint32_t lg_n, hipStream_t s) {
+    ntt_prepare_coset(t, s);
+    const uint64_t n = 1ULL << lg_n;
+    const Fr w8i = pnp::inverse(host_root(3));
+    Fr w[4] = {Fr::one(), w8i, w8i * w8i, w8i * w8i * w8i};
+    Fr nf = Fr::zero();
+    nf.v[0] = (uint32_t)(8 * n);
+    nf.v[1] = (uint32_t)((8 * n) >> 32);
+    const Fr inv8n = pnp::inverse(to_mont(nf));
+    const Fr gni = pnp::inverse(pow_u64(host_gen(), n));
+    Fr gn[8];
+    gn[0] = Fr::one();
+    for (int k = 1; k < 8; k++) gn[k] = gn[k - 1] * gni;
+    hipLaunchKernelGGL(k_t_combine, dim3((uint32_t)((len + 255) / 256)), dim3(256), 0, s, Y, len, q0, out,
+                       w[1], w[2], w[3], inv8n, t.coset_inv_hi.u64(), t.coset_inv_lo.u64(), gn[0], gn[1],
+                       gn[2], gn[3], gn[4], gn[5], gn[6], gn[7]);
+    PNP_HIP(hipGetLastError());
+}
+
+// out[b n + j] = in[8 j + m0 + b], b < nb   (natural 8n order -> block layout)
+__global__ void k_to_blocks(const uint64_t *in, uint64_t *out, uint64_t n, int m0, int nb) {
+    uint64_t j = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    if (j >= n) return;
+    for (int b = 0; b < nb; b++) store_fr(out, (uint64_t)b * n + j, load_fr(in, 8 * j + m0 + b));
+}
+void to_blocks(const uint64_t *in, uint64_t *out, uint32_t lg_n, int m0, int nb, hipStream_t s) {
+    const uint64_t n = 1ULL << lg_n;
+    hipLaunchKernelGGL(k_to_blocks, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, s, in, out, n, m0, nb);
+    PNP_HIP(hipGetLastError());
 }
 
 }  // namespace pnp

@@ -56,6 +56,8 @@ struct NttTables {
     bool coset_ready = false;
     // coset LDE twist per lg_n: (g w_8n^rev3(b))^j for block b, j < n
     std::map<uint32_t, DevBuf> lde_twist;
+    // block layout twists per lg_n: (g w_8n^m)^j and w_8n^(-m j), block m
+    std::map<uint32_t, DevBuf> blk_twist, blk_twist_inv;
 };
 const uint64_t *ntt_twiddles(NttTables &t, uint32_t lg, bool inverse, hipStream_t s);
 void ntt_prepare_coset(NttTables &t, hipStream_t s);
@@ -63,6 +65,17 @@ void ntt_prepare_coset(NttTables &t, hipStream_t s);
 void ntt_run(NttTables &t, uint64_t *d, uint32_t lg, bool inverse, bool coset, hipStream_t s);
 // out8[i] = i < n ? in[i] * g^i : 0, then forward NTT of size 8n (Ntt_coset::forward)
 void coset_lde8(NttTables &t, const uint64_t *in, uint64_t *out8, uint32_t lg_n, hipStream_t s);
+
+// block layout of the 8n coset (point i = 8 j + m -> block m, index j):
+// LDE of n coefficients into blocks m0 .. m0+nb-1 (nb a power of two)
+void lde_blocks(NttTables &t, const uint64_t *in, uint64_t *out, uint32_t lg_n, int m0, int nb,
+                hipStream_t s);
+// per block: unscaled inverse size-n DFT then twist by w_8n^(-m u)
+void intt_blocks(NttTables &t, uint64_t *d, uint32_t lg_n, int m0, int nb, hipStream_t s);
+// 8-point inverse DFT across blocks + g^-i / (8n): coefficient chunks u in [q0, q0+len)
+void t_combine(NttTables &t, const uint64_t *Y, uint64_t len, uint64_t q0, uint64_t *out,
+               uint32_t lg_n, hipStream_t s);
+void to_blocks(const uint64_t *in, uint64_t *out, uint32_t lg_n, int m0, int nb, hipStream_t s);
 
 // ---- live per-kernel timing with HIP events on the launching stream ----
 struct KernelTimer {
@@ -104,13 +117,20 @@ struct MsmWork {
     void *user = nullptr;
     uint64_t *xbuf = nullptr;
     uint64_t xbuf_bytes = 0;
+    // all-to-all for the distributed quotient (pnp_set_exchange_a2a)
+    pnp_alltoall_fn alltoall = nullptr;
+    void *a2a_user = nullptr;
+    uint64_t *a2a = nullptr;
+    uint64_t a2a_bytes = 0;
 };
 // sum_i s_i P_i; scalars Montgomery Fr; result written to host as XYZZ Fq (4x6 u64)
 // `table` (optional): msm_build_table(d_points, n) — the folded layout
 void msm_run(MsmWork &w, const uint64_t *d_points, const uint64_t *d_scalars_mont, uint64_t n,
              uint64_t *h_xyzz, hipStream_t s, const uint64_t *table = nullptr);
+// scalars_local: multi-GPU, d_scalars[b] hold only this rank's point range
 void msm_run_batch(MsmWork &w, const uint64_t *d_points, const uint64_t *const *d_scalars, int B,
-                   uint64_t n, uint64_t *h_xyzz, hipStream_t s, const uint64_t *table = nullptr);
+                   uint64_t n, uint64_t *h_xyzz, hipStream_t s, const uint64_t *table = nullptr,
+                   bool scalars_local = false);
 // multi-GPU MSMs: the points [p0, p1) rank `rank` of `world` takes
 void msm_point_range(uint64_t n, int rank, int world, uint64_t &p0, uint64_t &p1);
 // T[k*n + i] = 2^(c*k) P_i, k < W (msm_cfg(n)), affine, in the radix-2^29
@@ -130,6 +150,8 @@ void k_poly_eval(const uint64_t *d, uint64_t n, const Fr &x, DevBuf &scratch, Fr
 void k_poly_eval_multi(const uint64_t *const *polys, int npolys, uint64_t n, const Fr &x,
                        DevBuf &scratch, Fr *out, hipStream_t s);
 void k_poly_div_linear(uint64_t *d, uint64_t n, const Fr &z, DevBuf &scratch, hipStream_t s);
+// d[i] += c z^(len-1-i)
+void k_add_powers(uint64_t *d, uint64_t len, const Fr &c, const Fr &z, hipStream_t s);
 void k_random_fr(uint64_t *d, uint64_t n, uint64_t seed, hipStream_t s);
 // d[i] = c0 * r^i
 void k_geometric(uint64_t *d, uint64_t n, const Fr &c0, const Fr &r, hipStream_t s);

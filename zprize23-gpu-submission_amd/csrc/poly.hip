@@ -373,4 +373,25 @@ void k_random_fr(uint64_t *d, uint64_t n, uint64_t seed, hipStream_t s) {
     PNP_HIP(hipGetLastError());
 }
 
+// d[i] += c z^(len-1-i), i < len: the carry of a polynomial division by
+// (X - z) split over coefficient ranges (the part above this range)
+__global__ void k_add_powers_(uint64_t *d, uint64_t len, Fr c, Fr z, uint32_t chunk) {
+    uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    uint64_t lo = t * chunk;
+    if (lo >= len) return;
+    uint64_t hi = lo + chunk < len ? lo + chunk : len;
+    Fr p = c * pow_u64(z, len - hi);
+    for (uint64_t i = hi; i-- > lo;) {
+        store_fr(d, i, load_fr(d, i) + p);
+        p = p * z;
+    }
+}
+void k_add_powers(uint64_t *d, uint64_t len, const Fr &c, const Fr &z, hipStream_t s) {
+    if (!len) return;
+    const uint32_t chunk = 64;
+    hipLaunchKernelGGL(k_add_powers_, dim3(nblk((len + chunk - 1) / chunk)), dim3(256), 0, s, d, len, c, z,
+                       chunk);
+    PNP_HIP(hipGetLastError());
+}
+
 }  // namespace pnp

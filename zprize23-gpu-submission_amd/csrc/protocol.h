@@ -34,6 +34,7 @@ struct QuotArgs {
     // PI / Z_H = c_pi * pinv with c_pi = pi * w^pos / n
     const uint64_t *l1v, *pinv;
     Fr c_pi;
+    uint64_t n;  // block length: arrays are in block layout (point 8j + m -> m n + j)
     Fr alpha, alpha2, beta, gamma, delta, eps, zeta, lsep;
     Fr bk[4], opd, eopd, sep2, sep3;
 };

@@ -66,6 +66,52 @@ void set_infinity(CommitmentC *c) {
 
 void store_fr_host(uint64_t out[4], const Fr &a) { to_u64_limbs(a, out); }
 
+// k words from every rank (rank-major) through the MSM exchange buffer
+std::vector<uint64_t> shard_allgather(pnp_ctx *ctx, const uint64_t *mine, int k) {
+    MsmWork &wk = ctx->msm;
+    const uint64_t slot = 8 * (uint64_t)k;
+    if (wk.xbuf_bytes < slot * wk.world) {
+        set_error("exchange buffer %llu B < %llu B", (unsigned long long)wk.xbuf_bytes,
+                  (unsigned long long)(slot * wk.world));
+        throw Error(PNP_E_ARG);
+    }
+    PNP_HIP(hipMemcpyAsync(wk.xbuf + (uint64_t)k * wk.rank, mine, slot, hipMemcpyHostToDevice, ctx->stream));
+    PNP_HIP(hipStreamSynchronize(ctx->stream));
+    if (int rc = wk.allgather(wk.user, slot)) {
+        set_error("all-gather callback failed (%d)", rc);
+        throw Error(PNP_E_DEVICE);
+    }
+    std::vector<uint64_t> all((size_t)k * wk.world);
+    PNP_HIP(hipMemcpyAsync(all.data(), wk.xbuf, all.size() * 8, hipMemcpyDeviceToHost, ctx->stream));
+    PNP_HIP(hipStreamSynchronize(ctx->stream));
+    return all;
+}
+
+// In place p <- p / (X - z) (kzg10.cu:87-99) where this rank holds the
+// coefficient range [a, a + len) of p.  Quotient coefficient
+// q_i = sum_(k > i) p_k z^(k-i-1) = (division of the local slice) +
+// z^(a+len-1-i) C with C = sum_(k >= a+len) p_k z^(k-a-len): every rank
+// shares the value E_r of its slice at z, C follows from the E of the ranks
+// above.
+void div_linear_range(pnp_ctx *ctx, uint64_t *d, uint64_t len, const Fr &z, bool dist) {
+    hipStream_t s = ctx->stream;
+    if (!dist) {
+        k_poly_div_linear(d, len, z, ctx->scratch_a, s);
+        return;
+    }
+    const int world = ctx->msm.world, rank = ctx->msm.rank;
+    Fr e;
+    k_poly_eval(d, len, z, ctx->scratch_a, &e, s);
+    uint64_t mine[4];
+    to_u64_limbs(e, mine);
+    std::vector<uint64_t> all = shard_allgather(ctx, mine, 4);
+    const uint64_t n = len * world;  // equal ranges (world divides 8 and n)
+    Fr c = Fr::zero();
+    for (int r = world - 1; r > rank; r--) c = c * pow_u64(z, n / world) + from_u64_limbs<FrP>(&all[4 * r]);
+    k_poly_div_linear(d, len, z, ctx->scratch_a, s);
+    if (rank < world - 1) k_add_powers(d, len, c, z, s);
+}
+
 }  // namespace
 
 int prove_impl(pnp_ctx *ctx, const CircuitC *cs, int device_ptrs, ProofC *out) {
@@ -220,6 +266,19 @@ int prove_impl(pnp_ctx *ctx, const CircuitC *cs, int device_ptrs, ProofC *out) {
     // public input poly (pi.cu:11-15)
     // = iNTT of the evaluations v * e_pos, in closed form: v n^-1 w^(-pos j)
     const Fr n_inv = inverse(fr_from_u64(n));
+    // round-4 distribution (pnp_set_exchange_a2a, fixed at key load): this
+    // rank's coset blocks [mb0, mb0 + nb) and coefficient range [q0, q0 + len)
+    const int world = ctx->msm.world;
+    if (ctx->pk_blk_world != world || ctx->pk_blk_rank != ctx->msm.rank) {
+        set_error("sharding changed after pnp_load_prover_key");
+        return PNP_E_ARG;
+    }
+    const int mb0 = ctx->pk_mb0, nb = ctx->pk_nb;
+    const bool dist = nb < 8;
+    const uint64_t NB = (uint64_t)nb * n;
+    uint64_t q0 = 0, q1 = n;
+    if (dist) msm_point_range(n, ctx->msm.rank, world, q0, q1);
+    const uint64_t len = q1 - q0;
     const Fr pi_v = to_mont(from_u64_limbs<FrP>(cs->pi));
     const bool closed = ctx->pk_std_coset;  // L1, PI on the coset in closed form
     uint64_t *pi_poly = nullptr;
@@ -228,12 +287,13 @@ int prove_impl(pnp_ctx *ctx, const CircuitC *cs, int device_ptrs, ProofC *out) {
         Fr w_inv_pos = pow_u64(inverse(root_of_unity(lg)), cs->intended_pi_pos);
         k_geometric(pi_poly, n, pi_v * n_inv, w_inv_pos, s);
     } else if (ctx->pk_pinv_pos != cs->intended_pi_pos) {
-        // 1 / (x_i - w^pos), kept across proofs with the same PI position
+        // 1 / (x_i - w^pos) on this rank's blocks, kept across proofs with the
+        // same PI position
         ctx->pk_pinv_pos = ~0ULL;
-        if (!ctx->pk_pinv.p) ctx->pk_pinv.alloc(32 * N8);
+        if (ctx->pk_pinv.bytes < 32 * NB) ctx->pk_pinv.alloc(32 * NB);
         Fr wpos = pow_u64(root_of_unity(lg), cs->intended_pi_pos);
-        k_affine(ctx->pk_pinv.u64(), pk.linear_evaluations, Fr::one(), neg(wpos), N8, s);
-        k_batch_inverse(ctx->pk_pinv.u64(), N8, ctx->scratch_a, s);
+        k_affine(ctx->pk_pinv.u64(), ctx->blk("lin"), Fr::one(), neg(wpos), NB, s);
+        k_batch_inverse(ctx->pk_pinv.u64(), NB, ctx->scratch_a, s);
         ctx->pk_pinv_pos = cs->intended_pi_pos;
     }
     tm.mark("r3_z2_pi");
@@ -253,39 +313,41 @@ int prove_impl(pnp_ctx *ctx, const CircuitC *cs, int device_ptrs, ProofC *out) {
     tr.append_scalar("lookup separation challenge", lsep);
 
     QuotArgs q;
+    // coset evaluations in block layout, this rank's blocks only
+    auto lde = [&](const uint64_t *coeffs, uint64_t *dst) { lde_blocks(nt, coeffs, dst, lg, mb0, nb, s); };
     for (int j = 0; j < 4; j++) {
-        uint64_t *w8 = ctx->buf("w8_" + std::to_string(j), N8);
-        coset_lde8(nt, wpoly[j], w8, lg, s);
+        uint64_t *w8 = ctx->buf("w8_" + std::to_string(j), NB);
+        lde(wpoly[j], w8);
         q.w8[j] = w8;
     }
-    uint64_t *z8 = ctx->buf("z8", N8), *z28 = ctx->buf("z28", N8);
-    coset_lde8(nt, z_poly, z8, lg, s);
+    uint64_t *z8 = ctx->buf("z8", NB), *z28 = ctx->buf("z28", NB);
+    lde(z_poly, z8);
     q.z8 = z8;
     q.pi8 = nullptr;
     q.l18 = q.l1v = q.pinv = nullptr;
     if (closed) {
-        q.l1v = ctx->pk_l1v.u64();
+        q.l1v = ctx->blk("l1v");
         q.pinv = ctx->pk_pinv.u64();
         q.c_pi = pi_v * pow_u64(root_of_unity(lg), cs->intended_pi_pos) * n_inv;
     } else {
-        uint64_t *pi8 = ctx->buf("pi8", N8);
-        coset_lde8(nt, pi_poly, pi8, lg, s);
+        uint64_t *pi8 = ctx->buf("pi8", NB);
+        lde(pi_poly, pi8);
         q.pi8 = pi8;
     }
     q.z28 = nullptr;  // z2 = 1: its quotient terms cancel (protocol.h)
     if (!z2_one) {
-        coset_lde8(nt, z2_poly, z28, lg, s);
+        lde(z2_poly, z28);
         q.z28 = z28;
     }
     q.f8 = q.t8 = nullptr;
     if (!f_zero) {
-        uint64_t *f8 = ctx->buf("f8", N8);
-        coset_lde8(nt, f_poly, f8, lg, s);
+        uint64_t *f8 = ctx->buf("f8", NB);
+        lde(f_poly, f8);
         q.f8 = f8;
     }
     if (!table_zero) {
-        uint64_t *t8 = ctx->buf("t8", N8);
-        coset_lde8(nt, table_poly, t8, lg, s);
+        uint64_t *t8 = ctx->buf("t8", NB);
+        lde(table_poly, t8);
         q.t8 = t8;
     }
     q.h18 = q.h28 = nullptr;  // h1 = h2 = 0
@@ -293,29 +355,31 @@ int prove_impl(pnp_ctx *ctx, const CircuitC *cs, int device_ptrs, ProofC *out) {
     // one LDE of L1 (coefficients n^-1, no iNTT); alpha^2 is applied in the kernel
     Fr alpha2 = alpha * alpha;
     if (!closed) {
-        uint64_t *l1 = ctx->buf("l1", n), *l18 = ctx->buf("l18", N8);
+        uint64_t *l1 = ctx->buf("l1", n), *l18 = ctx->buf("l18", NB);
         k_geometric(l1, n, n_inv, Fr::one(), s);
-        coset_lde8(nt, l1, l18, lg, s);
+        lde(l1, l18);
         q.l18 = l18;
     }
     q.alpha2 = alpha2;
-    q.q_m = ctx->pk_qm_zero ? nullptr : pk.q_m_evals;
-    q.q_l = pk.q_l_evals;
-    q.q_r = pk.q_r_evals;
-    q.q_o = pk.q_o_evals;
-    q.q_4 = pk.q_4_evals;
-    q.q_c = pk.q_c_evals;
-    q.q_hl = pk.q_hl_evals;
-    q.q_hr = pk.q_hr_evals;
-    q.q_h4 = pk.q_h4_evals;
-    q.q_arith = pk.q_arith_evals;
-    q.q_lookup = ctx->pk_qlookup_zero ? nullptr : pk.q_lookup_evals;
-    q.sig[0] = pk.left_sigma_evals;
-    q.sig[1] = pk.right_sigma_evals;
-    q.sig[2] = pk.out_sigma_evals;
-    q.sig[3] = pk.fourth_sigma_evals;
-    q.lin = pk.linear_evaluations;
-    q.vh_inv = ctx->pk_vh_inv.u64();  // v_h^-1, computed at key load
+    // prover-key evaluations: block-layout copies made at key load
+    q.q_m = ctx->blk("q_m");  // nullptr = zero selector
+    q.q_l = ctx->blk("q_l");
+    q.q_r = ctx->blk("q_r");
+    q.q_o = ctx->blk("q_o");
+    q.q_4 = ctx->blk("q_4");
+    q.q_c = ctx->blk("q_c");
+    q.q_hl = ctx->blk("q_hl");
+    q.q_hr = ctx->blk("q_hr");
+    q.q_h4 = ctx->blk("q_h4");
+    q.q_arith = ctx->blk("q_arith");
+    q.q_lookup = ctx->blk("q_lookup");
+    q.sig[0] = ctx->blk("sig0");
+    q.sig[1] = ctx->blk("sig1");
+    q.sig[2] = ctx->blk("sig2");
+    q.sig[3] = ctx->blk("sig3");
+    q.lin = ctx->blk("lin");
+    q.vh_inv = ctx->blk("vh_inv");  // v_h^-1, computed at key load
+    q.n = n;
     q.alpha = alpha;
     q.beta = beta;
     q.gamma = gamma;
@@ -329,10 +393,10 @@ int prove_impl(pnp_ctx *ctx, const CircuitC *cs, int device_ptrs, ProofC *out) {
     q.sep2 = lsep * lsep;
     q.sep3 = q.sep2 * lsep;
     tm.mark("r4_lde");
-    uint64_t *t_poly = ctx->buf("t_poly", N8);
+    uint64_t *t_blk = ctx->buf("t_blk", NB);
     hipEvent_t qe0 = nullptr;
     ctx->ktimer.begin("quotient", s, qe0);
-    k_quotient(q, N8, t_poly, s);
+    k_quotient(q, NB, t_blk, s);
     {
         // algorithmic bytes: every coset array the kernel reads (nullptr = known
         // zero, not read) plus t, 32 B per point each
@@ -342,11 +406,43 @@ int prove_impl(pnp_ctx *ctx, const CircuitC *cs, int device_ptrs, ProofC *out) {
                                   q.t8, q.h18, q.h28, q.q_lookup, q.z28, q.l18, q.vh_inv, q.l1v, q.pinv};
         int nread = 0;
         for (const uint64_t *a : arrs) nread += a != nullptr;
-        ctx->ktimer.end("quotient", s, qe0, 32.0 * (double)N8 * (nread + 1));
+        ctx->ktimer.end("quotient", s, qe0, 32.0 * (double)NB * (nread + 1));
     }
     tm.mark("r4_quotient");
     ctx->ktimer.collect();
-    ntt_run(nt, t_poly, lg + 3, true, true, s);  // Intt_coset
+    // Intt_coset of the 8n values: per block an unscaled size-n inverse
+    // transform and a twist, then an 8-point inverse DFT across the blocks
+    // per coefficient index (ntt.hip t_combine) -> the 8 chunks t_1..t_8,
+    // here over this rank's coefficient range [q0, q0 + len): t_poly[k len + u]
+    intt_blocks(nt, t_blk, lg, mb0, nb, s);
+    uint64_t *t_poly = ctx->buf("t_poly", 8 * len);
+    if (!dist) {
+        t_combine(nt, t_blk, n, 0, t_poly, lg, s);
+    } else {
+        // all-to-all: rank r' receives, from every rank, that rank's blocks
+        // restricted to r''s coefficient range; slots arrive block-major
+        const uint64_t slot = (uint64_t)nb * len * 32;
+        if (!ctx->msm.alltoall || ctx->msm.a2a_bytes < 2 * slot * world) {
+            set_error("round-4 all-to-all buffer missing or < %llu B",
+                      (unsigned long long)(2 * slot * world));
+            return PNP_E_ARG;
+        }
+        uint64_t *a2a = ctx->msm.a2a;
+        for (int r = 0; r < world; r++) {
+            uint64_t r0, r1;
+            msm_point_range(n, r, world, r0, r1);
+            for (int b = 0; b < nb; b++)
+                PNP_HIP(hipMemcpyAsync(a2a + 4 * ((uint64_t)(r * nb + b) * len), t_blk + 4 * ((uint64_t)b * n + r0),
+                                       32 * len, hipMemcpyDeviceToDevice, s));
+        }
+        PNP_HIP(hipStreamSynchronize(s));
+        int rc = ctx->msm.alltoall(ctx->msm.a2a_user, slot);
+        if (rc != 0) {
+            set_error("round-4 all-to-all callback failed (%d)", rc);
+            return PNP_E_DEVICE;
+        }
+        t_combine(nt, a2a + 4 * (uint64_t)nb * len * world, len, q0, t_poly, lg, s);
+    }
     tm.mark("r4_intt8");
     CommitmentC *tcm[8] = {&out->t_1_comm, &out->t_2_comm, &out->t_3_comm, &out->t_4_comm,
                            &out->t_5_comm, &out->t_6_comm, &out->t_7_comm, &out->t_8_comm};
@@ -355,15 +451,21 @@ int prove_impl(pnp_ctx *ctx, const CircuitC *cs, int device_ptrs, ProofC *out) {
         // deg t < 6n) commit to the point at infinity without an MSM
         const uint64_t *sc[9];
         CommitmentC *oc[9];
-        int nb = 0;
+        int nc = 0;
+        uint64_t nz[8];
+        for (int k = 0; k < 8; k++) nz[k] = k_any_nonzero(t_poly + 4 * (uint64_t)k * len, 4 * len, ctx->scratch_b, s);
+        if (dist) {  // a chunk is zero when it is zero on every rank
+            std::vector<uint64_t> all = shard_allgather(ctx, nz, 8);
+            for (int k = 0; k < 8; k++)
+                for (int r = 0; r < world; r++) nz[k] |= all[8 * r + k];
+        }
         for (int k = 0; k < 8; k++) {
-            const uint64_t *chunk = t_poly + 4 * (uint64_t)k * n;
-            if (!k_any_nonzero(chunk, 4 * n, ctx->scratch_b, s)) {
+            if (!nz[k]) {
                 set_infinity(tcm[k]);
                 continue;
             }
-            sc[nb] = chunk;
-            oc[nb++] = tcm[k];
+            sc[nc] = t_poly + 4 * (uint64_t)k * len;
+            oc[nc++] = tcm[k];
         }
         if (z2_one) {
             // commit([1, 0, ...]) = 1 * powers_of_g[0], already affine
@@ -372,11 +474,15 @@ int prove_impl(pnp_ctx *ctx, const CircuitC *cs, int device_ptrs, ProofC *out) {
             PNP_HIP(hipStreamSynchronize(s));
             memcpy(out->z_2_comm.x, g0, 48);
             memcpy(out->z_2_comm.y, g0 + 6, 48);
+        } else if (dist) {
+            commit_affine(ctx, z2_poly, n, &out->z_2_comm);
         } else {
-            sc[nb] = z2_poly;
-            oc[nb++] = &out->z_2_comm;
+            sc[nc] = z2_poly;
+            oc[nc++] = &out->z_2_comm;
         }
-        commit_affine_batch(ctx, sc, nb, n, oc);
+        // distributed: the chunks hold this rank's coefficient range only,
+        // exactly the point range of its MSM share
+        commit_affine_batch(ctx, sc, nc, n, oc, dist);
     }
     const char *tl[8] = {"t_1", "t_2", "t_3", "t_4", "t_5", "t_6", "t_7", "t_8"};
     for (int k = 0; k < 8; k++) append_comm(tr, tl[k], *tcm[k]);
@@ -445,11 +551,13 @@ int prove_impl(pnp_ctx *ctx, const CircuitC *cs, int device_ptrs, ProofC *out) {
     const Fr qae = ld(ev->custom_evals.q_arith_eval);
     LinArgs la;
     la.k = 0;
-    auto push = [&](const uint64_t *p, const Fr &sc) {
+    // over this rank's coefficient range (replicated polynomials offset by q0)
+    auto push_local = [&](const uint64_t *p, const Fr &sc) {
         la.p[la.k] = p;
         la.s[la.k] = sc;
         la.k++;
     };
+    auto push = [&](const uint64_t *p, const Fr &sc) { push_local(p + 4 * q0, sc); };
     auto p5 = [](const Fr &x) { Fr x2 = x * x; return x2 * x2 * x; };
     // compute_linearisation_arithmetic (widget/arithmetic.cu:47-80), q_m coeffs empty
     push(pk.q_l_coeffs, ae * qae);
@@ -485,12 +593,12 @@ int prove_impl(pnp_ctx *ctx, const CircuitC *cs, int device_ptrs, ProofC *out) {
     {
         Fr p = neg(vh);
         for (int k = 0; k < 8; k++) {
-            push(t_poly + 4 * (uint64_t)k * n, p);
+            push_local(t_poly + 4 * (uint64_t)k * len, p);  // t_poly is range-local
             p = p * zn;
         }
     }
-    uint64_t *lin = ctx->buf("lin", n);
-    k_lincomb(la, n, lin, s);
+    uint64_t *lin = ctx->buf("lin", len);
+    k_lincomb(la, len, lin, s);
     tm.mark("r5_lin");
 
     // transcript appends (gen_proof.cuh:373-403)
@@ -525,7 +633,7 @@ int prove_impl(pnp_ctx *ctx, const CircuitC *cs, int device_ptrs, ProofC *out) {
     // Both "aggregate_witness" challenges are squeezed back to back in the
     // reference (nothing is appended in between), so both witness
     // polynomials are built first and committed in one batched MSM.
-    uint64_t *comb = ctx->buf("comb", n), *comb2 = ctx->buf("comb2", n);
+    uint64_t *comb = ctx->buf("comb", len), *comb2 = ctx->buf("comb2", len);
     Fr aw = tr.challenge_scalar("aggregate_witness");
     Fr saw = tr.challenge_scalar("aggregate_witness");
     {
@@ -538,14 +646,14 @@ int prove_impl(pnp_ctx *ctx, const CircuitC *cs, int device_ptrs, ProofC *out) {
         for (int k = 0; k < 11; k++) {
             bool skip = (k == 4 && f_zero) || k == 5 || (k == 6 && table_zero);
             if (!skip) {
-                oa.p[oa.k] = awp[k];
+                oa.p[oa.k] = k == 0 ? awp[k] : awp[k] + 4 * q0;  // lin is range-local
                 oa.s[oa.k] = p;
                 oa.k++;
             }
             p = p * aw;
         }
-        k_lincomb(oa, n, comb, s);
-        k_poly_div_linear(comb, n, zc, ctx->scratch_a, s);
+        k_lincomb(oa, len, comb, s);
+        div_linear_range(ctx, comb, len, zc, dist);
     }
     {
         const uint64_t *sawp[7] = {z_poly, wpoly[0], wpoly[1], wpoly[3], zero_n /* h1 */, z2_poly,
@@ -556,20 +664,20 @@ int prove_impl(pnp_ctx *ctx, const CircuitC *cs, int device_ptrs, ProofC *out) {
         for (int k = 0; k < 7; k++) {
             bool skip = k == 4 || (k == 6 && table_zero);
             if (!skip) {
-                oa.p[oa.k] = sawp[k];
+                oa.p[oa.k] = sawp[k] + 4 * q0;
                 oa.s[oa.k] = p;
                 oa.k++;
             }
             p = p * saw;
         }
-        k_lincomb(oa, n, comb2, s);
-        k_poly_div_linear(comb2, n, zw, ctx->scratch_a, s);
+        k_lincomb(oa, len, comb2, s);
+        div_linear_range(ctx, comb2, len, zw, dist);
     }
     tm.mark("r6_witness");
     {
         const uint64_t *sc[2] = {comb, comb2};
         CommitmentC *oc[2] = {&out->aw_opening, &out->saw_opening};
-        commit_affine_batch(ctx, sc, 2, n, oc);
+        commit_affine_batch(ctx, sc, 2, n, oc, dist);
     }
     tm.mark("r6_commit");
     return PNP_OK;

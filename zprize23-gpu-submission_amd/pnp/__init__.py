@@ -28,6 +28,7 @@ ERRORS = {-1: "PNP_E_ARG", -2: "PNP_E_DEVICE", -3: "PNP_E_NOKEY", -4: "PNP_E_ENV
 SYMBOLS = ("gen_proof", "pnp_last_error", "pnp_ctx_create", "pnp_ctx_destroy",
            "pnp_load_prover_key", "pnp_load_commit_key", "pnp_prove", "pnp_last_stage_times",
            "pnp_kernel_timing", "pnp_kernel_stats", "pnp_kernel_bytes", "pnp_set_msm_shard",
+           "pnp_set_exchange_a2a",
            "pnp_sync", "pnp_ntt", "pnp_coset_lde8", "pnp_commit", "pnp_commit_ck", "pnp_poly_eval",
            "pnp_poly_div_linear", "pnp_prefix_product", "pnp_batch_inverse",
            "pnp_synth_random_fr", "pnp_synth_srs", "pnp_synth_coset_consts", "pnp_synth_circuit")
@@ -35,6 +36,8 @@ SYMBOLS = ("gen_proof", "pnp_last_error", "pnp_ctx_create", "pnp_ctx_destroy",
 
 # int allgather(void *user, uint64_t bytes_per_rank) — pnp_set_msm_shard
 ALLGATHER_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_uint64)
+# int alltoall(void *user, uint64_t bytes_per_peer) — pnp_set_exchange_a2a
+ALLTOALL_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_uint64)
 
 
 class PnpError(RuntimeError):
@@ -72,6 +75,7 @@ def load(path: str = LIB_PATH):
     lib.pnp_kernel_stats.argtypes = [vp, C.c_char_p, C.POINTER(C.c_double), C.POINTER(C.c_int)]
     lib.pnp_kernel_bytes.argtypes = [vp, C.c_char_p, C.POINTER(C.c_double)]
     lib.pnp_set_msm_shard.argtypes = [vp, i32, i32, ALLGATHER_FN, vp, vp, u64]
+    lib.pnp_set_exchange_a2a.argtypes = [vp, ALLTOALL_FN, vp, vp, u64]
     lib.pnp_sync.argtypes = [vp]
     lib.pnp_ntt.argtypes = [vp, vp, C.c_uint32, i32, i32]
     lib.pnp_coset_lde8.argtypes = [vp, vp, vp, C.c_uint32]
@@ -160,7 +164,13 @@ class Context:
         check(self.lib.pnp_set_msm_shard(self.h, exchange.rank, exchange.world, cb, None,
                                          exchange.buf.data_ptr(), exchange.buf.numel() * 8),
               "pnp_set_msm_shard")
-        self._exchange = (exchange, cb)  # keep the callback alive
+        keep = [exchange, cb]
+        if exchange.a2a is not None:  # distributed round 4 (call before load_prover_key)
+            cb2 = exchange.c_alltoall()
+            check(self.lib.pnp_set_exchange_a2a(self.h, cb2, None, exchange.a2a.data_ptr(),
+                                                exchange.a2a.numel() * 8), "pnp_set_exchange_a2a")
+            keep.append(cb2)
+        self._exchange = keep  # keep the callbacks alive
 
     def kernel_stats(self, name: str):
         ms, cnt = C.c_double(), C.c_int()

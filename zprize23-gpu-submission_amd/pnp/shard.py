@@ -1,38 +1,43 @@
-"""Multi-GPU gen_proof: window-sharded MSM exchange (include/pnp_plonk.h,
-pnp_set_msm_shard).
+"""Multi-GPU gen_proof exchange (include/pnp_plonk.h, pnp_set_msm_shard and
+pnp_set_exchange_a2a).
 
 The reference proves on one GPU; SURVEY.md §8(e) maps its multi-GPU story to
-sharding the MSM bucket windows across the GPUs of a node.  Every rank runs
-the whole (replicated, deterministic) gen_proof pipeline; inside each batched
-MSM rank r accumulates and reduces only its contiguous slice of the virtual
-windows, writes the slice's window sums (XYZZ, 192 B each) into its slot of a
-shared HBM buffer, and this module's callback all-gathers the slots in place.
-The exchange is a few KiB per MSM batch, so one RCCL all-gather over xGMI
-costs microseconds; gloo (CPU tests, or several ranks sharing one GPU) goes
-through host memory.
+sharding the MSMs across the GPUs of a node.  Every rank runs the whole
+gen_proof and returns the same ProofC:
+  * MSMs: rank r takes a contiguous point range (every window) and the B
+    partial sums of a batch meet in one in-place all-gather of B x 192 B
+    (`gather`); the same slots carry a few scalars per rank.
+  * round 4 (optional, `a2a_bytes` > 0, world | 8): rank r owns 8/world of the
+    8n coset blocks for the LDEs and the quotient and one coefficient range of
+    everything after; one all-to-all (`alltoall`) moves the inverse block
+    transforms into coefficient ranges.
+RCCL (backend "nccl") runs both collectives on device buffers over xGMI; gloo
+(CPU tests, or several ranks sharing one GPU) goes through host memory.
 """
 import ctypes as C
 
-from . import ALLGATHER_FN
+from . import ALLGATHER_FN, ALLTOALL_FN
 
 
 class WindowExchange:
-    """In-place all-gather of per-rank MSM window-sum slots.
+    """Device buffers and collectives of one rank.
 
-    `buf` is an int64 tensor (HBM when `device` is a GPU) whose first
-    world * bytes_per_rank bytes are laid out slot-major; the library writes
-    slot `rank` and expects all slots filled after `gather` returns."""
+    `buf`: the all-gather slots (world * bytes_per_rank, rank-major).
+    `a2a`: the all-to-all buffer, send slots then receive slots."""
 
     def __init__(self, rank: int, world: int, group=None, device=None,
-                 capacity_bytes: int = 1 << 20):
+                 capacity_bytes: int = 1 << 20, a2a_bytes: int = 0):
         import torch
         import torch.distributed as dist
         self.rank, self.world, self.group = rank, world, group
         self.buf = torch.zeros(capacity_bytes // 8, dtype=torch.int64, device=device)
+        self.a2a = (torch.zeros(a2a_bytes // 8, dtype=torch.int64, device=device)
+                    if a2a_bytes and world > 1 else None)
         if self.buf.is_cuda:
             torch.cuda.synchronize()
         self.backend = dist.get_backend(group) if world > 1 else "none"
         self.calls = 0
+        self.a2a_calls = 0
         self.error = None
 
     def gather(self, bytes_per_rank: int) -> None:
@@ -56,6 +61,30 @@ class WindowExchange:
                 torch.cuda.current_stream().synchronize()
         self.calls += 1
 
+    def alltoall(self, bytes_per_peer: int) -> None:
+        import torch
+        import torch.distributed as dist
+        if self.a2a is None or bytes_per_peer % 8 or 2 * bytes_per_peer * self.world > self.a2a.numel() * 8:
+            raise ValueError(f"bad all-to-all slot size {bytes_per_peer}")
+        w = bytes_per_peer // 8
+        send = self.a2a[: w * self.world]
+        recv = self.a2a[w * self.world: 2 * w * self.world]
+        if self.a2a.is_cuda and self.backend == "nccl":
+            dist.all_to_all_single(recv, send, group=self.group)
+            torch.cuda.current_stream().synchronize()
+        else:
+            # through host memory, one exchange per peer pair (gloo)
+            h_send = send.cpu().clone()
+            h_recv = torch.empty_like(h_send)
+            if self.backend == "gloo":
+                dist.all_to_all_single(h_recv, h_send, group=self.group)
+            else:
+                h_recv.copy_(h_send)
+            recv.copy_(h_recv)
+            if self.a2a.is_cuda:
+                torch.cuda.current_stream().synchronize()
+        self.a2a_calls += 1
+
     def c_callback(self):
         def cb(_user, bytes_per_rank):
             try:
@@ -65,3 +94,22 @@ class WindowExchange:
                 self.error = e
                 return 1
         return ALLGATHER_FN(cb)
+
+    def c_alltoall(self):
+        def cb(_user, bytes_per_peer):
+            try:
+                self.alltoall(int(bytes_per_peer))
+                return 0
+            except Exception as e:
+                self.error = e
+                return 1
+        return ALLTOALL_FN(cb)
+
+
+def a2a_bytes_for(lg_n: int, world: int) -> int:
+    """All-to-all buffer of the distributed round 4 (0 when world does not
+    divide 8): send + receive slots of (8/world blocks) x (n/world) Fr."""
+    if world <= 1 or 8 % world:
+        return 0
+    n = 1 << lg_n
+    return 2 * world * (8 // world) * (n // world) * 32
