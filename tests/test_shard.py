@@ -3,8 +3,8 @@ distributed round 4.
 
 CPU: world_size-2 gloo ranks exercise the in-place slot all-gather and the
 all-to-all.
-GPU: 2, 3 and 4 ranks share the one GPU (gloo exchanges through host memory)
-and must each return the oracle's ProofC byte for byte — 2 and 4 ranks run the
+GPU: 2, 3, 4 and 8 ranks share the one GPU (gloo exchanges through host memory)
+and must each return the oracle's ProofC byte for byte — 2, 4 and 8 ranks run the
 distributed quotient (blocks + coefficient ranges + one all-to-all), 3 ranks
 (does not divide 8) only shard the MSMs, with uneven point ranges."""
 import os
@@ -53,7 +53,7 @@ def test_window_exchange_gloo_world2(tmp_path):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("world", [2, 3, 4])
+@pytest.mark.parametrize("world", [2, 3, 4, 8])
 def test_sharded_gen_proof_parity(tmp_path, world):
     from pnp_testlib import Inputs
     from pnp import abi
