@@ -124,12 +124,27 @@ class Synthetic:
                                w_r=abi.ptr(w["w_r"]), w_o=abi.ptr(w["w_o"]), w_4=abi.ptr(w["w_4"]))
 
 
-# integer-VALU ceiling of k_accumulate: one XYZZ mixed add = 10 Fq products,
-# each ~288 v_mad_u64_u32 (12x12 limb products for a*b and m*p, FIPS form);
-# v_mad_u64_u32 measured at ~62 lane-ops/clk/CU (tools/ubench_int.hip) x 256 CUs
-# x 2.4 GHz
-VALU_MAD_PER_S = 62 * 256 * 2.4e9
-MAD_PER_MADD = 10 * 288
+# Integer-VALU (issue) ceiling of k_accumulate29: one XYZZ mixed addition in
+# radix-2^29 Fq compiles to 3738 v_mad_u64_u32 + 292 v_lshl_add_u64 + 260
+# v_lshrrev_b64 + 140 v_mul_lo_u32 + 78 v_add3_u32 (~4.1-4.4 cycles per wave64
+# instruction each) + ~600 two-cycle ops (v_and/v_sub/v_lshrrev_b32): ~20,800
+# SIMD cycles per 64 madds (ISA of msm.hip, costs from tools/ubench_ops.hip).
+MADD_ISSUE_CYCLES = 20820
+SIMDS, CLOCK_HZ = 256 * 4, 2.4e9
+
+
+PMC_FILE = os.path.join(REPO, "profiles", "r01_pmc", "accumulate_traffic.json")
+
+
+def pmc_traffic():
+    """HBM bytes per k_accumulate29 launch from the committed rocprofv3 PMC
+    passes (FETCH_SIZE and WRITE_SIZE in separate runs of this bench; see
+    DESIGN.md 5), or None when absent — PMC counters cannot be read live."""
+    try:
+        with open(PMC_FILE) as f:
+            return json.load(f)["bytes_per_launch"]
+    except (OSError, ValueError, KeyError):
+        return None
 
 
 def cpu_baseline(lg: int, seconds_budget: float):
@@ -223,7 +238,7 @@ def main():
         # (credited bytes / 128) * W, W = 256/16 windows at c = 16 (n >= 2^20)
         n_windows = 16 if args.lg >= 20 else -(-256 // max(args.lg - 3, 4))
         madds_per_s = acc_bytes / 128 * n_windows / (acc_ms / 1e3) if acc_ms > 0 else 0.0
-        valu_peak = VALU_MAD_PER_S / MAD_PER_MADD
+        valu_peak = SIMDS * CLOCK_HZ * 64 / MADD_ISSUE_CYCLES
         q_gbs = q_bytes / (q_ms / 1e3) / 1e9 if q_ms > 0 else 0.0
         out = {
             "metric": METRIC,
@@ -242,9 +257,9 @@ def main():
                                    f"quotient on 2^{args.lg + 3} coset, pk+SRS+witness HBM-resident",
                        "domain_log2": args.lg, "gates": gates,
                        "parallelism": f"msm-window-shard x{world}" if world > 1 else "single"},
-            "roofline": {"bound": "hbm", "kernel": "k_accumulate (MSM bucket accumulation)",
+            "roofline": {"bound": "hbm", "kernel": "k_accumulate29 (MSM bucket accumulation)",
                          "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
+                         "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": pmc_traffic(),
                          "note": "k_accumulate is integer-VALU bound (XYZZ mixed adds), not "
                                  "HBM bound; algorithmic bytes = points*(96+32) per window "
                                  "sweep (SURVEY 8d); 'valu' gives the binding ceiling",

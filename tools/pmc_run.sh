@@ -5,8 +5,9 @@
 set -e
 R=$(pwd)
 TAG=${1:-pmc}
-RX='k_accumulate|k_dif_pass|k_quotient|k_scatter|k_reduce|k_bitrev_tiles|k_hist'
+RX='k_accumulate29|k_dif_pass|k_quotient|k_coarse_scatter|k_fine_sort|k_tree_level|k_bitrev_tiles|k_lde_twist|k_t_combine'
 cd /tmp && export TMPDIR=/tmp
+mkdir -p $R/gpurun_out/$TAG
 i=0
 for P in "FETCH_SIZE" "WRITE_SIZE" "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVES"; do
   i=$((i+1))

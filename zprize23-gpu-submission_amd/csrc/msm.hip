@@ -53,8 +53,14 @@ __global__ void k_digits(const uint64_t *scalars, uint64_t n, int c, int W, uint
     for (int w = 0; w < W; w++) {
         int bit = w * c;
         int li = bit >> 5, sh = bit & 31;
-        uint64_t word = li < 8 ? s.v[li] : 0;
-        if (li + 1 < 8) word |= (uint64_t)s.v[li + 1] << 32;
+        // limbs li, li + 1 by selects (a dynamic register index would go to scratch)
+        uint32_t lo32 = 0, hi32 = 0;
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+            lo32 = li == k ? s.v[k] : lo32;
+            hi32 = li + 1 == k ? s.v[k] : hi32;
+        }
+        uint64_t word = lo32 | ((uint64_t)hi32 << 32);
         uint32_t raw = (uint32_t)(word >> sh) & ((1u << c) - 1);
         raw += carry;
         uint32_t key = KEY_ZERO;

@@ -476,7 +476,7 @@ void intt_blocks(NttTables &t, uint64_t *d, uint32_t lg_n, int m0, int nb, hipSt
 // transforms Y_m (block-major, `len` entries each, covering u in [q0, q0+len)):
 //   c_(u + n m1) = g^-(u + n m1) / (8n) sum_m w_8^(-m m1) Y_m[u]
 // -> out[m1 len + (u - q0)]: radix-2 8-point inverse DFT per u.
-__global__ void k_t_combine(const uint64_t *Y, uint64_t len, uint64_t q0, uint64_t *out, Fr w1, Fr w2,
+__global__ __launch_bounds__(256) void k_t_combine(const uint64_t *Y, uint64_t len, uint64_t q0, uint64_t *out, Fr w1, Fr w2,
                             Fr w3, Fr inv8n, const uint64_t *chi, const uint64_t *clo, Fr gn0, Fr gn1,
                             Fr gn2, Fr gn3, Fr gn4, Fr gn5, Fr gn6, Fr gn7) {
     uint64_t u = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
