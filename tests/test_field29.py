@@ -58,6 +58,33 @@ def mul29(a, b):
     return r
 
 
+def sqr29(a):
+    """sqr29 of field29.cuh: cross products against doubled limbs."""
+    assert all(x < 2**29 for x in a)
+    q = C["F29_Q"]
+    a2 = [2 * x for x in a]
+    m, r, acc = [0] * 14, [0] * 14, 0
+    for k in range(27):
+        for i in range(max(0, k - 13), 14):
+            if 2 * i < k and k - i <= 13:
+                acc += a[i] * a2[k - i]
+        if k % 2 == 0:
+            acc += a[k // 2] * a[k // 2]
+        for i in range(max(0, k - 13), min(k, 14)):
+            acc += m[i] * q[k - i]
+        if k < 14:
+            m[k] = ((acc & 0xFFFFFFFF) * QINV) & M29
+            acc += m[k] * q[0]
+            assert acc & M29 == 0
+        else:
+            r[k - 14] = acc & M29
+        assert acc < 2**64
+        acc >>= 29
+    r[13] = acc
+    assert acc < 2**29
+    return r
+
+
 def sub29(a, b, K):
     r, c = [0] * 14, 0
     for i in range(13):
@@ -98,6 +125,10 @@ def test_mul_exact_and_bounded():
         r = mul29(limbs(a), limbs(b))
         assert val(r) % Q == a * b * pow(R406, -1, Q) % Q
         assert val(r) < 2**382
+        s = sqr29(limbs(a))
+        assert val(s) == val(mul29(limbs(a), limbs(a)))
+    top = limbs(2**391 - 1)  # every limb at its maximum: worst column sums
+    assert val(sqr29(top)) == val(mul29(top, top))
 
 
 # ---- G1 (y^2 = x^3 + 4) affine reference
@@ -121,10 +152,10 @@ def madd29(p, x2, y2):
     u2, s2 = mul29(x2, ZZ), mul29(y2, ZZZ)
     P, R = sub29(u2, X, KB), sub29(s2, Y, KB)
     assert val(P) < 2**391 and val(R) < 2**391
-    pp = mul29(P, P)
+    pp = sqr29(P)
     ppp = mul29(P, pp)
     q = mul29(X, pp)
-    x3 = sub29(sub29(sub29(mul29(R, R), ppp, KA), q, KA), q, KA)
+    x3 = sub29(sub29(sub29(sqr29(R), ppp, KA), q, KA), q, KA)
     assert val(x3) < 2**389
     t = sub29(q, x3, KB)
     assert val(t) < 2**391

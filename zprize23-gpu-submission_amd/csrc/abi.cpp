@@ -155,6 +155,12 @@ void pnp_ctx_destroy(pnp_ctx *ctx) {
     if (!ctx) return;
     (void)hipSetDevice(ctx->device);
     (void)hipStreamSynchronize(ctx->stream);
+    if (ctx->msm.s2) {
+        (void)hipStreamSynchronize(ctx->msm.s2);
+        (void)hipStreamDestroy(ctx->msm.s2);
+    }
+    for (hipEvent_t e : ctx->msm.ev)
+        if (e) (void)hipEventDestroy(e);
     (void)hipStreamDestroy(ctx->stream);
     delete ctx;
 }

@@ -51,6 +51,35 @@ __device__ __forceinline__ F29 mul29(const F29 &a, const F29 &b) {
     return r;
 }
 
+// Montgomery square: the cross products a_i a_j (i < j) once, against the
+// doubled limb 2 a_j (< 2^30): a column then holds <= 7 products < 2^59, 1
+// square < 2^58 and <= 14 reduction products < 2^58 — still < 2^64.
+// 105 + 196 multiply-adds instead of 196 + 196.
+__device__ __forceinline__ F29 sqr29(const F29 &a) {
+    uint32_t m[14], a2[14];
+#pragma unroll
+    for (int i = 0; i < 14; i++) a2[i] = a.l[i] << 1;
+    F29 r;
+    uint64_t acc = 0;
+#pragma unroll
+    for (int k = 0; k < 27; k++) {
+#pragma unroll
+        for (int i = (k > 13 ? k - 13 : 0); 2 * i < k; i++) acc += (uint64_t)a.l[i] * a2[k - i];
+        if ((k & 1) == 0) acc += (uint64_t)a.l[k / 2] * a.l[k / 2];
+#pragma unroll
+        for (int i = (k > 13 ? k - 13 : 0); i < (k < 14 ? k : 14); i++) acc += (uint64_t)m[i] * F29_Q[k - i];
+        if (k < 14) {
+            m[k] = ((uint32_t)acc * F29_QINV) & F29_M;
+            acc += (uint64_t)m[k] * F29_Q[0];
+        } else {
+            r.l[k - 14] = (uint32_t)acc & F29_M;
+        }
+        acc >>= 29;
+    }
+    r.l[13] = (uint32_t)acc;
+    return r;
+}
+
 // a + K - b (K = F29_KA or F29_KB, b < K), carries normalised
 __device__ __forceinline__ F29 sub29(const F29 &a, const F29 &b, const uint32_t *K) {
     F29 r;

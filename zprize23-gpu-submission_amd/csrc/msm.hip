@@ -446,10 +446,10 @@ __device__ __forceinline__ void madd29(Xyzz29 &p, const F29 &x2, const F29 &y2) 
     F29 s2 = mul29(y2, p.zzz);
     F29 P = sub29(u2, p.x, F29_KB);
     F29 R = sub29(s2, p.y, F29_KB);
-    F29 pp = mul29(P, P);
+    F29 pp = sqr29(P);
     F29 ppp = mul29(P, pp);
     F29 q = mul29(p.x, pp);
-    F29 x3 = sub29(sub29(sub29(mul29(R, R), ppp, F29_KA), q, F29_KA), q, F29_KA);
+    F29 x3 = sub29(sub29(sub29(sqr29(R), ppp, F29_KA), q, F29_KA), q, F29_KA);
     F29 y3 = sub29(mul29(R, sub29(q, x3, F29_KB)), mul29(p.y, ppp), F29_KA);
     p.zz = mul29(p.zz, pp);
     p.zzz = mul29(p.zzz, ppp);
@@ -466,7 +466,10 @@ __device__ __forceinline__ bool store29(uint64_t *dst, const Xyzz29 &p) {
     return !zz.is_zero();
 }
 
-__global__ __launch_bounds__(256) void k_accumulate29(const uint32_t *pts29, const uint32_t *sorted,
+#ifndef PNP_ACC_WAVES
+#define PNP_ACC_WAVES 3
+#endif
+__global__ __launch_bounds__(256, PNP_ACC_WAVES) void k_accumulate29(const uint32_t *pts29, const uint32_t *sorted,
                                                       const uint32_t *offs, uint64_t U, uint32_t S,
                                                       uint64_t *buckets, uint64_t *head,
                                                       uint64_t *tail, uint32_t *redo,
@@ -519,9 +522,9 @@ __global__ __launch_bounds__(64) void k_accumulate_redo(const uint32_t *pts29, c
                                                         const uint32_t *offs, uint64_t U, uint32_t S,
                                                         uint64_t *buckets, uint64_t *head,
                                                         uint64_t *tail, const uint32_t *redo,
-                                                        uint32_t nredo) {
+                                                        const uint32_t *nredo) {
     uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
-    if (r >= nredo) return;
+    if (r >= *nredo) return;
     auto ld = [pts29](uint32_t i, Fq &x, Fq &y) {
         x = to_fq32(load29(pts29 + 28ULL * i));
         y = to_fq32(load29(pts29 + 28ULL * i + 14));
@@ -631,6 +634,114 @@ static Xyzz get_xyzz(const uint64_t *e) {
 // (XYZZ) land in h_xyzz.  Per-window layout: the B*W windows are "virtual
 // windows" of NB buckets each.  Folded layout (table != nullptr): virtual
 // window b = MSM b with the W key rows of its windows, one bucket set.
+// ---- one group of virtual windows: sort, accumulate (+ merge), reduce
+struct GroupPlan {
+    KeyRows kr;
+    int nv;  // virtual windows (bucket sets)
+};
+
+static void sort_group(MsmWork &wk, MsmGroup &gb, const uint32_t *keys, const GroupPlan &gp,
+                       const MsmCfg &g, hipStream_t s) {
+    const int nv = gp.nv;
+    const uint64_t n = gp.kr.n, WB = (uint64_t)nv * g.NB;
+    // points per coarse-pass workgroup: ~512 workgroups in all, >= 1024 points each
+    const int nch0 = std::max(1, 512 / std::max(nv, 1));
+    const uint64_t chunk = std::max<uint64_t>(1024, (n + nch0 - 1) / nch0);
+    const int nch = (int)((n + chunk - 1) / chunk);
+    const int cb = std::min(SORT_CB, g.c - 1), fb = g.c - 1 - cb, NBc = 1 << cb;
+    if (fb > SORT_FB_MAX) {
+        set_error("msm: window of %d bits exceeds the sort's %d", g.c, SORT_CB + SORT_FB_MAX + 1);
+        throw Error(PNP_E_ARG);
+    }
+    const uint64_t nbins = (uint64_t)nv * NBc;
+    const uint64_t nent = (uint64_t)nv * gp.kr.rows * n;  // upper bound (zero digits drop out)
+    auto need = [](DevBuf &b, size_t bytes) { if (b.bytes < bytes) b.alloc(bytes); };
+    need(gb.counts, (nbins * nch + 1) * 4);
+    need(gb.offsets, (WB + 1) * 4);
+    need(gb.ent, nent * 4 + 4);
+    need(gb.fkey, nent * 2 + 8);
+    need(gb.sorted, nent * 4 + 4);
+    uint32_t *counts = static_cast<uint32_t *>(gb.counts.p);
+    uint32_t *bstart = static_cast<uint32_t *>(gb.offsets.p);
+    dim3 grid((uint32_t)nch, (uint32_t)nv);
+    hipLaunchKernelGGL(k_coarse_hist, grid, dim3(1024), 0, s, keys, gp.kr, fb, NBc, chunk, nch, counts);
+    PNP_HIP(hipGetLastError());
+    const uint64_t ncount = nbins * nch;
+    PNP_HIP(hipMemsetAsync(counts + ncount, 0, 4, s));
+    scan_u32(counts, ncount + 1, gb.scan_tmp, s);  // counts[ncount] = total
+    uint32_t *ent = static_cast<uint32_t *>(gb.ent.p);
+    uint16_t *fk = static_cast<uint16_t *>(gb.fkey.p);
+    hipLaunchKernelGGL(k_coarse_scatter, grid, dim3(1024), 0, s, keys, gp.kr, fb, NBc, chunk, nch,
+                       counts, ent, fk);
+    PNP_HIP(hipGetLastError());
+    hipLaunchKernelGGL(k_fine_sort, dim3((uint32_t)nbins), dim3(1024), 0, s, ent, fk, counts, nch, fb,
+                       bstart, static_cast<uint32_t *>(gb.sorted.p));
+    PNP_HIP(hipGetLastError());
+    PNP_HIP(hipMemcpyAsync(bstart + WB, counts + ncount, 4, hipMemcpyDeviceToDevice, s));
+}
+
+// buckets of the group (XYZZ, R384) into gb.buckets
+static void accumulate_group(MsmWork &wk, MsmGroup &gb, const GroupPlan &gp, const MsmCfg &g,
+                             const uint64_t *pts, const uint64_t *table, hipStream_t s) {
+    const int nv = gp.nv;
+    const uint64_t n = gp.kr.n, WB = (uint64_t)nv * g.NB;
+    const uint64_t nent = (uint64_t)nv * gp.kr.rows * n;
+    auto need = [](DevBuf &b, size_t bytes) { if (b.bytes < bytes) b.alloc(bytes); };
+    need(gb.buckets, (WB * 24 + WB * 72 + 64) * 8);  // buckets + reduction tree scratch
+    const uint32_t *bstart = static_cast<const uint32_t *>(gb.offsets.p);
+    const uint32_t *sorted = static_cast<const uint32_t *>(gb.sorted.p);
+    uint64_t *bk = gb.buckets.u64();
+    hipEvent_t ev0 = nullptr;
+    if (wk.timer) wk.timer->begin("msm_accumulate", s, ev0);
+    // balanced accumulate: S entries per thread, S >= 64 or ~2^20 lanes (every
+    // bucket piece beyond the first costs an addition in msm_merge_pieces)
+    const uint32_t S = (uint32_t)std::max<uint64_t>(64, (nent >> 20) & ~7ULL);
+    const uint64_t nthr = (nent + S - 1) / S;
+    need(gb.seg, nthr * 2 * 24 * 8);
+    uint64_t *head = gb.seg.u64(), *tail = head + nthr * 24;
+    if (table) {
+        need(gb.redo, nthr * 4 + 16);
+        uint32_t *nredo = static_cast<uint32_t *>(gb.redo.p), *redo = nredo + 4;
+        PNP_HIP(hipMemsetAsync(nredo, 0, 4, s));
+        const uint32_t *t29 = reinterpret_cast<const uint32_t *>(table);
+        const uint32_t blocks = (uint32_t)((nthr + 255) / 256);
+        hipLaunchKernelGGL(k_accumulate29, dim3(blocks), dim3(256), 0, s, t29, sorted, bstart, WB, S, bk,
+                           head, tail, redo, nredo);
+        PNP_HIP(hipGetLastError());
+        // equal / opposite points or infinity inside a piece: exact recomputation
+        // of the flagged lanes (the count stays on the device: no host sync)
+        hipLaunchKernelGGL(k_accumulate_redo, dim3((uint32_t)((nthr + 63) / 64)), dim3(64), 0, s, t29,
+                           sorted, bstart, WB, S, bk, head, tail, redo, nredo);
+        PNP_HIP(hipGetLastError());
+    } else {
+        hipLaunchKernelGGL(k_accumulate_flat, dim3((uint32_t)((nthr + 255) / 256)), dim3(256), 0, s, pts,
+                           sorted, bstart, 1, WB, S, bk, head, tail);
+        PNP_HIP(hipGetLastError());
+    }
+    msm_merge_pieces(bstart, 1, WB, S, (uint32_t)(nent / WB / S + 1), head, tail, bk, s);
+    // algorithmic bytes: each point (96 B) and scalar (32 B)
+    // once per window sweep
+    if (wk.timer) wk.timer->end("msm_accumulate", s, ev0, (double)n * 128.0 * nv * gp.kr.rows / g.W);
+}
+
+static const uint64_t *reduce_group(MsmGroup &gb, const GroupPlan &gp, const MsmCfg &g, hipStream_t s) {
+    const uint64_t WB = (uint64_t)gp.nv * g.NB;
+    uint64_t *bk = gb.buckets.u64();
+    return msm_reduce(bk, (uint64_t)gp.nv, g.NB, bk + WB * 24, s);
+}
+
+static hipEvent_t ev_get(MsmWork &wk, int i) {
+    if (!wk.ev[i]) PNP_HIP(hipEventCreateWithFlags(&wk.ev[i], hipEventDisableTiming));
+    return wk.ev[i];
+}
+
+// B independent MSMs over the same n points, on this GPU only; the B results
+// (XYZZ) land in h_xyzz.  Per-window layout: the B*W windows are "virtual
+// windows" of NB buckets each.  Folded layout (table != nullptr): virtual
+// window b = MSM b with the W key rows of its windows, one bucket set.
+// Optionally (PNP_MSM_PIPE) the batch is split into two groups (halves of the
+// MSMs, or of the windows when B = 1) pipelined over two streams: group 1's
+// sort beside group 0's accumulation, group 0's bucket tree beside group 1's.
 static void msm_local_batch(MsmWork &wk, const uint64_t *d_points, const uint64_t *const *d_scalars,
                             int B, uint64_t n, uint64_t *h_xyzz, hipStream_t s,
                             const uint64_t *table) {
@@ -640,123 +751,97 @@ static void msm_local_batch(MsmWork &wk, const uint64_t *d_points, const uint64_
     }
     const bool folded = table != nullptr;
     const MsmCfg g = msm_cfg(n, folded ? wk.fold_c : 0);
-    KeyRows kr;
-    kr.n = n;
-    const int nv = folded ? B : B * g.W;  // virtual windows
-    if (folded) {
-        kr.vstride = g.W;
-        kr.off = 0;
-        kr.rows = g.W;
-        kr.id_row0 = 0;
-        kr.id_mul = n;
-    } else {
-        kr.vstride = 1;
-        kr.off = 0;
-        kr.rows = 1;
-        kr.id_row0 = 0;
-        kr.id_mul = 0;
-    }
-    const uint64_t WB = (uint64_t)nv * g.NB;
-    // points per coarse-pass workgroup: ~512 workgroups in all, >= 1024 points each
-    const int nch0 = std::max(1, 512 / std::max(nv, 1));
-    const uint64_t chunk = std::max<uint64_t>(1024, (n + nch0 - 1) / nch0);
-    const int nch = (int)((n + chunk - 1) / chunk);
     auto need = [](DevBuf &b, size_t bytes) { if (b.bytes < bytes) b.alloc(bytes); };
     need(wk.digits, (uint64_t)g.W * B * n * 4);
-    const int cb = std::min(SORT_CB, g.c - 1), fb = g.c - 1 - cb, NBc = 1 << cb;
-    if (fb > SORT_FB_MAX) {
-        set_error("msm: window of %d bits exceeds the sort's %d", g.c, SORT_CB + SORT_FB_MAX + 1);
-        throw Error(PNP_E_ARG);
-    }
-    const uint64_t nbins = (uint64_t)nv * NBc;
-    const uint64_t nent = (uint64_t)nv * kr.rows * n;  // upper bound (zero digits drop out)
-    need(wk.counts, (nbins * nch + 1) * 4);
-    need(wk.offsets, (WB + 1) * 4);
-    need(wk.ent, nent * 4 + 4);
-    need(wk.fkey, nent * 2 + 8);
-    need(wk.sorted, nent * 4 + 4);
-    need(wk.buckets, (WB * 24 + WB * 72 + 64) * 8);  // buckets + reduction tree scratch
     uint32_t *keys = static_cast<uint32_t *>(wk.digits.p);
-    uint32_t *counts = static_cast<uint32_t *>(wk.counts.p);
-    uint32_t *bstart = static_cast<uint32_t *>(wk.offsets.p);
-    uint32_t *sorted = static_cast<uint32_t *>(wk.sorted.p);
-    const uint64_t *pts = folded ? table : d_points;
-
-    const uint64_t *res = nullptr;  // nv XYZZ window sums on the device
-    {
-        for (int b = 0; b < B; b++) {
-            hipLaunchKernelGGL(k_digits, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, s,
-                               d_scalars[b], n, g.c, g.W, keys + (uint64_t)b * g.W * n);
-            PNP_HIP(hipGetLastError());
-        }
-        dim3 grid((uint32_t)nch, (uint32_t)nv);
-        hipLaunchKernelGGL(k_coarse_hist, grid, dim3(1024), 0, s, keys, kr, fb, NBc, chunk, nch,
-                           counts);
+    for (int b = 0; b < B; b++) {
+        hipLaunchKernelGGL(k_digits, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, s, d_scalars[b], n,
+                           g.c, g.W, keys + (uint64_t)b * g.W * n);
         PNP_HIP(hipGetLastError());
-        const uint64_t ncount = nbins * nch;
-        PNP_HIP(hipMemsetAsync(counts + ncount, 0, 4, s));
-        scan_u32(counts, ncount + 1, wk.scan_tmp, s);  // counts[ncount] = total
-        uint32_t *ent = static_cast<uint32_t *>(wk.ent.p);
-        uint16_t *fk = static_cast<uint16_t *>(wk.fkey.p);
-        hipLaunchKernelGGL(k_coarse_scatter, grid, dim3(1024), 0, s, keys, kr, fb, NBc, chunk, nch,
-                           counts, ent, fk);
-        PNP_HIP(hipGetLastError());
-        hipLaunchKernelGGL(k_fine_sort, dim3((uint32_t)nbins), dim3(1024), 0, s, ent, fk, counts,
-                           nch, fb, bstart, sorted);
-        PNP_HIP(hipGetLastError());
-        PNP_HIP(hipMemcpyAsync(bstart + WB, counts + ncount, 4, hipMemcpyDeviceToDevice, s));
-        uint64_t *bk = wk.buckets.u64();
-        hipEvent_t ev0 = nullptr;
-        if (wk.timer) wk.timer->begin("msm_accumulate", s, ev0);
-        // balanced accumulate: S entries per thread, S >= 64 or ~2^20 lanes (every
-        // bucket piece beyond the first costs an addition in msm_merge_pieces)
-        const uint32_t S = (uint32_t)std::max<uint64_t>(64, (nent >> 20) & ~7ULL);
-        const uint64_t nthr = (nent + S - 1) / S;
-        need(wk.seg, nthr * 2 * 24 * 8);
-        uint64_t *head = wk.seg.u64(), *tail = head + nthr * 24;
-        if (folded) {
-            need(wk.redo, nthr * 4 + 16);
-            uint32_t *nredo = static_cast<uint32_t *>(wk.redo.p), *redo = nredo + 4;
-            PNP_HIP(hipMemsetAsync(nredo, 0, 4, s));
-            const uint32_t *t29 = reinterpret_cast<const uint32_t *>(table);
-            hipLaunchKernelGGL(k_accumulate29, dim3((uint32_t)((nthr + 255) / 256)), dim3(256), 0,
-                               s, t29, sorted, bstart, WB, S, bk, head, tail, redo, nredo);
-            PNP_HIP(hipGetLastError());
-            uint32_t h_redo = 0;
-            PNP_HIP(hipMemcpyAsync(&h_redo, nredo, 4, hipMemcpyDeviceToHost, s));
-            PNP_HIP(hipStreamSynchronize(s));
-            if (h_redo) {  // equal / opposite points or infinity inside a piece
-                hipLaunchKernelGGL(k_accumulate_redo, dim3((h_redo + 63) / 64), dim3(64), 0, s, t29,
-                                   sorted, bstart, WB, S, bk, head, tail, redo, h_redo);
-                PNP_HIP(hipGetLastError());
-            }
-        } else {
-            hipLaunchKernelGGL(k_accumulate_flat, dim3((uint32_t)((nthr + 255) / 256)), dim3(256), 0,
-                               s, pts, sorted, bstart, 1, WB, S, bk, head, tail);
-            PNP_HIP(hipGetLastError());
-        }
-        msm_merge_pieces(bstart, 1, WB, S, (uint32_t)(nent / WB / S + 1), head, tail, bk, s);
-        // algorithmic bytes: each point (96 B) and scalar (32 B)
-        // once per window sweep
-        if (wk.timer)
-            wk.timer->end("msm_accumulate", s, ev0, (double)n * 128.0 * nv * kr.rows / g.W);
-        res = msm_reduce(bk, (uint64_t)nv, g.NB, bk + WB * 24, s);
     }
-    std::vector<uint64_t> win((size_t)nv * 24);
-    PNP_HIP(hipMemcpyAsync(win.data(), res, win.size() * 8, hipMemcpyDeviceToHost, s));
+    // groups: (plan, first MSM of its results)
+    GroupPlan gp[2];
+    int ng = 1, first[2] = {0, 0};
+    KeyRows kr;
+    kr.n = n;
+    // Two-stream pipelining measured 3% SLOWER per proof on MI355X (the sort
+    // and tree kernels steal issue slots from the VALU-bound accumulation and
+    // slow down themselves): one group unless PNP_MSM_PIPE=1 (experiments).
+    static const bool no_pipe = getenv("PNP_MSM_PIPE") == nullptr;
+    if (!folded) {
+        kr.vstride = 1, kr.off = 0, kr.rows = 1, kr.id_row0 = 0, kr.id_mul = 0;
+        gp[0] = {kr, B * g.W};
+    } else if (no_pipe) {
+        kr.vstride = g.W, kr.off = 0, kr.rows = g.W, kr.id_row0 = 0, kr.id_mul = n;
+        gp[0] = {kr, B};
+    } else if (B >= 2) {
+        const int h = (B + 1) / 2;
+        kr.vstride = g.W, kr.off = 0, kr.rows = g.W, kr.id_row0 = 0, kr.id_mul = n;
+        gp[0] = {kr, h};
+        kr.off = h * g.W;
+        gp[1] = {kr, B - h};
+        first[1] = h;
+        ng = 2;
+    } else if (g.W >= 2) {  // one MSM: split its windows
+        const int h = g.W / 2;
+        kr.vstride = g.W, kr.off = 0, kr.rows = h, kr.id_row0 = 0, kr.id_mul = n;
+        gp[0] = {kr, 1};
+        kr.off = h, kr.rows = g.W - h, kr.id_row0 = h;
+        gp[1] = {kr, 1};
+        ng = 2;
+    } else {
+        kr.vstride = g.W, kr.off = 0, kr.rows = g.W, kr.id_row0 = 0, kr.id_mul = n;
+        gp[0] = {kr, 1};
+    }
+    const uint64_t *pts = folded ? table : d_points;
+    const uint64_t *res[2] = {nullptr, nullptr};
+    if (ng == 1) {
+        sort_group(wk, wk.grp[0], keys, gp[0], g, s);
+        accumulate_group(wk, wk.grp[0], gp[0], g, pts, table, s);
+        res[0] = reduce_group(wk.grp[0], gp[0], g, s);
+    } else {
+        if (!wk.s2) PNP_HIP(hipStreamCreateWithFlags(&wk.s2, hipStreamNonBlocking));
+        hipEvent_t evD = ev_get(wk, 0), evS1 = ev_get(wk, 1), evA0 = ev_get(wk, 2), evR0 = ev_get(wk, 3);
+        PNP_HIP(hipEventRecord(evD, s));
+        PNP_HIP(hipStreamWaitEvent(wk.s2, evD, 0));
+        sort_group(wk, wk.grp[1], keys, gp[1], g, wk.s2);
+        PNP_HIP(hipEventRecord(evS1, wk.s2));
+        sort_group(wk, wk.grp[0], keys, gp[0], g, s);
+        accumulate_group(wk, wk.grp[0], gp[0], g, pts, table, s);
+        PNP_HIP(hipEventRecord(evA0, s));
+        PNP_HIP(hipStreamWaitEvent(wk.s2, evA0, 0));
+        res[0] = reduce_group(wk.grp[0], gp[0], g, wk.s2);
+        PNP_HIP(hipEventRecord(evR0, wk.s2));
+        PNP_HIP(hipStreamWaitEvent(s, evS1, 0));
+        accumulate_group(wk, wk.grp[1], gp[1], g, pts, table, s);
+        res[1] = reduce_group(wk.grp[1], gp[1], g, s);
+        PNP_HIP(hipStreamWaitEvent(s, evR0, 0));
+    }
+    std::vector<uint64_t> win[2];
+    for (int k = 0; k < ng; k++) {
+        win[k].resize((size_t)gp[k].nv * 24);
+        PNP_HIP(hipMemcpyAsync(win[k].data(), res[k], win[k].size() * 8, hipMemcpyDeviceToHost, s));
+    }
     PNP_HIP(hipStreamSynchronize(s));
     if (wk.timer) wk.timer->collect();
-    for (int b = 0; b < B; b++) {
-        Xyzz acc = Xyzz::inf();
-        if (folded) {
-            acc = get_xyzz(&win[(size_t)b * 24]);
-        } else {
-            for (int w = g.W - 1; w >= 0; w--) {
-                for (int k = 0; k < g.c; k++) acc = dbl(acc);
-                acc = add(acc, get_xyzz(&win[((size_t)b * g.W + w) * 24]));
+    for (int b = 0; b < B; b++) put_xyzz(Xyzz::inf(), h_xyzz + 24 * b);
+    for (int k = 0; k < ng; k++) {
+        for (int v = 0; v < gp[k].nv; v++) {
+            if (folded) {
+                const int b = B == 1 ? 0 : first[k] + v;
+                put_xyzz(add(get_xyzz(h_xyzz + 24 * b), get_xyzz(&win[k][(size_t)v * 24])), h_xyzz + 24 * b);
             }
         }
-        put_xyzz(acc, h_xyzz + 24 * b);
+    }
+    if (!folded) {
+        for (int b = 0; b < B; b++) {
+            Xyzz acc = Xyzz::inf();
+            for (int w = g.W - 1; w >= 0; w--) {
+                for (int k = 0; k < g.c; k++) acc = dbl(acc);
+                acc = add(acc, get_xyzz(&win[0][((size_t)b * g.W + w) * 24]));
+            }
+            put_xyzz(acc, h_xyzz + 24 * b);
+        }
     }
 }
 

@@ -100,14 +100,19 @@ struct KernelTimer {
 };
 
 // ---- MSM (msm.hip) ----
+// buffers of one group of an MSM batch: counts (coarse-bin counts -> offsets,
+// scan_tmp), ent/fkey (pass-A entries and fine keys), offsets (bucket
+// starts), sorted (entries by bucket), buckets (XYZZ buckets + reduction tree),
+// seg (split-bucket pieces), redo (segments the radix-2^29 accumulation hands
+// back to the exact path)
+struct MsmGroup {
+    DevBuf counts, offsets, scan_tmp, ent, fkey, sorted, buckets, seg, redo;
+};
 struct MsmWork {
-    // digits: u16 keys; counts: coarse-bin counts -> offsets (scan, scan_tmp);
-    // ent/fkey: pass-A entries and fine keys; offsets: bucket starts;
-    // sorted: entries by bucket; buckets: XYZZ buckets + reduction tree;
-    // seg: split-bucket pieces
-    // redo: segments the radix-2^29 accumulation hands back to the exact path
-    DevBuf digits, sorted, counts, offsets, scan_tmp, ent, fkey, buckets, seg, redo;
-    size_t cap_n = 0;
+    DevBuf digits;  // u32 keys of every (MSM, window, point)
+    MsmGroup grp[2];  // the two pipelined groups of a batch
+    hipStream_t s2 = nullptr;
+    hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
     KernelTimer *timer = nullptr;
     // point-range sharding across ranks (pnp_set_msm_shard)
     // window bits of the folded layout (msm_cfg default when 0; PNP_FOLD_C)

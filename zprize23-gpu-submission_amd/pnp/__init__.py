@@ -17,7 +17,8 @@ import os
 from . import abi
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(os.path.dirname(_HERE), "lib", "libpnp_plonk.so")
+LIB_PATH = os.environ.get("PNP_PLONK_LIB",
+                          os.path.join(os.path.dirname(_HERE), "lib", "libpnp_plonk.so"))
 _LIB = None
 
 PNP_OK = 0
