@@ -125,11 +125,11 @@ class Synthetic:
 
 
 # Integer-VALU (issue) ceiling of k_accumulate29: one XYZZ mixed addition in
-# radix-2^29 Fq compiles to 3738 v_mad_u64_u32 + 292 v_lshl_add_u64 + 260
+# radix-2^29 Fq compiles to 3738 v_mad_u64_u32 + 258 v_lshl_add_u64 + 260
 # v_lshrrev_b64 + 140 v_mul_lo_u32 + 78 v_add3_u32 (~4.1-4.4 cycles per wave64
-# instruction each) + ~600 two-cycle ops (v_and/v_sub/v_lshrrev_b32): ~20,800
+# instruction each) + ~600 two-cycle ops (v_and/v_sub/v_lshrrev_b32): ~20,750
 # SIMD cycles per 64 madds (ISA of msm.hip, costs from tools/ubench_ops.hip).
-MADD_ISSUE_CYCLES = 20820
+MADD_ISSUE_CYCLES = 20745
 SIMDS, CLOCK_HZ = 256 * 4, 2.4e9
 
 
@@ -217,6 +217,7 @@ def main():
     stages = ctx.stage_times()
     acc_ms, acc_n = ctx.kernel_stats("msm_accumulate")
     acc_bytes = ctx.kernel_bytes("msm_accumulate")
+    entries = ctx.kernel_bytes("msm_entries")
     q_ms, q_n = ctx.kernel_stats("quotient")
     q_bytes = ctx.kernel_bytes("quotient")
     ctx.kernel_timing(False)
@@ -234,10 +235,8 @@ def main():
         # algorithmic bytes per launch (library-credited: points x windows the
         # launch swept x 128 B) / average launch duration
         achieved = acc_bytes / (acc_ms / 1e3) / 1e9 if acc_ms > 0 else 0.0
-        # every window sweep adds each point once: madds = points*sweeps =
-        # (credited bytes / 128) * W, W = 256/16 windows at c = 16 (n >= 2^20)
-        n_windows = 16 if args.lg >= 20 else -(-256 // max(args.lg - 3, 4))
-        madds_per_s = acc_bytes / 128 * n_windows / (acc_ms / 1e3) if acc_ms > 0 else 0.0
+        # mixed additions = sorted (point, window) entries, counted by the library
+        madds_per_s = entries / (acc_ms / 1e3) if acc_ms > 0 else 0.0
         valu_peak = SIMDS * CLOCK_HZ * 64 / MADD_ISSUE_CYCLES
         q_gbs = q_bytes / (q_ms / 1e3) / 1e9 if q_ms > 0 else 0.0
         out = {

@@ -102,6 +102,31 @@ def test_msm_vs_oracle(ctx, n):
     assert (_commit_ck(ctx, pts, sc) == exp).all()
 
 
+@pytest.mark.parametrize("c", [18, 20])
+def test_msm_folded_wide_windows(c, monkeypatch):
+    """The folded fixed-base layout with the wide windows used at 2^22 (and the
+    running-sum tree leaves), forced on a small MSM (PNP_FOLD_C)."""
+    import pnp
+    monkeypatch.setenv("PNP_FOLD_C", str(c))
+    ctx = pnp.Context(0)
+    try:
+        n = 5000
+        rng = np.random.default_rng(c)
+        lib = oracle()
+        tau = rand_fr_mont_arr(rng, 1)
+        pts = np.zeros((n, 12), dtype=np.uint64)
+        lib.or_srs(vp(pts), n, vp(tau))
+        pts[100:110] = pts[7]  # repeated bases: degenerate pieces -> exact redo
+        sc = rand_fr_mont_arr(rng, n)
+        sc[::5] = 0
+        sc[100:110] = sc[7]
+        exp = np.zeros(12, dtype=np.uint64)
+        lib.or_commit(vp(pts), vp(sc), n, vp(exp))
+        assert (_commit_ck(ctx, pts, sc) == exp).all()
+    finally:
+        ctx.close()
+
+
 def test_msm_edge_cases(ctx):
     lib = oracle()
     rng = np.random.default_rng(5)

@@ -368,10 +368,12 @@ __device__ __forceinline__ uint32_t bucket_start(const uint32_t *offs, uint64_t 
 }
 // The segment walk shared by the exact kernels; `ld(e)` yields the affine
 // point of sorted entry e (sign bit stripped by the caller).
-template <class LoadPt>
-__device__ __forceinline__ void segment32(uint64_t t, LoadPt ld, const uint32_t *sorted,
-                                          const uint32_t *offs, int nch, uint64_t U, uint32_t S,
-                                          uint64_t *buckets, uint64_t *head, uint64_t *tail) {
+// The segment walk shared by the exact kernels; `ld(e)` yields the affine
+// point of sorted entry e (sign bit stripped by the caller), `st(where, i, P)`
+// stores a finished piece: where = 0 bucket i, 1 head[i], 2 tail[i].
+template <class LoadPt, class StorePt>
+__device__ __forceinline__ void segment32(uint64_t t, LoadPt ld, StorePt st, const uint32_t *sorted,
+                                          const uint32_t *offs, int nch, uint64_t U, uint32_t S) {
     const uint32_t total = bucket_start(offs, U, nch);
     const uint64_t lo64 = t * S;
     if (lo64 >= total) return;
@@ -389,8 +391,8 @@ __device__ __forceinline__ void segment32(uint64_t t, LoadPt ld, const uint32_t 
     Xyzz acc = Xyzz::inf();
     for (uint32_t k = lo; k < hi; k++) {
         if (k == next) {  // bucket boundary: emit the finished piece
-            if (first) store_xyzz(head + 24 * t, acc);
-            else store_xyzz(buckets + 24 * cur, acc);
+            if (first) st(1, t, acc);
+            else st(0, cur, acc);
             first = false;
             acc = Xyzz::inf();
             do {  // skip empty buckets
@@ -404,9 +406,9 @@ __device__ __forceinline__ void segment32(uint64_t t, LoadPt ld, const uint32_t 
         if (e >> 31) y = neg(y);
         acc = madd(acc, x, y);
     }
-    if (first) store_xyzz(head + 24 * t, acc);
-    else if (next > hi) store_xyzz(tail + 24 * t, acc);
-    else store_xyzz(buckets + 24 * cur, acc);
+    if (first) st(1, t, acc);
+    else if (next > hi) st(2, t, acc);
+    else st(0, cur, acc);
 }
 
 __global__ __launch_bounds__(256) void k_accumulate_flat(const uint64_t *points,
@@ -419,7 +421,10 @@ __global__ __launch_bounds__(256) void k_accumulate_flat(const uint64_t *points,
         x = load_fq(points + 12ULL * i);
         y = load_fq(points + 12ULL * i + 6);
     };
-    segment32(t, ld, sorted, offs, nch, U, S, buckets, head, tail);
+    auto st = [=](int where, uint64_t i, const Xyzz &p) {
+        store_xyzz((where == 0 ? buckets : where == 1 ? head : tail) + 24 * i, p);
+    };
+    segment32(t, ld, st, sorted, offs, nch, U, S);
 }
 
 // ---- radix-2^29 accumulation (field29.cuh) over the folded table in F29 form
@@ -456,14 +461,35 @@ __device__ __forceinline__ void madd29(Xyzz29 &p, const F29 &x2, const F29 &y2) 
     p.x = x3;
     p.y = y3;
 }
-// store as canonical R384 XYZZ; false when ZZ = 0 (a degenerate step)
-__device__ __forceinline__ bool store29(uint64_t *dst, const Xyzz29 &p) {
-    Fq zz = to_fq32(p.zz);
-    store_fq(dst, to_fq32(p.x));
-    store_fq(dst + 6, to_fq32(p.y));
-    store_fq(dst + 12, zz);
-    store_fq(dst + 18, to_fq32(p.zzz));
-    return !zz.is_zero();
+// Pieces leave the accumulation in raw radix-2^29 form (56 u32 per XYZZ
+// point, 4 x 14 limbs): the conversion to R384 (4 products) happens once per
+// piece in k_merge_pieces29, not on the divergent boundary path of this loop.
+__device__ __forceinline__ void store_f29(uint32_t *dst, const F29 &a) {
+    uint4 *q = reinterpret_cast<uint4 *>(dst);
+    q[0] = make_uint4(a.l[0], a.l[1], a.l[2], a.l[3]);
+    q[1] = make_uint4(a.l[4], a.l[5], a.l[6], a.l[7]);
+    q[2] = make_uint4(a.l[8], a.l[9], a.l[10], a.l[11]);
+    *reinterpret_cast<uint2 *>(dst + 12) = make_uint2(a.l[12], a.l[13]);
+}
+// ZZ is a product output (< 2^382 < 3q) with normalised limbs: zero mod q
+// iff it equals 0, q or 2q limb for limb
+__device__ __forceinline__ bool zero29(const F29 &v) {
+    uint32_t z = 0, a = 0, b = 0;
+#pragma unroll
+    for (int i = 0; i < 14; i++) {
+        z |= v.l[i];
+        a |= v.l[i] ^ F29_Q[i];
+        b |= v.l[i] ^ F29_Q2[i];
+    }
+    return z == 0 || a == 0 || b == 0;
+}
+// raw store; false when ZZ = 0 mod q (a degenerate step in the piece)
+__device__ __forceinline__ bool store29(uint32_t *dst, const Xyzz29 &p) {
+    store_f29(dst, p.x);
+    store_f29(dst + 14, p.y);
+    store_f29(dst + 28, p.zz);
+    store_f29(dst + 42, p.zzz);
+    return !zero29(p.zz);
 }
 
 #ifndef PNP_ACC_WAVES
@@ -471,8 +497,8 @@ __device__ __forceinline__ bool store29(uint64_t *dst, const Xyzz29 &p) {
 #endif
 __global__ __launch_bounds__(256, PNP_ACC_WAVES) void k_accumulate29(const uint32_t *pts29, const uint32_t *sorted,
                                                       const uint32_t *offs, uint64_t U, uint32_t S,
-                                                      uint64_t *buckets, uint64_t *head,
-                                                      uint64_t *tail, uint32_t *redo,
+                                                      uint32_t *buckets, uint32_t *head,
+                                                      uint32_t *tail, uint32_t *redo,
                                                       uint32_t *nredo) {
     uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
     const uint32_t total = offs[U];
@@ -492,7 +518,7 @@ __global__ __launch_bounds__(256, PNP_ACC_WAVES) void k_accumulate29(const uint3
     Xyzz29 acc;
     for (uint32_t k = lo; k < hi; k++) {
         if (k == next) {
-            ok &= store29(first ? head + 24 * t : buckets + 24 * cur, acc);
+            ok &= store29(first ? head + 56 * t : buckets + 56 * cur, acc);
             first = false;
             fresh = true;
             do {
@@ -513,15 +539,15 @@ __global__ __launch_bounds__(256, PNP_ACC_WAVES) void k_accumulate29(const uint3
             madd29(acc, x, y);
         }
     }
-    ok &= store29(first ? head + 24 * t : (next > hi ? tail + 24 * t : buckets + 24 * cur), acc);
+    ok &= store29(first ? head + 56 * t : (next > hi ? tail + 56 * t : buckets + 56 * cur), acc);
     if (!ok) redo[atomicAdd(nredo, 1u)] = (uint32_t)t;
 }
 
 // exact 32-bit recomputation of the segments k_accumulate29 flagged
 __global__ __launch_bounds__(64) void k_accumulate_redo(const uint32_t *pts29, const uint32_t *sorted,
                                                         const uint32_t *offs, uint64_t U, uint32_t S,
-                                                        uint64_t *buckets, uint64_t *head,
-                                                        uint64_t *tail, const uint32_t *redo,
+                                                        uint32_t *buckets, uint32_t *head,
+                                                        uint32_t *tail, const uint32_t *redo,
                                                         const uint32_t *nredo) {
     uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= *nredo) return;
@@ -529,7 +555,14 @@ __global__ __launch_bounds__(64) void k_accumulate_redo(const uint32_t *pts29, c
         x = to_fq32(load29(pts29 + 28ULL * i));
         y = to_fq32(load29(pts29 + 28ULL * i + 14));
     };
-    segment32(redo[r], ld, sorted, offs, 1, U, S, buckets, head, tail);
+    auto st = [=](int where, uint64_t i, const Xyzz &p) {
+        uint32_t *d = (where == 0 ? buckets : where == 1 ? head : tail) + 56 * i;
+        store_f29(d, from_fq32(p.x));
+        store_f29(d + 14, from_fq32(p.y));
+        store_f29(d + 28, from_fq32(p.zz));
+        store_f29(d + 42, from_fq32(p.zzz));
+    };
+    segment32(redo[r], ld, st, sorted, offs, 1, U, S);
 }
 
 // ---------------------------------------------------------------- folded table
@@ -588,7 +621,7 @@ __global__ void k_table_to29(const uint64_t *T, uint64_t count, uint32_t *T29) {
 }
 
 void msm_build_table(DevBuf &tab, const uint64_t *d_points, uint64_t n, int c, hipStream_t s) {
-    MsmCfg g = msm_cfg(n, c);
+    MsmCfg g = msm_cfg(n, c, true);
     DevBuf t32((uint64_t)g.W * n * 96);
     uint64_t *T = t32.u64();
     PNP_HIP(hipMemcpyAsync(T, d_points, n * 96, hipMemcpyDeviceToDevice, s));
@@ -697,31 +730,39 @@ static void accumulate_group(MsmWork &wk, MsmGroup &gb, const GroupPlan &gp, con
     // bucket piece beyond the first costs an addition in msm_merge_pieces)
     const uint32_t S = (uint32_t)std::max<uint64_t>(64, (nent >> 20) & ~7ULL);
     const uint64_t nthr = (nent + S - 1) / S;
-    need(gb.seg, nthr * 2 * 24 * 8);
-    uint64_t *head = gb.seg.u64(), *tail = head + nthr * 24;
     if (table) {
+        // raw radix-2^29 pieces: buckets inside one segment, then heads, tails
+        need(gb.seg, (WB + 2 * nthr) * 224);
+        uint32_t *bk29 = static_cast<uint32_t *>(gb.seg.p);
+        uint32_t *head = bk29 + 56 * WB, *tail = head + 56 * nthr;
         need(gb.redo, nthr * 4 + 16);
         uint32_t *nredo = static_cast<uint32_t *>(gb.redo.p), *redo = nredo + 4;
         PNP_HIP(hipMemsetAsync(nredo, 0, 4, s));
         const uint32_t *t29 = reinterpret_cast<const uint32_t *>(table);
         const uint32_t blocks = (uint32_t)((nthr + 255) / 256);
-        hipLaunchKernelGGL(k_accumulate29, dim3(blocks), dim3(256), 0, s, t29, sorted, bstart, WB, S, bk,
+        hipLaunchKernelGGL(k_accumulate29, dim3(blocks), dim3(256), 0, s, t29, sorted, bstart, WB, S, bk29,
                            head, tail, redo, nredo);
         PNP_HIP(hipGetLastError());
         // equal / opposite points or infinity inside a piece: exact recomputation
         // of the flagged lanes (the count stays on the device: no host sync)
         hipLaunchKernelGGL(k_accumulate_redo, dim3((uint32_t)((nthr + 63) / 64)), dim3(64), 0, s, t29,
-                           sorted, bstart, WB, S, bk, head, tail, redo, nredo);
+                           sorted, bstart, WB, S, bk29, head, tail, redo, nredo);
         PNP_HIP(hipGetLastError());
+        msm_merge_pieces29(bstart, WB, S, (uint32_t)(nent / WB / S + 1), bk29, head, tail, bk, s);
     } else {
+        need(gb.seg, nthr * 2 * 24 * 8);
+        uint64_t *head = gb.seg.u64(), *tail = head + nthr * 24;
         hipLaunchKernelGGL(k_accumulate_flat, dim3((uint32_t)((nthr + 255) / 256)), dim3(256), 0, s, pts,
                            sorted, bstart, 1, WB, S, bk, head, tail);
         PNP_HIP(hipGetLastError());
+        msm_merge_pieces(bstart, 1, WB, S, (uint32_t)(nent / WB / S + 1), head, tail, bk, s);
     }
-    msm_merge_pieces(bstart, 1, WB, S, (uint32_t)(nent / WB / S + 1), head, tail, bk, s);
     // algorithmic bytes: each point (96 B) and scalar (32 B)
     // once per window sweep
-    if (wk.timer) wk.timer->end("msm_accumulate", s, ev0, (double)n * 128.0 * nv * gp.kr.rows / g.W);
+    if (wk.timer) {
+        wk.timer->end("msm_accumulate", s, ev0, (double)n * 128.0 * nv * gp.kr.rows / g.W);
+        wk.timer->credit("msm_entries", (double)nent);  // ~ mixed additions (zero digits drop out)
+    }
 }
 
 static const uint64_t *reduce_group(MsmGroup &gb, const GroupPlan &gp, const MsmCfg &g, hipStream_t s) {
@@ -750,7 +791,7 @@ static void msm_local_batch(MsmWork &wk, const uint64_t *d_points, const uint64_
         return;
     }
     const bool folded = table != nullptr;
-    const MsmCfg g = msm_cfg(n, folded ? wk.fold_c : 0);
+    const MsmCfg g = msm_cfg(n, folded ? wk.fold_c : 0, folded);
     auto need = [](DevBuf &b, size_t bytes) { if (b.bytes < bytes) b.alloc(bytes); };
     need(wk.digits, (uint64_t)g.W * B * n * 4);
     uint32_t *keys = static_cast<uint32_t *>(wk.digits.p);

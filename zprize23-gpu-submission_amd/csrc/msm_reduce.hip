@@ -17,6 +17,7 @@
 // sum.  One launch per level, one lane per node.
 #include "msm_internal.h"
 #include "ec.cuh"
+#include "field29.cuh"
 
 namespace pnp {
 
@@ -30,6 +31,29 @@ __global__ __launch_bounds__(256) void k_tree_leaf(const uint64_t *bk, uint64_t 
     store_xyzz(o, S);
     store_xyzz(o + 24, add(S, b1));
     store_xyzz(o + 48, dbl(S));
+}
+
+// leaves of height 4 from 16 buckets by running sums (right to left):
+// S = sum B_k, T = sum (k+1) B_k, D = 16 S.  Throughput-friendlier than the
+// pairwise leaf when the window has many buckets (depth 30 additions + 5
+// doublings, 2 additions per bucket).
+__global__ __launch_bounds__(256) void k_tree_leaf16(const uint64_t *bk, uint64_t nout, uint64_t *out) {
+    uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    if (t >= nout) return;
+    const uint64_t *b = bk + 24 * 16 * t;
+    Xyzz S = load_xyzz(b + 24 * 15), T = S;
+#pragma unroll 1
+    for (int k = 14; k >= 0; k--) {
+        S = add(S, load_xyzz(b + 24 * k));
+        T = add(T, S);
+    }
+    uint64_t *o = out + 72 * t;
+    store_xyzz(o, S);
+    store_xyzz(o + 24, T);
+    Xyzz D = S;
+#pragma unroll 1
+    for (int k = 0; k < 4; k++) D = dbl(D);
+    store_xyzz(o + 48, D);
 }
 
 // node t from nodes 2t, 2t+1 of the level below; triples (S, T, D) of 72 u64.
@@ -97,6 +121,75 @@ void msm_merge_pieces(const uint32_t *offs, int nch, uint64_t U, uint32_t S, uin
     PNP_HIP(hipGetLastError());
 }
 
+// Folded layout: the pieces are raw radix-2^29 XYZZ points (56 u32, see
+// msm.hip store29); a bucket inside one lane's segment is bk29[u], else
+// tail29[t0] + head29[t0+1] + ... + head29[t1].  Every piece is converted to
+// R384 here; every non-empty bucket is written to bk, empty ones as infinity.
+__device__ __forceinline__ F29 ld29(const uint32_t *p) {
+    const uint4 *q = reinterpret_cast<const uint4 *>(p);
+    uint4 a = q[0], b = q[1], c = q[2];
+    uint2 d = *reinterpret_cast<const uint2 *>(p + 12);
+    F29 r;
+    r.l[0] = a.x; r.l[1] = a.y; r.l[2] = a.z; r.l[3] = a.w;
+    r.l[4] = b.x; r.l[5] = b.y; r.l[6] = b.z; r.l[7] = b.w;
+    r.l[8] = c.x; r.l[9] = c.y; r.l[10] = c.z; r.l[11] = c.w;
+    r.l[12] = d.x; r.l[13] = d.y;
+    return r;
+}
+__device__ __forceinline__ Xyzz piece29(const uint32_t *p) {
+    Xyzz r;
+    r.x = to_fq32(ld29(p));
+    r.y = to_fq32(ld29(p + 14));
+    r.zz = to_fq32(ld29(p + 28));
+    r.zzz = to_fq32(ld29(p + 42));
+    return r;
+}
+__global__ __launch_bounds__(256) void k_merge_pieces29(const uint32_t *offs, uint64_t U, uint32_t S,
+                                                        int G, const uint32_t *bk29,
+                                                        const uint32_t *head, const uint32_t *tail,
+                                                        uint64_t *bk) {
+    __shared__ uint64_t lds[256 * 24];
+    const uint64_t g = (blockIdx.x * (uint64_t)blockDim.x + threadIdx.x) / G;
+    const int j = threadIdx.x % G;
+    bool live = false;
+    Xyzz acc = Xyzz::inf();
+    if (g < U) {
+        uint32_t s0 = offs[g], e0 = offs[g + 1];
+        if (s0 != e0) {
+            live = true;
+            uint32_t t0 = s0 / S, t1 = (e0 - 1) / S;
+            if (t0 == t1) {
+                if (j == 0) acc = piece29(bk29 + 56 * g);
+            } else {
+#pragma unroll 1
+                for (uint32_t k = j; k <= t1 - t0; k += G)
+                    acc = add(acc, piece29(k == 0 ? tail + 56ULL * t0 : head + 56ULL * (t0 + k)));
+            }
+        } else if (j == 0) {
+            store_xyzz(bk + 24 * g, Xyzz::inf());
+        }
+    }
+    uint64_t *mine = lds + 24 * threadIdx.x;
+    for (int h = G / 2; h >= 1; h /= 2) {
+        store_xyzz(mine, acc);
+        __syncthreads();
+        if (live && j < h) acc = add(acc, load_xyzz(mine + 24 * h));
+        __syncthreads();
+    }
+    if (live && j == 0) store_xyzz(bk + 24 * g, acc);
+}
+
+void msm_merge_pieces29(const uint32_t *offs, uint64_t U, uint32_t S, uint32_t pieces,
+                        const uint32_t *bk29, const uint32_t *head, const uint32_t *tail, uint64_t *bk,
+                        hipStream_t s) {
+    int G = 1;
+    while (G < 8 && (uint32_t)G * 8 <= pieces) G *= 2;
+    const uint64_t blocks = (U * G + 255) / 256;
+    hipLaunchKernelGGL(k_merge_pieces29, dim3((uint32_t)blocks), dim3(256), 0, s, offs, U, S, G, bk29,
+                       head, tail, bk);
+    PNP_HIP(hipGetLastError());
+}
+
 // ---------------------------------------------------------------- tree
 // the roots' T, packed
 __global__ void k_tree_roots(const uint64_t *in, uint64_t n, uint64_t *out) {
@@ -107,10 +200,14 @@ __global__ void k_tree_roots(const uint64_t *in, uint64_t n, uint64_t *out) {
 const uint64_t *msm_reduce(const uint64_t *bk, uint64_t nwin, int NB, uint64_t *scratch,
                            hipStream_t s) {
     if (NB == 1) return bk;
-    // two ping-pong triple arrays: level sizes nwin*NB/2, /4, ...
-    uint64_t m = nwin * (uint64_t)NB / 2;
+    // two ping-pong triple arrays: level sizes nwin*NB/2 (or /16), then halving
+    const bool wide = NB >= (1 << 18);  // many buckets per window: running-sum leaves
+    uint64_t m = nwin * (uint64_t)NB / (wide ? 16 : 2);
     uint64_t *a = scratch, *b = scratch + 72 * m;
-    hipLaunchKernelGGL(k_tree_leaf, dim3((uint32_t)((m + 255) / 256)), dim3(256), 0, s, bk, m, a);
+    if (wide)
+        hipLaunchKernelGGL(k_tree_leaf16, dim3((uint32_t)((m + 255) / 256)), dim3(256), 0, s, bk, m, a);
+    else
+        hipLaunchKernelGGL(k_tree_leaf, dim3((uint32_t)((m + 255) / 256)), dim3(256), 0, s, bk, m, a);
     PNP_HIP(hipGetLastError());
     while (m > nwin) {
         m /= 2;

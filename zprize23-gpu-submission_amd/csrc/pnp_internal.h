@@ -97,6 +97,10 @@ struct KernelTimer {
     // `bytes`: algorithmic bytes credited to this launch
     void end(const char *name, hipStream_t s, hipEvent_t e0, double bytes = 0);
     void collect();  // call after the stream is synchronized
+    // add `units` to a counter read back with pnp_kernel_bytes (no timing)
+    void credit(const char *name, double units) {
+        if (enabled) stats[name].bytes += units;
+    }
 };
 
 // ---- MSM (msm.hip) ----
