@@ -5,7 +5,7 @@
 set -e
 R=$(pwd)
 TAG=${1:-pmc}
-RX='k_accumulate29|k_dif_pass|k_quotient|k_coarse_scatter|k_fine_sort|k_tree_level|k_bitrev_tiles|k_lde_twist|k_t_combine'
+RX='k_accumulate29|k_ntt_pass|k_quotient|k_coarse_scatter|k_fine_sort|k_tree_level|k_t_combine'
 cd /tmp && export TMPDIR=/tmp
 mkdir -p $R/gpurun_out/$TAG
 i=0

@@ -87,14 +87,21 @@ __device__ __forceinline__ Fr coset_pow(const uint64_t *hi, const uint64_t *lo, 
     return load_fr(hi, i >> 12) * load_fr(lo, i & 4095);
 }
 
-// ---------------------------------------------------------------- DIF pass
-// One pass = K DIF levels with half sizes H_lo*2^(K-1) ... H_lo over tiles of
+// ---------------------------------------------------------------- DIF / DIT pass
+// One pass = K levels with half sizes H_lo*2^(K-1) ... H_lo over tiles of
 // TILE elements (G = TILE >> K interleaved sub-transforms per tile).
-template <int K>
-__global__ __launch_bounds__(NTT_THREADS) void k_dif_pass(uint64_t *data, const uint64_t *tw,
-                                                           uint32_t lg_n, uint32_t lg_hlo) {
+// DIF (natural in, bit-reversed out): levels from the largest half size down,
+// butterfly (a + b, (a - b) w).  DIT (bit-reversed in, natural out): levels
+// from the smallest half size up, butterfly (a + b w, a - b w), same twiddles.
+// Optional fusions: `src` + `pre` (load src[idx & src_mask] * pre[idx] instead
+// of data[idx]: the coset twist of an LDE in its first pass) and `post` (store
+// x * post[idx]: the block twist after the last inverse pass).
+template <int K, bool DIT>
+__global__ __launch_bounds__(NTT_THREADS) void k_ntt_pass(uint64_t *data, const uint64_t *tw,
+                                                           uint32_t lg_n, uint32_t lg_hlo,
+                                                           const uint64_t *src, const uint64_t *pre,
+                                                           uint64_t src_mask, const uint64_t *post) {
     constexpr int G = TILE >> K;
-    constexpr int ROWS = 1 << K;
     __shared__ uint4 lds_lo[TILE];
     __shared__ uint4 lds_hi[TILE];
     const uint64_t hlo = 1ULL << lg_hlo;
@@ -105,12 +112,19 @@ __global__ __launch_bounds__(NTT_THREADS) void k_dif_pass(uint64_t *data, const 
         uint64_t gid = gid0 + g;
         uint64_t j = gid & (hlo - 1), b = gid >> lg_hlo;
         uint64_t idx = (b << (lg_hlo + K)) + j + ((uint64_t)m << lg_hlo);
-        const uint4 *src = reinterpret_cast<const uint4 *>(data + 4 * idx);
-        lds_lo[e] = src[0];
-        lds_hi[e] = src[1];
+        if (src) {
+            Fr x = load_fr(src, idx & src_mask) * load_fr(pre, idx);
+            lds_lo[e] = make_uint4(x.v[0], x.v[1], x.v[2], x.v[3]);
+            lds_hi[e] = make_uint4(x.v[4], x.v[5], x.v[6], x.v[7]);
+        } else {
+            const uint4 *p = reinterpret_cast<const uint4 *>(data + 4 * idx);
+            lds_lo[e] = p[0];
+            lds_hi[e] = p[1];
+        }
     }
     __syncthreads();
-    for (int l = K - 1; l >= 0; l--) {
+    for (int step = 0; step < K; step++) {
+        const int l = DIT ? step : K - 1 - step;
         const uint32_t sh = lg_n - 1 - lg_hlo - l;
         for (int bf = threadIdx.x; bf < TILE / 2; bf += NTT_THREADS) {
             int g = bf % G, q = bf / G;
@@ -127,8 +141,15 @@ __global__ __launch_bounds__(NTT_THREADS) void k_dif_pass(uint64_t *data, const 
             a.v[4] = a1.x; a.v[5] = a1.y; a.v[6] = a1.z; a.v[7] = a1.w;
             b.v[0] = b0.x; b.v[1] = b0.y; b.v[2] = b0.z; b.v[3] = b0.w;
             b.v[4] = b1.x; b.v[5] = b1.y; b.v[6] = b1.z; b.v[7] = b1.w;
-            Fr s = a + b;
-            Fr d = (a - b) * w;
+            Fr s, d;
+            if (DIT) {
+                Fr t = b * w;
+                s = a + t;
+                d = a - t;
+            } else {
+                s = a + b;
+                d = (a - b) * w;
+            }
             lds_lo[e0] = make_uint4(s.v[0], s.v[1], s.v[2], s.v[3]);
             lds_hi[e0] = make_uint4(s.v[4], s.v[5], s.v[6], s.v[7]);
             lds_lo[e1] = make_uint4(d.v[0], d.v[1], d.v[2], d.v[3]);
@@ -141,14 +162,23 @@ __global__ __launch_bounds__(NTT_THREADS) void k_dif_pass(uint64_t *data, const 
         uint64_t gid = gid0 + g;
         uint64_t j = gid & (hlo - 1), b = gid >> lg_hlo;
         uint64_t idx = (b << (lg_hlo + K)) + j + ((uint64_t)m << lg_hlo);
-        uint4 *dst = reinterpret_cast<uint4 *>(data + 4 * idx);
-        dst[0] = lds_lo[e];
-        dst[1] = lds_hi[e];
+        if (post) {
+            uint4 lo = lds_lo[e], hi = lds_hi[e];
+            Fr x;
+            x.v[0] = lo.x; x.v[1] = lo.y; x.v[2] = lo.z; x.v[3] = lo.w;
+            x.v[4] = hi.x; x.v[5] = hi.y; x.v[6] = hi.z; x.v[7] = hi.w;
+            store_fr(data, idx, x * load_fr(post, idx));
+        } else {
+            uint4 *dst = reinterpret_cast<uint4 *>(data + 4 * idx);
+            dst[0] = lds_lo[e];
+            dst[1] = lds_hi[e];
+        }
     }
 }
 
 // small transforms (N < TILE): one workgroup does everything in LDS
-__global__ __launch_bounds__(NTT_THREADS) void k_dif_small(uint64_t *data, const uint64_t *tw,
+template <bool DIT>
+__global__ __launch_bounds__(NTT_THREADS) void k_ntt_small(uint64_t *data, const uint64_t *tw,
                                                             uint32_t lg_n) {
     __shared__ uint4 lds_lo[TILE];
     __shared__ uint4 lds_hi[TILE];
@@ -159,7 +189,8 @@ __global__ __launch_bounds__(NTT_THREADS) void k_dif_small(uint64_t *data, const
         lds_hi[e] = src[1];
     }
     __syncthreads();
-    for (int l = (int)lg_n - 1; l >= 0; l--) {
+    for (int step = 0; step < (int)lg_n; step++) {
+        const int l = DIT ? step : (int)lg_n - 1 - step;
         for (int bf = threadIdx.x; bf < n / 2; bf += NTT_THREADS) {
             int mlow = bf & ((1 << l) - 1);
             int m = ((bf >> l) << (l + 1)) | mlow;
@@ -171,8 +202,15 @@ __global__ __launch_bounds__(NTT_THREADS) void k_dif_small(uint64_t *data, const
             a.v[4] = a1.x; a.v[5] = a1.y; a.v[6] = a1.z; a.v[7] = a1.w;
             b.v[0] = b0.x; b.v[1] = b0.y; b.v[2] = b0.z; b.v[3] = b0.w;
             b.v[4] = b1.x; b.v[5] = b1.y; b.v[6] = b1.z; b.v[7] = b1.w;
-            Fr s = a + b;
-            Fr d = (a - b) * w;
+            Fr s, d;
+            if (DIT) {
+                Fr t = b * w;
+                s = a + t;
+                d = a - t;
+            } else {
+                s = a + b;
+                d = (a - b) * w;
+            }
             lds_lo[e0] = make_uint4(s.v[0], s.v[1], s.v[2], s.v[3]);
             lds_hi[e0] = make_uint4(s.v[4], s.v[5], s.v[6], s.v[7]);
             lds_lo[e1] = make_uint4(d.v[0], d.v[1], d.v[2], d.v[3]);
@@ -289,33 +327,64 @@ __global__ void k_pad_coset(const uint64_t *in, uint64_t *out, uint64_t n, uint6
     store_fr(out, i, x);
 }
 
-// DIF of size 2^lg on each of the 2^(lg_total - lg) consecutive blocks of d
-static void dif(NttTables &t, uint64_t *d, uint32_t lg, bool inverse, hipStream_t s,
-                uint32_t lg_total = 0) {
+// Fused extras of the first (src, pre) and last (post) pass, see k_ntt_pass
+struct PassFuse {
+    const uint64_t *src = nullptr, *pre = nullptr, *post = nullptr;
+    uint64_t src_mask = 0;
+};
+__global__ void k_mul_table(uint64_t *d, const uint64_t *T, uint64_t N);
+__global__ void k_lde_twist(const uint64_t *in, const uint64_t *T, uint64_t *out, uint64_t n, uint64_t N);
+
+// DIF (natural -> bit-reversed) or DIT (bit-reversed -> natural) of size 2^lg
+// on each of the 2^(lg_total - lg) consecutive blocks of d
+static void ntt_core(NttTables &t, uint64_t *d, uint32_t lg, bool inverse, bool dit, hipStream_t s,
+                     uint32_t lg_total = 0, const PassFuse &fz = PassFuse()) {
     if (lg_total < lg) lg_total = lg;
+    const uint64_t N = 1ULL << lg_total;
     const uint64_t *tw = ntt_twiddles(t, lg, inverse, s);
     if (lg_total < 10 || (lg <= 10 && lg_total == lg)) {
+        if (fz.src) {
+            hipLaunchKernelGGL(k_lde_twist, dim3((uint32_t)((N + 255) / 256)), dim3(256), 0, s, fz.src,
+                               fz.pre, d, fz.src_mask + 1, N);
+            PNP_HIP(hipGetLastError());
+        }
         for (uint64_t b = 0; b < (1ULL << (lg_total - lg)); b++) {
-            hipLaunchKernelGGL(k_dif_small, dim3(1), dim3(NTT_THREADS), 0, s, d + 4 * (b << lg), tw, lg);
+            if (dit)
+                hipLaunchKernelGGL(k_ntt_small<true>, dim3(1), dim3(NTT_THREADS), 0, s, d + 4 * (b << lg), tw, lg);
+            else
+                hipLaunchKernelGGL(k_ntt_small<false>, dim3(1), dim3(NTT_THREADS), 0, s, d + 4 * (b << lg), tw, lg);
+            PNP_HIP(hipGetLastError());
+        }
+        if (fz.post) {
+            hipLaunchKernelGGL(k_mul_table, dim3((uint32_t)((N + 255) / 256)), dim3(256), 0, s, d, fz.post, N);
             PNP_HIP(hipGetLastError());
         }
         return;
     }
-    // split lg into passes of at most 10 levels (balanced), top levels first
-    int npass = (lg + 9) / 10;
-    int rem = lg;
-    uint32_t top = lg;  // current largest half-size exponent + 1
+    // split lg into passes of at most 10 levels (balanced); DIF runs them from
+    // the largest half size down, DIT from the smallest up
+    const int npass = (lg + 9) / 10;
+    int ks[4], rem = lg;
     for (int p = 0; p < npass; p++) {
-        int k = (rem + (npass - p) - 1) / (npass - p);
-        rem -= k;
-        uint32_t lg_hlo = top - k;  // smallest half size of this pass = 2^(top-k)
-        uint64_t groups = (1ULL << lg_total) >> k;
-        uint32_t blocks = (uint32_t)(groups / (TILE >> k));
+        ks[p] = (rem + (npass - p) - 1) / (npass - p);
+        rem -= ks[p];
+    }
+    uint32_t lo = dit ? 0 : lg;  // DIF: current top exponent; DIT: current bottom
+    for (int p = 0; p < npass; p++) {
+        const int k = ks[p];
+        const uint32_t lg_hlo = dit ? lo : lo - k;
+        const uint32_t blocks = (uint32_t)((N >> k) / (TILE >> k));
+        const uint64_t *src = p == 0 ? fz.src : nullptr, *pre = p == 0 ? fz.pre : nullptr;
+        const uint64_t *post = p == npass - 1 ? fz.post : nullptr;
         switch (k) {
-#define PNP_CASE(KK)                                                                          \
-    case KK:                                                                                  \
-        hipLaunchKernelGGL(k_dif_pass<KK>, dim3(blocks), dim3(NTT_THREADS), 0, s, d, tw, lg, \
-                           lg_hlo);                                                           \
+#define PNP_CASE(KK)                                                                               \
+    case KK:                                                                                       \
+        if (dit)                                                                                   \
+            hipLaunchKernelGGL((k_ntt_pass<KK, true>), dim3(blocks), dim3(NTT_THREADS), 0, s, d, tw, \
+                               lg, lg_hlo, src, pre, fz.src_mask, post);                          \
+        else                                                                                       \
+            hipLaunchKernelGGL((k_ntt_pass<KK, false>), dim3(blocks), dim3(NTT_THREADS), 0, s, d, tw, \
+                               lg, lg_hlo, src, pre, fz.src_mask, post);                          \
         break;
             PNP_CASE(1) PNP_CASE(2) PNP_CASE(3) PNP_CASE(4) PNP_CASE(5)
             PNP_CASE(6) PNP_CASE(7) PNP_CASE(8) PNP_CASE(9) PNP_CASE(10)
@@ -325,8 +394,13 @@ static void dif(NttTables &t, uint64_t *d, uint32_t lg, bool inverse, hipStream_
                 throw Error(PNP_E_ARG);
         }
         PNP_HIP(hipGetLastError());
-        top -= k;
+        lo = dit ? lo + k : lo - k;
     }
+}
+
+static void dif(NttTables &t, uint64_t *d, uint32_t lg, bool inverse, hipStream_t s,
+                uint32_t lg_total = 0) {
+    ntt_core(t, d, lg, inverse, false, s, lg_total);
 }
 
 static void bitrev(uint64_t *d, uint32_t lg, const Scale &sc, hipStream_t s, uint32_t nblocks = 1) {
@@ -443,16 +517,18 @@ static uint32_t lg_blocks(int nb) {
     return l;
 }
 
-// out[b n + j] = f(g w_8n^(8 j + m0 + b)), b < nb, for the n coefficients `in`
+// out[b n + brev(j)] = f(g w_8n^(8 j + m0 + b)), b < nb, for the n
+// coefficients `in`: the twist is fused into the first DIF pass and the DIF's
+// bit-reversed output is kept ("block-bitrev layout", no reversal pass); the
+// quotient's arrays share the layout and intt_blocks undoes it with a DIT.
 void lde_blocks(NttTables &t, const uint64_t *in, uint64_t *out, uint32_t lg_n, int m0, int nb,
                 hipStream_t s) {
-    const uint64_t n = 1ULL << lg_n, N = n * nb;
-    const uint64_t *T = block_twist_table(t, lg_n, false, s) + 4 * (uint64_t)m0 * n;
-    hipLaunchKernelGGL(k_lde_twist, dim3((uint32_t)((N + 255) / 256)), dim3(256), 0, s, in, T, out, n, N);
-    PNP_HIP(hipGetLastError());
-    if (lg_n > 0) dif(t, out, lg_n, false, s, lg_n + lg_blocks(nb));
-    Scale sc{0, Fr::one(), nullptr, nullptr};
-    bitrev(out, lg_n, sc, s, nb);
+    const uint64_t n = 1ULL << lg_n;
+    PassFuse fz;
+    fz.src = in;
+    fz.pre = block_twist_table(t, lg_n, false, s) + 4 * (uint64_t)m0 * n;
+    fz.src_mask = n - 1;
+    ntt_core(t, out, lg_n, false, false, s, lg_n + lg_blocks(nb), fz);
 }
 
 __global__ void k_mul_table(uint64_t *d, const uint64_t *T, uint64_t N) {
@@ -460,16 +536,14 @@ __global__ void k_mul_table(uint64_t *d, const uint64_t *T, uint64_t N) {
     if (i < N) store_fr(d, i, load_fr(d, i) * load_fr(T, i));
 }
 
-// in place, block b < nb holding residue m = m0 + b:
-//   Y_m[u] = w_8n^(-m u) sum_j d[b n + j] w_n^(-j u)      (no 1/n scaling)
+// in place, block b < nb holding residue m = m0 + b in block-bitrev layout:
+//   Y_m[u] = w_8n^(-m u) sum_j d[b n + brev(j)] w_n^(-j u)      (no 1/n scaling)
+// as a DIT (bit-reversed in, natural out) with the twist fused into its last pass
 void intt_blocks(NttTables &t, uint64_t *d, uint32_t lg_n, int m0, int nb, hipStream_t s) {
-    const uint64_t n = 1ULL << lg_n, N = n * nb;
-    if (lg_n > 0) dif(t, d, lg_n, true, s, lg_n + lg_blocks(nb));
-    Scale sc{0, Fr::one(), nullptr, nullptr};
-    bitrev(d, lg_n, sc, s, nb);
-    const uint64_t *T = block_twist_table(t, lg_n, true, s) + 4 * (uint64_t)m0 * n;
-    hipLaunchKernelGGL(k_mul_table, dim3((uint32_t)((N + 255) / 256)), dim3(256), 0, s, d, T, N);
-    PNP_HIP(hipGetLastError());
+    const uint64_t n = 1ULL << lg_n;
+    PassFuse fz;
+    fz.post = block_twist_table(t, lg_n, true, s) + 4 * (uint64_t)m0 * n;
+    ntt_core(t, d, lg_n, true, true, s, lg_n + lg_blocks(nb), fz);
 }
 
 // Coefficients of the 8n-point coset interpolant from the 8 twisted block
@@ -538,15 +612,18 @@ void t_combine(NttTables &t, const uint64_t *Y, uint64_t len, uint64_t q0, uint6
     PNP_HIP(hipGetLastError());
 }
 
-// out[b n + j] = in[8 j + m0 + b], b < nb   (natural 8n order -> block layout)
-__global__ void k_to_blocks(const uint64_t *in, uint64_t *out, uint64_t n, int m0, int nb) {
+// out[b n + brev(j)] = in[8 j + m0 + b], b < nb
+// (natural 8n order -> block-bitrev layout, see lde_blocks)
+__global__ void k_to_blocks(const uint64_t *in, uint64_t *out, uint64_t n, uint32_t lg_n, int m0, int nb) {
     uint64_t j = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
     if (j >= n) return;
-    for (int b = 0; b < nb; b++) store_fr(out, (uint64_t)b * n + j, load_fr(in, 8 * j + m0 + b));
+    const uint64_t p = lg_n ? brev((uint32_t)j, lg_n) : 0;
+    for (int b = 0; b < nb; b++) store_fr(out, (uint64_t)b * n + p, load_fr(in, 8 * j + m0 + b));
 }
 void to_blocks(const uint64_t *in, uint64_t *out, uint32_t lg_n, int m0, int nb, hipStream_t s) {
     const uint64_t n = 1ULL << lg_n;
-    hipLaunchKernelGGL(k_to_blocks, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, s, in, out, n, m0, nb);
+    hipLaunchKernelGGL(k_to_blocks, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, s, in, out, n, lg_n,
+                       m0, nb);
     PNP_HIP(hipGetLastError());
 }
 

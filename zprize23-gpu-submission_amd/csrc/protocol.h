@@ -34,7 +34,8 @@ struct QuotArgs {
     // PI / Z_H = c_pi * pinv with c_pi = pi * w^pos / n
     const uint64_t *l1v, *pinv;
     Fr c_pi;
-    uint64_t n;  // block length: arrays are in block layout (point 8j + m -> m n + j)
+    uint64_t n;     // block length: arrays are in block-bitrev layout
+    uint32_t lg_n;  // (point 8j + m -> m n + brev(j), ntt.hip lde_blocks)
     Fr alpha, alpha2, beta, gamma, delta, eps, zeta, lsep;
     Fr bk[4], opd, eopd, sep2, sep3;
 };

@@ -197,9 +197,14 @@ __device__ __forceinline__ Fr pow5(const Fr &a) {
 __global__ __launch_bounds__(256) void k_quotient_(QuotArgs q, uint64_t N8, uint64_t *out) {
     uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
     if (i >= N8) return;
-    // the coset point w_8n^8 further: index j + 1 of the same block
-    const uint64_t jb = i & (q.n - 1);
-    const uint64_t nx = i - jb + ((jb + 1) & (q.n - 1));
+    // the coset point w_8n^8 further: index j + 1 of the same block, at its
+    // bit-reversed position (block-bitrev layout, ntt.hip lde_blocks)
+    const uint64_t jp = i & (q.n - 1);
+    uint64_t nx = i;
+    if (q.lg_n) {
+        const uint32_t j = __brev((uint32_t)jp) >> (32 - q.lg_n);
+        nx = i - jp + (__brev((j + 1) & (uint32_t)(q.n - 1)) >> (32 - q.lg_n));
+    }
     Fr a = load_fr(q.w8[0], i), b = load_fr(q.w8[1], i), c = load_fr(q.w8[2], i), d = load_fr(q.w8[3], i);
     // compute_quotient_i (widget/arithmetic.cu:7-45) + pi
     Fr acc = a * load_fr(q.q_l, i);

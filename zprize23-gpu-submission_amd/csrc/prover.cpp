@@ -380,6 +380,7 @@ int prove_impl(pnp_ctx *ctx, const CircuitC *cs, int device_ptrs, ProofC *out) {
     q.lin = ctx->blk("lin");
     q.vh_inv = ctx->blk("vh_inv");  // v_h^-1, computed at key load
     q.n = n;
+    q.lg_n = lg;
     q.alpha = alpha;
     q.beta = beta;
     q.gamma = gamma;
