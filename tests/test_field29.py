@@ -85,6 +85,29 @@ def sqr29(a):
     return r
 
 
+def mul2_29(a, b, c, d):
+    """mul2_29 of field29.cuh: a b + c d, one reduction."""
+    assert all(x < 2**29 for x in a + b + c + d)
+    q = C["F29_Q"]
+    m, r, acc = [0] * 14, [0] * 14, 0
+    for k in range(27):
+        for i in range(max(0, k - 13), min(k, 13) + 1):
+            acc += a[i] * b[k - i] + c[i] * d[k - i]
+        for i in range(max(0, k - 13), min(k, 14)):
+            acc += m[i] * q[k - i]
+        if k < 14:
+            m[k] = ((acc & 0xFFFFFFFF) * QINV) & M29
+            acc += m[k] * q[0]
+            assert acc & M29 == 0
+        else:
+            r[k - 14] = acc & M29
+        assert acc < 2**64
+        acc >>= 29
+    r[13] = acc
+    assert acc < 2**29
+    return r
+
+
 def sub29(a, b, K):
     r, c = [0] * 14, 0
     for i in range(13):
@@ -127,8 +150,13 @@ def test_mul_exact_and_bounded():
         assert val(r) < 2**382
         s = sqr29(limbs(a))
         assert val(s) == val(mul29(limbs(a), limbs(a)))
+        c, d = rnd.randrange(2**391), rnd.randrange(2**391)
+        t = mul2_29(limbs(a), limbs(b), limbs(c), limbs(d))
+        assert val(t) % Q == (a * b + c * d) * pow(R406, -1, Q) % Q
+        assert val(t) < 2**382
     top = limbs(2**391 - 1)  # every limb at its maximum: worst column sums
     assert val(sqr29(top)) == val(mul29(top, top))
+    mul2_29(top, top, top, top)
 
 
 # ---- G1 (y^2 = x^3 + 4) affine reference
@@ -159,7 +187,8 @@ def madd29(p, x2, y2):
     assert val(x3) < 2**389
     t = sub29(q, x3, KB)
     assert val(t) < 2**391
-    y3 = sub29(mul29(R, t), mul29(Y, ppp), KA)
+    y3 = mul2_29(R, t, Y, sub29([0] * 14, ppp, KA))
+    assert val(y3) < 2**382
     return x3, y3, mul29(ZZ, pp), mul29(ZZZ, ppp)
 
 

@@ -444,7 +444,8 @@ struct Xyzz29 {
     F29 x, y, zz, zzz;
 };
 // P += (x2, y2), madd-2008-s.  Bounds (see field29.cuh): products < 2^382,
-// stored coordinates < 2^389, every product input < 2^391.  No equal /
+// stored coordinates < 2^389, every product input < 2^391 (Y3 < 2^382 comes
+// from mul2_29).  No equal /
 // opposite / infinity cases: those make ZZ = 0 mod q, detected per piece.
 __device__ __forceinline__ void madd29(Xyzz29 &p, const F29 &x2, const F29 &y2) {
     F29 u2 = mul29(x2, p.zz);
@@ -455,7 +456,8 @@ __device__ __forceinline__ void madd29(Xyzz29 &p, const F29 &x2, const F29 &y2) 
     F29 ppp = mul29(P, pp);
     F29 q = mul29(p.x, pp);
     F29 x3 = sub29(sub29(sub29(sqr29(R), ppp, F29_KA), q, F29_KA), q, F29_KA);
-    F29 y3 = sub29(mul29(R, sub29(q, x3, F29_KB)), mul29(p.y, ppp), F29_KA);
+    // Y3 = R (Q - X3) - Y PPP as R (Q - X3) + Y (KA - PPP), one reduction
+    F29 y3 = mul2_29(R, sub29(q, x3, F29_KB), p.y, neg29(ppp, F29_KA));
     p.zz = mul29(p.zz, pp);
     p.zzz = mul29(p.zzz, ppp);
     p.x = x3;
@@ -495,6 +497,9 @@ __device__ __forceinline__ bool store29(uint32_t *dst, const Xyzz29 &p) {
 #ifndef PNP_ACC_WAVES
 #define PNP_ACC_WAVES 3
 #endif
+#ifndef PNP_ACC_PREFETCH
+#define PNP_ACC_PREFETCH 0
+#endif
 __global__ __launch_bounds__(256, PNP_ACC_WAVES) void k_accumulate29(const uint32_t *pts29, const uint32_t *sorted,
                                                       const uint32_t *offs, uint64_t U, uint32_t S,
                                                       uint32_t *buckets, uint32_t *head,
@@ -516,7 +521,20 @@ __global__ __launch_bounds__(256, PNP_ACC_WAVES) void k_accumulate29(const uint3
     uint32_t next = offs[cur + 1];
     bool ok = true, fresh = true;
     Xyzz29 acc;
+#if PNP_ACC_PREFETCH == 2
+    uint32_t ei = sorted[lo];  // next entry's index, one iteration ahead
+#elif PNP_ACC_PREFETCH
+    // software pipeline: entry k+2's index and entry k+1's point are loaded
+    // while entry k is added (the gathers otherwise stall every iteration)
+    uint32_t e = sorted[lo], en = lo + 1 < hi ? sorted[lo + 1] : e;
+    F29 x = load29(pts29 + 28ULL * (e & 0x7FFFFFFFu)), y = load29(pts29 + 28ULL * (e & 0x7FFFFFFFu) + 14);
+#endif
     for (uint32_t k = lo; k < hi; k++) {
+#if PNP_ACC_PREFETCH == 1
+        const uint32_t *pn = pts29 + 28ULL * (en & 0x7FFFFFFFu);
+        const F29 xn = load29(pn), yn = load29(pn + 14);
+        const uint32_t enn = k + 2 < hi ? sorted[k + 2] : en;
+#endif
         if (k == next) {
             ok &= store29(first ? head + 56 * t : buckets + 56 * cur, acc);
             first = false;
@@ -526,9 +544,16 @@ __global__ __launch_bounds__(256, PNP_ACC_WAVES) void k_accumulate29(const uint3
                 next = offs[cur + 1];
             } while (next == k);
         }
+#if PNP_ACC_PREFETCH == 0
         uint32_t e = sorted[k];
         const uint32_t *p = pts29 + 28ULL * (e & 0x7FFFFFFFu);
         F29 x = load29(p), y = load29(p + 14);
+#elif PNP_ACC_PREFETCH == 2
+        const uint32_t e = ei;
+        ei = k + 1 < hi ? sorted[k + 1] : ei;
+        const uint32_t *p = pts29 + 28ULL * (e & 0x7FFFFFFFu);
+        F29 x = load29(p), y = load29(p + 14);
+#endif
         if (e >> 31) y = neg29(y, F29_KA);
         if (fresh) {
             acc.x = x;
@@ -538,6 +563,12 @@ __global__ __launch_bounds__(256, PNP_ACC_WAVES) void k_accumulate29(const uint3
         } else {
             madd29(acc, x, y);
         }
+#if PNP_ACC_PREFETCH == 1
+        x = xn;
+        y = yn;
+        e = en;
+        en = enn;
+#endif
     }
     ok &= store29(first ? head + 56 * t : (next > hi ? tail + 56 * t : buckets + 56 * cur), acc);
     if (!ok) redo[atomicAdd(nredo, 1u)] = (uint32_t)t;

@@ -22,7 +22,10 @@
 namespace pnp {
 
 static constexpr int TILE = 1024;
-static constexpr int NTT_THREADS = 256;
+#ifndef PNP_NTT_THREADS
+#define PNP_NTT_THREADS 512
+#endif
+static constexpr int NTT_THREADS = PNP_NTT_THREADS;
 
 // ---------------------------------------------------------------- tables
 __global__ void k_powers_table(uint64_t *out, uint64_t count, Fr base, uint32_t chunk) {
