@@ -96,8 +96,18 @@ using Fr = Fp<FrP>;
 using Fq = Fp<FqP>;
 
 // ---- raw multi-limb helpers ----
+// On the device the carry chains use clang's add/sub-with-carry builtins,
+// which lower to one v_add_co_u32 / v_addc_co_u32 (v_sub_co / v_subb_co) per
+// limb.  The 64-bit formulation below compiled to two v_lshl_add_u64 and
+// three v_mov per limb (measured: a fifth of an NTT butterfly's VALU issue).
 template <int N>
 PNP_HD uint32_t add_n(uint32_t *r, const uint32_t *a, const uint32_t *b) {
+#ifdef __HIP_DEVICE_COMPILE__
+    uint32_t c = 0;
+#pragma unroll
+    for (int i = 0; i < N; i++) r[i] = __builtin_addc(a[i], b[i], c, &c);
+    return c;
+#else
     uint64_t c = 0;
 #pragma unroll
     for (int i = 0; i < N; i++) {
@@ -105,9 +115,16 @@ PNP_HD uint32_t add_n(uint32_t *r, const uint32_t *a, const uint32_t *b) {
         r[i] = (uint32_t)c;
     }
     return (uint32_t)(c >> 32);
+#endif
 }
 template <int N>
 PNP_HD uint32_t sub_n(uint32_t *r, const uint32_t *a, const uint32_t *b) {
+#ifdef __HIP_DEVICE_COMPILE__
+    uint32_t br = 0;
+#pragma unroll
+    for (int i = 0; i < N; i++) r[i] = __builtin_subc(a[i], b[i], br, &br);
+    return br;
+#else
     uint32_t br = 0;
 #pragma unroll
     for (int i = 0; i < N; i++) {
@@ -116,6 +133,7 @@ PNP_HD uint32_t sub_n(uint32_t *r, const uint32_t *a, const uint32_t *b) {
         br = (uint32_t)(d >> 32) & 1u;
     }
     return br;
+#endif
 }
 
 // r = a - P if a >= P else a   (a < 2P)
