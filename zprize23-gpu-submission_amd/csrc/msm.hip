@@ -759,7 +759,22 @@ static void accumulate_group(MsmWork &wk, MsmGroup &gb, const GroupPlan &gp, con
     if (wk.timer) wk.timer->begin("msm_accumulate", s, ev0);
     // balanced accumulate: S entries per thread, S >= 64 or ~2^20 lanes (every
     // bucket piece beyond the first costs an addition in msm_merge_pieces)
-    const uint32_t S = (uint32_t)std::max<uint64_t>(64, (nent >> 20) & ~7ULL);
+    uint32_t S = (uint32_t)std::max<uint64_t>(64, (nent >> 20) & ~7ULL);
+    if (table) {
+        // whole rounds of resident waves: the lane count a multiple of the
+        // chip's wave slots (CUs x 4 SIMDs x PNP_ACC_WAVES x 64 lanes), so the
+        // last round does not run a fraction of the chip
+        static uint64_t slots = 0;
+        if (!slots) {
+            int dev = 0, cus = 0;
+            PNP_HIP(hipGetDevice(&dev));
+            PNP_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+            slots = (uint64_t)cus * 4 * PNP_ACC_WAVES * 64;
+        }
+        const uint64_t per = (nent + slots - 1) / slots;  // entries per lane in one round
+        const uint64_t rounds = std::max<uint64_t>(1, per / S);
+        S = (uint32_t)((per + rounds - 1) / rounds);
+    }
     const uint64_t nthr = (nent + S - 1) / S;
     if (table) {
         // raw radix-2^29 pieces: buckets inside one segment, then heads, tails

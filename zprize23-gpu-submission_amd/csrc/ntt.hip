@@ -129,6 +129,8 @@ __global__ __launch_bounds__(NTT_THREADS) void k_ntt_pass(uint64_t *data, const 
     for (int step = 0; step < K; step++) {
         const int l = DIT ? step : K - 1 - step;
         const uint32_t sh = lg_n - 1 - lg_hlo - l;
+        // half size 1: every twiddle is w^0 = 1 (uniform branch, no product)
+        const bool unit = lg_hlo == 0 && l == 0;
         for (int bf = threadIdx.x; bf < TILE / 2; bf += NTT_THREADS) {
             int g = bf % G, q = bf / G;
             int mlow = q & ((1 << l) - 1);
@@ -137,7 +139,6 @@ __global__ __launch_bounds__(NTT_THREADS) void k_ntt_pass(uint64_t *data, const 
             uint64_t gid = gid0 + g;
             uint64_t j = gid & (hlo - 1);
             uint64_t r = j + ((uint64_t)mlow << lg_hlo);
-            Fr w = load_fr(tw, r << sh);
             uint4 a0 = lds_lo[e0], a1 = lds_hi[e0], b0 = lds_lo[e1], b1 = lds_hi[e1];
             Fr a, b;
             a.v[0] = a0.x; a.v[1] = a0.y; a.v[2] = a0.z; a.v[3] = a0.w;
@@ -145,13 +146,16 @@ __global__ __launch_bounds__(NTT_THREADS) void k_ntt_pass(uint64_t *data, const 
             b.v[0] = b0.x; b.v[1] = b0.y; b.v[2] = b0.z; b.v[3] = b0.w;
             b.v[4] = b1.x; b.v[5] = b1.y; b.v[6] = b1.z; b.v[7] = b1.w;
             Fr s, d;
-            if (DIT) {
-                Fr t = b * w;
+            if (unit) {
+                s = a + b;
+                d = a - b;
+            } else if (DIT) {
+                Fr t = b * load_fr(tw, r << sh);
                 s = a + t;
                 d = a - t;
             } else {
                 s = a + b;
-                d = (a - b) * w;
+                d = (a - b) * load_fr(tw, r << sh);
             }
             lds_lo[e0] = make_uint4(s.v[0], s.v[1], s.v[2], s.v[3]);
             lds_hi[e0] = make_uint4(s.v[4], s.v[5], s.v[6], s.v[7]);
