@@ -33,17 +33,21 @@ __global__ __launch_bounds__(256) void k_tree_leaf(const uint64_t *bk, uint64_t 
     store_xyzz(o + 48, dbl(S));
 }
 
-// leaves of height 4 from 16 buckets by running sums (right to left):
-// S = sum B_k, T = sum (k+1) B_k, D = 16 S.  Throughput-friendlier than the
-// pairwise leaf when the window has many buckets (depth 30 additions + 5
-// doublings, 2 additions per bucket).
-__global__ __launch_bounds__(256) void k_tree_leaf16(const uint64_t *bk, uint64_t nout, uint64_t *out) {
+// leaves of height log2(LW) from LW buckets by running sums (right to left):
+// S = sum B_k, T = sum (k+1) B_k, D = LW S.  Throughput-friendlier than the
+// pairwise leaf when the window has many buckets (2 additions per bucket,
+// depth ~LW additions + log2(LW) doublings).
+#ifndef PNP_LEAF_W
+#define PNP_LEAF_W 8
+#endif
+template <int LW>
+__global__ __launch_bounds__(256) void k_tree_leafw(const uint64_t *bk, uint64_t nout, uint64_t *out) {
     uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
     if (t >= nout) return;
-    const uint64_t *b = bk + 24 * 16 * t;
-    Xyzz S = load_xyzz(b + 24 * 15), T = S;
+    const uint64_t *b = bk + 24 * LW * t;
+    Xyzz S = load_xyzz(b + 24 * (LW - 1)), T = S;
 #pragma unroll 1
-    for (int k = 14; k >= 0; k--) {
+    for (int k = LW - 2; k >= 0; k--) {
         S = add(S, load_xyzz(b + 24 * k));
         T = add(T, S);
     }
@@ -52,17 +56,18 @@ __global__ __launch_bounds__(256) void k_tree_leaf16(const uint64_t *bk, uint64_
     store_xyzz(o + 24, T);
     Xyzz D = S;
 #pragma unroll 1
-    for (int k = 0; k < 4; k++) D = dbl(D);
+    for (int k = 1; k < LW; k *= 2) D = dbl(D);
     store_xyzz(o + 48, D);
 }
 
 // node t from nodes 2t, 2t+1 of the level below; triples (S, T, D) of 72 u64.
-// Three lanes per node (one per component), each at most two operations deep.
+// Three lanes per node, one per component (blockIdx.y, so every wave runs one
+// path: divergent components would serialise 1 + 2 + 2 operations), each at
+// most two operations deep.
 __global__ __launch_bounds__(256) void k_tree_level(const uint64_t *in, uint64_t nout, uint64_t *out) {
-    uint64_t q = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
-    if (q >= 3 * nout) return;
-    const uint64_t t = q / 3;
-    const int c = (int)(q - 3 * t);
+    const uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    if (t >= nout) return;
+    const int c = (int)blockIdx.y;
     const uint64_t *L = in + 144 * t, *R = L + 72;
     Xyzz r;
     if (c == 0) {
@@ -202,16 +207,16 @@ const uint64_t *msm_reduce(const uint64_t *bk, uint64_t nwin, int NB, uint64_t *
     if (NB == 1) return bk;
     // two ping-pong triple arrays: level sizes nwin*NB/2 (or /16), then halving
     const bool wide = NB >= (1 << 18);  // many buckets per window: running-sum leaves
-    uint64_t m = nwin * (uint64_t)NB / (wide ? 16 : 2);
+    uint64_t m = nwin * (uint64_t)NB / (wide ? PNP_LEAF_W : 2);
     uint64_t *a = scratch, *b = scratch + 72 * m;
     if (wide)
-        hipLaunchKernelGGL(k_tree_leaf16, dim3((uint32_t)((m + 255) / 256)), dim3(256), 0, s, bk, m, a);
+        hipLaunchKernelGGL(k_tree_leafw<PNP_LEAF_W>, dim3((uint32_t)((m + 255) / 256)), dim3(256), 0, s, bk, m, a);
     else
         hipLaunchKernelGGL(k_tree_leaf, dim3((uint32_t)((m + 255) / 256)), dim3(256), 0, s, bk, m, a);
     PNP_HIP(hipGetLastError());
     while (m > nwin) {
         m /= 2;
-        hipLaunchKernelGGL(k_tree_level, dim3((uint32_t)((3 * m + 255) / 256)), dim3(256), 0, s, a, m, b);
+        hipLaunchKernelGGL(k_tree_level, dim3((uint32_t)((m + 255) / 256), 3), dim3(256), 0, s, a, m, b);
         PNP_HIP(hipGetLastError());
         std::swap(a, b);
     }
