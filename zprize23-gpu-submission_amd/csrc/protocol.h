@@ -57,6 +57,8 @@ void k_lookup_nd(uint64_t *num, uint64_t *den, const uint64_t *f, const uint64_t
                  hipStream_t s);
 void k_mul_inplace(uint64_t *a, const uint64_t *b, uint64_t n, hipStream_t s);
 bool k_any_nonzero(const uint64_t *v, uint64_t words, DevBuf &scratch, hipStream_t s);
+void k_any_nonzero_n(const uint64_t *v, uint64_t words, uint64_t stride, int cnt, bool *nz, DevBuf &scratch,
+                     hipStream_t s);
 // any word of a differs from b
 bool k_any_diff(const uint64_t *a, const uint64_t *b, uint64_t words, DevBuf &scratch, hipStream_t s);
 // out_i = a * in_i + b

@@ -16,6 +16,7 @@
 //                  polynomial, KZG opening combine) KZG/kzg10.cu:116-145
 #include "pnp_internal.h"
 #include "protocol.h"
+#include <vector>
 
 namespace pnp {
 
@@ -132,26 +133,45 @@ void k_mul_inplace(uint64_t *a, const uint64_t *b, uint64_t n, hipStream_t s) {
 }
 
 // any non-zero word -> *flag = 1
-__global__ void k_any_nonzero_(const uint64_t *v, uint64_t words, unsigned *flag) {
-    uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
-    uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+// flag[blockIdx.y] |= any word of vector blockIdx.y (cnt vectors of `words`
+// u64 each, `stride` words apart) is nonzero; 16-byte loads, grid-stride
+__global__ __launch_bounds__(256) void k_any_nonzero_(const uint64_t *v, uint64_t words, uint64_t stride,
+                                                      unsigned *flag) {
+    const ulonglong2 *p = reinterpret_cast<const ulonglong2 *>(v + stride * blockIdx.y);
+    const uint64_t pairs = words / 2;
     uint64_t acc = 0;
-    for (; i < words; i += stride) acc |= v[i];
-    if (__any(acc != 0) && (threadIdx.x & 63) == 0) atomicOr(flag, 1u);
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < pairs;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        const ulonglong2 x = p[i];
+        acc |= x.x | x.y;
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0 && (words & 1)) acc |= v[stride * blockIdx.y + words - 1];
+    if (__any(acc != 0) && (threadIdx.x & 63) == 0) atomicOr(flag + blockIdx.y, 1u);
+}
+// nz[k] = vector k (of cnt, `words` u64 each, `stride` apart) has a nonzero
+// word; one launch, one host synchronisation
+void k_any_nonzero_n(const uint64_t *v, uint64_t words, uint64_t stride, int cnt, bool *nz, DevBuf &scratch,
+                     hipStream_t s) {
+    if (scratch.bytes < 4 * (size_t)cnt + 16) scratch.alloc(4 * (size_t)cnt + 16);
+    unsigned *flag = static_cast<unsigned *>(scratch.p);
+    PNP_HIP(hipMemsetAsync(flag, 0, 4 * (size_t)cnt, s));
+    if (words) {
+        uint64_t blocks = (words / 2 + 255) / 256;
+        if (blocks > 2048) blocks = 2048;
+        if (blocks == 0) blocks = 1;
+        hipLaunchKernelGGL(k_any_nonzero_, dim3((uint32_t)blocks, (uint32_t)cnt), dim3(256), 0, s, v, words,
+                           stride, flag);
+        PNP_HIP(hipGetLastError());
+    }
+    std::vector<unsigned> h(cnt);
+    PNP_HIP(hipMemcpyAsync(h.data(), flag, 4 * (size_t)cnt, hipMemcpyDeviceToHost, s));
+    PNP_HIP(hipStreamSynchronize(s));
+    for (int k = 0; k < cnt; k++) nz[k] = h[k] != 0;
 }
 bool k_any_nonzero(const uint64_t *v, uint64_t words, DevBuf &scratch, hipStream_t s) {
-    if (!words) return false;
-    if (scratch.bytes < 16) scratch.alloc(16);
-    unsigned *flag = static_cast<unsigned *>(scratch.p);
-    PNP_HIP(hipMemsetAsync(flag, 0, 4, s));
-    uint64_t blocks = (words + 255) / 256;
-    if (blocks > 4096) blocks = 4096;
-    hipLaunchKernelGGL(k_any_nonzero_, dim3((uint32_t)blocks), dim3(256), 0, s, v, words, flag);
-    PNP_HIP(hipGetLastError());
-    unsigned h = 0;
-    PNP_HIP(hipMemcpyAsync(&h, flag, 4, hipMemcpyDeviceToHost, s));
-    PNP_HIP(hipStreamSynchronize(s));
-    return h != 0;
+    bool nz = false;
+    if (words) k_any_nonzero_n(v, words, words, 1, &nz, scratch, s);
+    return nz;
 }
 
 __global__ void k_any_diff_(const uint64_t *a, const uint64_t *b, uint64_t words, unsigned *flag) {
@@ -206,28 +226,28 @@ __global__ __launch_bounds__(256) void k_quotient_(QuotArgs q, uint64_t N8, uint
         nx = i - jp + (__brev((j + 1) & (uint32_t)(q.n - 1)) >> (32 - q.lg_n));
     }
     Fr a = load_fr(q.w8[0], i), b = load_fr(q.w8[1], i), c = load_fr(q.w8[2], i), d = load_fr(q.w8[3], i);
-    // compute_quotient_i (widget/arithmetic.cu:7-45) + pi
-    Fr acc = a * load_fr(q.q_l, i);
+    // compute_quotient_i (widget/arithmetic.cu:7-45) + pi; sums of two
+    // products share one Montgomery reduction (fr_mul2)
+    Fr acc = fr_mul2(a, load_fr(q.q_l, i), b, load_fr(q.q_r, i));
     if (q.q_m) acc += a * b * load_fr(q.q_m, i);
-    acc += b * load_fr(q.q_r, i);
-    acc += c * load_fr(q.q_o, i);
-    acc += d * load_fr(q.q_4, i);
-    acc += pow5(a) * load_fr(q.q_hl, i);
-    acc += pow5(b) * load_fr(q.q_hr, i);
+    acc += fr_mul2(c, load_fr(q.q_o, i), d, load_fr(q.q_4, i));
+    acc += fr_mul2(pow5(a), load_fr(q.q_hl, i), pow5(b), load_fr(q.q_hr, i));
     acc += pow5(d) * load_fr(q.q_h4, i);
     acc += load_fr(q.q_c, i);
     Fr num = acc * load_fr(q.q_arith, i) + ld(q.pi8, i);  // pi8 = nullptr: closed form below
     // permutation_compute_quotient (proof_system/permutation.cu:267-296)
     Fr x = load_fr(q.lin, i);
     Fr zi = load_fr(q.z8, i), zn = load_fr(q.z8, nx);
-    Fr pa = (x * q.beta + a + q.gamma) * (x * q.bk[1] + b + q.gamma) *
-            (x * q.bk[2] + c + q.gamma) * (x * q.bk[3] + d + q.gamma);
-    pa = pa * zi * q.alpha;
+    // x beta k_j for the coset constants k = 1, 7, 13, 17 (permutation/
+    // constants.cu:3-15) by doublings and additions instead of products
+    const Fr xb = x * q.beta, x2 = xb + xb, x4 = x2 + x2, x8 = x4 + x4;
+    const Fr xb7 = x8 - xb, xb13 = x8 + x4 + xb, xb17 = x8 + x8 + xb;
+    Fr pa = (xb + a + q.gamma) * (xb7 + b + q.gamma) * (xb13 + c + q.gamma) * (xb17 + d + q.gamma);
     Fr pb = (load_fr(q.sig[0], i) * q.beta + a + q.gamma) * (load_fr(q.sig[1], i) * q.beta + b + q.gamma) *
             (load_fr(q.sig[2], i) * q.beta + c + q.gamma) * (load_fr(q.sig[3], i) * q.beta + d + q.gamma);
-    pb = pb * zn * q.alpha;
+    // alpha (pa zi - pb zn), the difference as one two-product sum
+    num += fr_mul2(pa, zi, pb, neg(zn)) * q.alpha;
     // L1 scaled by alpha^2 (quotient.cu:3-8 LDEs alpha^2 L1; linear, so fold it here)
-    num += pa - pb;
     // terms carrying L1, over Z_H (closed form) or not (LDE of L1)
     Fr l1t = (zi - Fr::one()) * q.alpha2;
     // _compute_quotient_i (widget/lookup.cu:3-134)
@@ -249,7 +269,7 @@ __global__ __launch_bounds__(256) void k_quotient_(QuotArgs q, uint64_t N8, uint
         num += lk;
     }
     if (q.l1v) {
-        Fr r = num * load_fr(q.vh_inv, i) + l1t * load_fr(q.l1v, i);
+        Fr r = fr_mul2(num, load_fr(q.vh_inv, i), l1t, load_fr(q.l1v, i));
         if (q.pinv) r += q.c_pi * load_fr(q.pinv, i);
         store_fr(out, i, r);
     } else {

@@ -388,7 +388,13 @@ int prove_impl(pnp_ctx *ctx, const CircuitC *cs, int device_ptrs, ProofC *out) {
     q.eps = eps;
     q.zeta = zeta;
     q.lsep = lsep;
+    // the kernel derives beta k_j from beta for k = 1, 7, 13, 17
     for (int j = 0; j < 4; j++) q.bk[j] = pa.bk[j];
+    if (!(pa.bk[1] == beta * fr_from_u64(7) && pa.bk[2] == beta * fr_from_u64(13) &&
+          pa.bk[3] == beta * fr_from_u64(17))) {
+        set_error("quotient: unexpected permutation coset constants");
+        return PNP_E_ARG;
+    }
     q.opd = delta + Fr::one();
     q.eopd = eps * q.opd;
     q.sep2 = lsep * lsep;
@@ -454,7 +460,11 @@ int prove_impl(pnp_ctx *ctx, const CircuitC *cs, int device_ptrs, ProofC *out) {
         CommitmentC *oc[9];
         int nc = 0;
         uint64_t nz[8];
-        for (int k = 0; k < 8; k++) nz[k] = k_any_nonzero(t_poly + 4 * (uint64_t)k * len, 4 * len, ctx->scratch_b, s);
+        {
+            bool b[8];
+            k_any_nonzero_n(t_poly, 4 * len, 4 * len, 8, b, ctx->scratch_b, s);
+            for (int k = 0; k < 8; k++) nz[k] = b[k];
+        }
         if (dist) {  // a chunk is zero when it is zero on every rank
             std::vector<uint64_t> all = shard_allgather(ctx, nz, 8);
             for (int k = 0; k < 8; k++)
