@@ -125,11 +125,11 @@ class Synthetic:
 
 
 # Integer-VALU (issue) ceiling of k_accumulate29: one XYZZ mixed addition in
-# radix-2^29 Fq compiles to 3738 v_mad_u64_u32 + 258 v_lshl_add_u64 + 260
-# v_lshrrev_b64 + 140 v_mul_lo_u32 + 78 v_add3_u32 (~4.1-4.4 cycles per wave64
-# instruction each) + ~600 two-cycle ops (v_and/v_sub/v_lshrrev_b32): ~20,750
-# SIMD cycles per 64 madds (ISA of msm.hip, costs from tools/ubench_ops.hip).
-MADD_ISSUE_CYCLES = 20745
+# radix-2^29 Fq (Y3 as a two-product sum) compiles to 3552 v_mad_u64_u32 +
+# 240 v_lshl_add_u64 + 235 v_lshrrev_b64 + 126 v_mul_lo_u32 + ... ; priced with
+# the per-wave64 issue costs of tools/ubench_ops.hip (VOP3 ~4.2, VOP1/2 ~2.2
+# cycles) by tools/isa_model.py: 19,761 SIMD cycles per 64 additions.
+MADD_ISSUE_CYCLES = 19761
 SIMDS, CLOCK_HZ = 256 * 4, 2.4e9
 
 
