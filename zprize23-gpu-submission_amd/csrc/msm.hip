@@ -497,14 +497,62 @@ __device__ __forceinline__ bool store29(uint32_t *dst, const Xyzz29 &p) {
 #ifndef PNP_ACC_WAVES
 #define PNP_ACC_WAVES 3
 #endif
-#ifndef PNP_ACC_PREFETCH
-#define PNP_ACC_PREFETCH 0
+// Folded-table entry stride in u32: x, y (14 limbs each) padded to 128 B so a
+// gathered point is exactly one cache line (112 B at a 112 B stride straddles
+// two lines in 7 of 8 cases)
+#ifndef PNP_PT29
+#define PNP_PT29 32
 #endif
+static constexpr uint64_t PT29 = PNP_PT29;
+
+// Gather staging (PNP_ACC_GLDS): the next entry's point (7 x 16 B per lane) is
+// fetched global -> LDS by global_load_lds_dwordx4 while the current entry is
+// added, so the ~us gather latency hides behind the addition without holding
+// 28 more VGPRs (register prefetch spilled at the 3-wave budget).  Each wave
+// owns 7 KiB of LDS: chunk c of lane l at stage[wave][c][l] (lane-linear, as
+// the LDS-DMA destination requires).
+#ifndef PNP_ACC_GLDS
+#define PNP_ACC_GLDS 1
+#endif
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef __attribute__((address_space(1))) void glob_void_t;
+__device__ __forceinline__ void stage_point(const uint32_t *p, uint4 *st) {
+#pragma unroll
+    for (int c = 0; c < 7; c++)
+        __builtin_amdgcn_global_load_lds((glob_void_t *)(p + 4 * c), (lds_void_t *)(st + 64 * c), 16, 0, 0);
+}
+__device__ __forceinline__ void unstage_point(const uint4 *st, F29 &x, F29 &y) {
+    uint32_t w[28];
+#pragma unroll
+    for (int c = 0; c < 7; c++) {
+        const uint4 v = st[64 * c];
+        w[4 * c] = v.x;
+        w[4 * c + 1] = v.y;
+        w[4 * c + 2] = v.z;
+        w[4 * c + 3] = v.w;
+    }
+#pragma unroll
+    for (int i = 0; i < 14; i++) {
+        x.l[i] = w[i];
+        y.l[i] = w[14 + i];
+    }
+}
+
 __global__ __launch_bounds__(256, PNP_ACC_WAVES) void k_accumulate29(const uint32_t *pts29, const uint32_t *sorted,
                                                       const uint32_t *offs, uint64_t U, uint32_t S,
                                                       uint32_t *buckets, uint32_t *head,
                                                       uint32_t *tail, uint32_t *redo,
                                                       uint32_t *nredo) {
+#if PNP_ACC_GLDS
+    // per wave: the staged point (7 x 64 x 16 B) and the staged next index
+    // (64 x 4 B); both arrive by LDS-DMA, so no ordinary global load result is
+    // consumed inside the loop (that would make the compiler drain the DMA)
+    __shared__ uint4 stage[4 * 7 * 64];
+    __shared__ uint32_t sidx[4 * 64];
+    const uint32_t wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
+    uint4 *wave_base = stage + 7 * 64 * wv;
+    uint32_t *idx_base = sidx + 64 * wv;
+#endif
     uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
     const uint32_t total = offs[U];
     const uint64_t lo64 = t * S;
@@ -521,20 +569,13 @@ __global__ __launch_bounds__(256, PNP_ACC_WAVES) void k_accumulate29(const uint3
     uint32_t next = offs[cur + 1];
     bool ok = true, fresh = true;
     Xyzz29 acc;
-#if PNP_ACC_PREFETCH == 2
-    uint32_t ei = sorted[lo];  // next entry's index, one iteration ahead
-#elif PNP_ACC_PREFETCH
-    // software pipeline: entry k+2's index and entry k+1's point are loaded
-    // while entry k is added (the gathers otherwise stall every iteration)
-    uint32_t e = sorted[lo], en = lo + 1 < hi ? sorted[lo + 1] : e;
-    F29 x = load29(pts29 + 28ULL * (e & 0x7FFFFFFFu)), y = load29(pts29 + 28ULL * (e & 0x7FFFFFFFu) + 14);
+#if PNP_ACC_GLDS
+    uint32_t e = sorted[lo];
+    stage_point(pts29 + PT29 * (e & 0x7FFFFFFFu), wave_base);
+    if (lo + 1 < hi)
+        __builtin_amdgcn_global_load_lds((glob_void_t *)(sorted + lo + 1), (lds_void_t *)idx_base, 4, 0, 0);
 #endif
     for (uint32_t k = lo; k < hi; k++) {
-#if PNP_ACC_PREFETCH == 1
-        const uint32_t *pn = pts29 + 28ULL * (en & 0x7FFFFFFFu);
-        const F29 xn = load29(pn), yn = load29(pn + 14);
-        const uint32_t enn = k + 2 < hi ? sorted[k + 2] : en;
-#endif
         if (k == next) {
             ok &= store29(first ? head + 56 * t : buckets + 56 * cur, acc);
             first = false;
@@ -544,17 +585,27 @@ __global__ __launch_bounds__(256, PNP_ACC_WAVES) void k_accumulate29(const uint3
                 next = offs[cur + 1];
             } while (next == k);
         }
-#if PNP_ACC_PREFETCH == 0
-        uint32_t e = sorted[k];
-        const uint32_t *p = pts29 + 28ULL * (e & 0x7FFFFFFFu);
+#if PNP_ACC_GLDS
+        F29 x, y;
+        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): point k and index k+1 have landed
+        unstage_point(wave_base + ln, x, y);
+        const uint32_t en = idx_base[ln];
+        __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): read out before they are overwritten
+        const uint32_t ecur = e;
+        if (k + 1 < hi) {
+            stage_point(pts29 + PT29 * (en & 0x7FFFFFFFu), wave_base);
+            if (k + 2 < hi)
+                __builtin_amdgcn_global_load_lds((glob_void_t *)(sorted + k + 2), (lds_void_t *)idx_base, 4, 0,
+                                                 0);
+            e = en;
+        }
+        if (ecur >> 31) y = neg29(y, F29_KA);
+#else
+        const uint32_t e = sorted[k];
+        const uint32_t *p = pts29 + PT29 * (e & 0x7FFFFFFFu);
         F29 x = load29(p), y = load29(p + 14);
-#elif PNP_ACC_PREFETCH == 2
-        const uint32_t e = ei;
-        ei = k + 1 < hi ? sorted[k + 1] : ei;
-        const uint32_t *p = pts29 + 28ULL * (e & 0x7FFFFFFFu);
-        F29 x = load29(p), y = load29(p + 14);
-#endif
         if (e >> 31) y = neg29(y, F29_KA);
+#endif
         if (fresh) {
             acc.x = x;
             acc.y = y;
@@ -563,12 +614,6 @@ __global__ __launch_bounds__(256, PNP_ACC_WAVES) void k_accumulate29(const uint3
         } else {
             madd29(acc, x, y);
         }
-#if PNP_ACC_PREFETCH == 1
-        x = xn;
-        y = yn;
-        e = en;
-        en = enn;
-#endif
     }
     ok &= store29(first ? head + 56 * t : (next > hi ? tail + 56 * t : buckets + 56 * cur), acc);
     if (!ok) redo[atomicAdd(nredo, 1u)] = (uint32_t)t;
@@ -583,8 +628,8 @@ __global__ __launch_bounds__(64) void k_accumulate_redo(const uint32_t *pts29, c
     uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= *nredo) return;
     auto ld = [pts29](uint32_t i, Fq &x, Fq &y) {
-        x = to_fq32(load29(pts29 + 28ULL * i));
-        y = to_fq32(load29(pts29 + 28ULL * i + 14));
+        x = to_fq32(load29(pts29 + PT29 * i));
+        y = to_fq32(load29(pts29 + PT29 * i + 14));
     };
     auto st = [=](int where, uint64_t i, const Xyzz &p) {
         uint32_t *d = (where == 0 ? buckets : where == 1 ? head : tail) + 56 * i;
@@ -643,7 +688,7 @@ __global__ void k_table_to29(const uint64_t *T, uint64_t count, uint32_t *T29) {
     uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
     if (i >= count) return;
     F29 x = from_fq32(load_fq(T + 12 * i)), y = from_fq32(load_fq(T + 12 * i + 6));
-    uint32_t *o = T29 + 28 * i;
+    uint32_t *o = T29 + PT29 * i;
 #pragma unroll
     for (int j = 0; j < 14; j++) {
         o[j] = x.l[j];
@@ -671,7 +716,7 @@ void msm_build_table(DevBuf &tab, const uint64_t *d_points, uint64_t n, int c, h
         PNP_HIP(hipStreamSynchronize(s));
     }
     const uint64_t count = (uint64_t)g.W * n;
-    tab.alloc(count * 112);
+    tab.alloc(count * PT29 * 4);
     hipLaunchKernelGGL(k_table_to29, dim3((uint32_t)((count + 255) / 256)), dim3(256), 0, s, T, count,
                        static_cast<uint32_t *>(tab.p));
     PNP_HIP(hipGetLastError());

@@ -143,7 +143,7 @@ void msm_run_batch(MsmWork &w, const uint64_t *d_points, const uint64_t *const *
 // multi-GPU MSMs: the points [p0, p1) rank `rank` of `world` takes
 void msm_point_range(uint64_t n, int rank, int world, uint64_t &p0, uint64_t &p1);
 // T[k*n + i] = 2^(c*k) P_i, k < W (msm_cfg(n)), affine, in the radix-2^29
-// form of field29.cuh (x, y: 14 u32 each, 112 B per point)
+// form of field29.cuh (x, y: 14 u32 each, padded to 128 B per point)
 void msm_build_table(DevBuf &tab, const uint64_t *d_points, uint64_t n, int c, hipStream_t s);
 // host: XYZZ -> affine Montgomery (inf -> (0, one))
 void xyzz_to_affine_host(const uint64_t *xyzz, uint64_t *aff12);
