@@ -21,7 +21,11 @@
 
 namespace pnp {
 
-static constexpr int TILE = 1024;
+#ifndef PNP_NTT_LGTILE
+#define PNP_NTT_LGTILE 10
+#endif
+static constexpr int LGTILE = PNP_NTT_LGTILE;  // elements per LDS tile = levels per pass (max)
+static constexpr int TILE = 1 << LGTILE;
 #ifndef PNP_NTT_THREADS
 #define PNP_NTT_THREADS 512
 #endif
@@ -349,7 +353,7 @@ static void ntt_core(NttTables &t, uint64_t *d, uint32_t lg, bool inverse, bool 
     if (lg_total < lg) lg_total = lg;
     const uint64_t N = 1ULL << lg_total;
     const uint64_t *tw = ntt_twiddles(t, lg, inverse, s);
-    if (lg_total < 10 || (lg <= 10 && lg_total == lg)) {
+    if (lg_total < (uint32_t)LGTILE || (lg <= (uint32_t)LGTILE && lg_total == lg)) {
         if (fz.src) {
             hipLaunchKernelGGL(k_lde_twist, dim3((uint32_t)((N + 255) / 256)), dim3(256), 0, s, fz.src,
                                fz.pre, d, fz.src_mask + 1, N);
@@ -368,9 +372,9 @@ static void ntt_core(NttTables &t, uint64_t *d, uint32_t lg, bool inverse, bool 
         }
         return;
     }
-    // split lg into passes of at most 10 levels (balanced); DIF runs them from
+    // split lg into passes of at most LGTILE levels (balanced); DIF runs them from
     // the largest half size down, DIT from the smallest up
-    const int npass = (lg + 9) / 10;
+    const int npass = (lg + LGTILE - 1) / LGTILE;
     int ks[4], rem = lg;
     for (int p = 0; p < npass; p++) {
         ks[p] = (rem + (npass - p) - 1) / (npass - p);
@@ -395,6 +399,9 @@ static void ntt_core(NttTables &t, uint64_t *d, uint32_t lg, bool inverse, bool 
         break;
             PNP_CASE(1) PNP_CASE(2) PNP_CASE(3) PNP_CASE(4) PNP_CASE(5)
             PNP_CASE(6) PNP_CASE(7) PNP_CASE(8) PNP_CASE(9) PNP_CASE(10)
+#if PNP_NTT_LGTILE >= 11
+            PNP_CASE(11)
+#endif
 #undef PNP_CASE
             default:
                 set_error("bad NTT pass size %d", k);
