@@ -28,6 +28,32 @@ struct F29 {
 
 #define F29_M 0x1FFFFFFFu
 
+// acc + a b as ONE v_mad_u64_u32 the compiler cannot reassociate: with plain
+// C++ additions LLVM starts every column's products from 0 and adds the
+// carry afterwards (one v_lshl_add_u64 per column, ~5% of a product)
+#ifndef PNP_F29_ASM
+#define PNP_F29_ASM 0
+#endif
+// acc + a q with the modulus limb q in an SGPR (a compile-time constant)
+__device__ __forceinline__ uint64_t mad29q(uint32_t a, uint32_t q, uint64_t acc) {
+#if PNP_F29_ASM
+    uint64_t r, cdummy;
+    asm volatile("v_mad_u64_u32 %0, %1, %2, %3, %4" : "=v"(r), "=s"(cdummy) : "v"(a), "s"(q), "v"(acc));
+    return r;
+#else
+    return acc + (uint64_t)a * q;
+#endif
+}
+__device__ __forceinline__ uint64_t mad29(uint32_t a, uint32_t b, uint64_t acc) {
+#if PNP_F29_ASM
+    uint64_t r, cdummy;
+    asm volatile("v_mad_u64_u32 %0, %1, %2, %3, %4" : "=v"(r), "=s"(cdummy) : "v"(a), "v"(b), "v"(acc));
+    return r;
+#else
+    return acc + (uint64_t)a * b;
+#endif
+}
+
 // Montgomery product a b 2^-406 (product scanning, one 64-bit accumulator)
 __device__ __forceinline__ F29 mul29(const F29 &a, const F29 &b) {
     uint32_t m[14];
@@ -36,12 +62,12 @@ __device__ __forceinline__ F29 mul29(const F29 &a, const F29 &b) {
 #pragma unroll
     for (int k = 0; k < 27; k++) {
 #pragma unroll
-        for (int i = (k > 13 ? k - 13 : 0); i <= (k < 13 ? k : 13); i++) acc += (uint64_t)a.l[i] * b.l[k - i];
+        for (int i = (k > 13 ? k - 13 : 0); i <= (k < 13 ? k : 13); i++) acc = mad29(a.l[i], b.l[k - i], acc);
 #pragma unroll
-        for (int i = (k > 13 ? k - 13 : 0); i < (k < 14 ? k : 14); i++) acc += (uint64_t)m[i] * F29_Q[k - i];
+        for (int i = (k > 13 ? k - 13 : 0); i < (k < 14 ? k : 14); i++) acc = mad29q(m[i], F29_Q[k - i], acc);
         if (k < 14) {
             m[k] = ((uint32_t)acc * F29_QINV) & F29_M;
-            acc += (uint64_t)m[k] * F29_Q[0];
+            acc = mad29q(m[k], F29_Q[0], acc);
         } else {
             r.l[k - 14] = (uint32_t)acc & F29_M;
         }
@@ -64,13 +90,13 @@ __device__ __forceinline__ F29 sqr29(const F29 &a) {
 #pragma unroll
     for (int k = 0; k < 27; k++) {
 #pragma unroll
-        for (int i = (k > 13 ? k - 13 : 0); 2 * i < k; i++) acc += (uint64_t)a.l[i] * a2[k - i];
-        if ((k & 1) == 0) acc += (uint64_t)a.l[k / 2] * a.l[k / 2];
+        for (int i = (k > 13 ? k - 13 : 0); 2 * i < k; i++) acc = mad29(a.l[i], a2[k - i], acc);
+        if ((k & 1) == 0) acc = mad29(a.l[k / 2], a.l[k / 2], acc);
 #pragma unroll
-        for (int i = (k > 13 ? k - 13 : 0); i < (k < 14 ? k : 14); i++) acc += (uint64_t)m[i] * F29_Q[k - i];
+        for (int i = (k > 13 ? k - 13 : 0); i < (k < 14 ? k : 14); i++) acc = mad29q(m[i], F29_Q[k - i], acc);
         if (k < 14) {
             m[k] = ((uint32_t)acc * F29_QINV) & F29_M;
-            acc += (uint64_t)m[k] * F29_Q[0];
+            acc = mad29q(m[k], F29_Q[0], acc);
         } else {
             r.l[k - 14] = (uint32_t)acc & F29_M;
         }
@@ -93,14 +119,14 @@ __device__ __forceinline__ F29 mul2_29(const F29 &a, const F29 &b, const F29 &c,
     for (int k = 0; k < 27; k++) {
 #pragma unroll
         for (int i = (k > 13 ? k - 13 : 0); i <= (k < 13 ? k : 13); i++) {
-            acc += (uint64_t)a.l[i] * b.l[k - i];
-            acc += (uint64_t)c.l[i] * d.l[k - i];
+            acc = mad29(a.l[i], b.l[k - i], acc);
+            acc = mad29(c.l[i], d.l[k - i], acc);
         }
 #pragma unroll
-        for (int i = (k > 13 ? k - 13 : 0); i < (k < 14 ? k : 14); i++) acc += (uint64_t)m[i] * F29_Q[k - i];
+        for (int i = (k > 13 ? k - 13 : 0); i < (k < 14 ? k : 14); i++) acc = mad29q(m[i], F29_Q[k - i], acc);
         if (k < 14) {
             m[k] = ((uint32_t)acc * F29_QINV) & F29_M;
-            acc += (uint64_t)m[k] * F29_Q[0];
+            acc = mad29q(m[k], F29_Q[0], acc);
         } else {
             r.l[k - 14] = (uint32_t)acc & F29_M;
         }

@@ -96,7 +96,10 @@ struct KeyRows {
 // bin's entries leave as one run (a one-pass scatter straight to 2^15 buckets
 // wrote ~8x its payload to HBM).  Keys, fine keys and entries are read four
 // per lane (8 / 4 / 16-byte loads).
-constexpr int SORT_CB = 8;
+#ifndef PNP_SORT_CB
+#define PNP_SORT_CB 9
+#endif
+constexpr int SORT_CB = PNP_SORT_CB;
 constexpr int SORT_FB_MAX = 11;
 __global__ __launch_bounds__(1024) void k_coarse_hist(const uint32_t *keys, KeyRows kr, int fb,
                                                       int NBc, uint64_t chunk, int nch,
@@ -200,7 +203,7 @@ static void scan_u32(uint32_t *d, uint64_t n, DevBuf &scratch, hipStream_t s) {
 // entries of a tile leave as one contiguous run (coalesced stores).
 constexpr int TILE_K = 4096;
 __device__ __forceinline__ void tile_scan(uint32_t *lh, uint32_t *lofs, int nb) {
-    // exclusive scan of lh[0..nb) into lofs by wave 0 (nb <= 256)
+    // exclusive scan of lh[0..nb) into lofs by wave 0
     if (threadIdx.x < 64) {
         const int per = (nb + 63) / 64, b0 = threadIdx.x * per;
         uint32_t loc = 0;
@@ -284,7 +287,10 @@ __global__ __launch_bounds__(1024) void k_coarse_scatter(const uint32_t *keys, K
 // [p << fb, (p + 1) << fb); writes every bucket's start and the sorted entries
 // Histogram first (bucket starts), then tiles of 8192 entries counting-sorted
 // in LDS and written out one run per fine bin (~32 entries at 2^22).
-constexpr int TILE_F = 8192;
+#ifndef PNP_TILE_F
+#define PNP_TILE_F 8192
+#endif
+constexpr int TILE_F = PNP_TILE_F;
 __global__ __launch_bounds__(1024) void k_fine_sort(const uint32_t *ent, const uint16_t *fk,
                                                     const uint32_t *coffs, int nch, int fb,
                                                     uint32_t *bstart, uint32_t *sorted) {
