@@ -222,3 +222,82 @@ def test_madd_chain(seed):
     X, Y, ZZ, ZZZ = (from_m(v) for v in acc)
     assert X * pow(ZZ, -1, Q) % Q == ref[0]
     assert Y * pow(ZZZ, -1, Q) % Q == ref[1]
+
+
+# ---- general XYZZ addition / doubling in radix 2^29 (groundwork for the
+# bucket merge and tree in F29; not yet used by a kernel)
+def add29n(a, b):
+    """a + b with carries normalised (limbs < 2^29)."""
+    r, c = [0] * 14, 0
+    for i in range(13):
+        t = a[i] + b[i] + c
+        r[i], c = t & M29, t >> 29
+    r[13] = a[13] + b[13] + c
+    return r
+
+
+def xadd29(p, q):
+    """add-2008-s on XYZZ inputs, no exceptional cases (they leave ZZ = 0 mod q)."""
+    KA, KB = C["F29_KA"], C["F29_KB"]
+    X1, Y1, ZZ1, ZZZ1 = p
+    X2, Y2, ZZ2, ZZZ2 = q
+    u1, u2 = mul29(X1, ZZ2), mul29(X2, ZZ1)
+    s1, s2 = mul29(Y1, ZZZ2), mul29(Y2, ZZZ1)
+    P, R = sub29(u2, u1, KB), sub29(s2, s1, KB)
+    pp = sqr29(P)
+    ppp = mul29(P, pp)
+    q_ = mul29(u1, pp)
+    x3 = sub29(sub29(sub29(sqr29(R), ppp, KA), q_, KA), q_, KA)
+    assert val(x3) < 2**389
+    y3 = mul2_29(R, sub29(q_, x3, KB), s1, sub29([0] * 14, ppp, KA))
+    return x3, y3, mul29(mul29(ZZ1, ZZ2), pp), mul29(mul29(ZZZ1, ZZZ2), ppp)
+
+
+def xdbl29(p):
+    """dbl-2008-s-1 (a = 0) on an XYZZ input."""
+    KA, KB = C["F29_KA"], C["F29_KB"]
+    X, Y, ZZ, ZZZ = p
+    U = add29n(Y, Y)
+    V = sqr29(U)
+    W = mul29(U, V)
+    S = mul29(X, V)
+    xx = sqr29(X)
+    M = add29n(add29n(xx, xx), xx)
+    x3 = sub29(sub29(sqr29(M), S, KA), S, KA)
+    assert val(x3) < 2**389
+    y3 = mul2_29(M, sub29(S, x3, KB), W, sub29([0] * 14, Y, KB))
+    return x3, y3, mul29(V, ZZ), mul29(W, ZZZ)
+
+
+def _aff(p):
+    X, Y, ZZ, ZZZ = (from_m(v) for v in p)
+    return X * pow(ZZ, -1, Q) % Q, Y * pow(ZZZ, -1, Q) % Q
+
+
+def _dbl_aff(p):
+    x, y = p
+    lam = 3 * x * x * pow(2 * y, -1, Q) % Q
+    x3 = (lam * lam - 2 * x) % Q
+    return x3, (lam * (x - x3) - y) % Q
+
+
+def _mulg(k):
+    acc, base = None, (G1X, G1Y)
+    while k:
+        if k & 1:
+            acc = base if acc is None else aff_add(acc, base)
+        base = _dbl_aff(base)
+        k >>= 1
+    return acc
+
+
+def test_xadd_xdbl():
+    rnd = random.Random(7)
+    a, b = _mulg(rnd.randrange(1, 2**64)), _mulg(rnd.randrange(1, 2**64))
+    A = (to_m(a[0]), to_m(a[1]), to_m(1), to_m(1))
+    B = (to_m(b[0]), to_m(b[1]), to_m(1), to_m(1))
+    AB = xadd29(A, B)
+    assert _aff(AB) == aff_add(a, b)
+    assert _aff(xdbl29(A)) == _dbl_aff(a)
+    assert _aff(xadd29(AB, A)) == aff_add(aff_add(a, b), a)
+    assert _aff(xdbl29(AB)) == _dbl_aff(aff_add(a, b))
