@@ -72,6 +72,9 @@ void or_transcript_append_scalar(or_transcript *t, const char *label, const uint
 void or_transcript_append_point(or_transcript *t, const char *label, const uint64_t aff[12]);
 void or_transcript_append_pi(or_transcript *t, const char *label,
                              const uint64_t pi_canon[4], uint64_t pos);
+/* several public inputs, positions strictly increasing (BTreeMap order) */
+void or_transcript_append_pis(or_transcript *t, const char *label, uint64_t k,
+                              const uint64_t *pos, const uint64_t *vals_canon);
 void or_transcript_challenge_bytes(or_transcript *t, const char *label, uint8_t *out, size_t len);
 void or_transcript_challenge_scalar(or_transcript *t, const char *label, uint64_t out_mont[4]);
 /* raw state for fixtures: 200 B strobe state + pos, pos_begin, cur_flags */
@@ -81,6 +84,35 @@ void or_keccak_f1600(uint64_t st[25]);
 
 /* ---- full prover: gen_proof.cuh:10-489 ---- */
 int or_gen_proof(const CircuitC *cs, const ProverKeyC *pk, const CommitKeyC *ck, ProofC *out);
+
+/* ---- verifier: proof.rs:123-431 (Proof::verify), circuit.rs:325-344 ---- */
+/* commitments to the preprocessed polynomials, affine Montgomery, infinity
+ * = (0, Fq one); g = powers_of_g[0] (the KZG verifier key's G) */
+#define OR_VK_POLYS 23
+typedef struct {
+    uint64_t n;
+    uint64_t g[12];
+    uint64_t q_m[12], q_l[12], q_r[12], q_o[12], q_4[12], q_c[12], q_hl[12], q_hr[12], q_h4[12],
+        q_arith[12];
+    uint64_t range[12], logic[12], fixed_group_add[12], variable_group_add[12];
+    uint64_t left_sigma[12], right_sigma[12], out_sigma[12], fourth_sigma[12];
+    uint64_t q_lookup[12], table_1[12], table_2[12], table_3[12], table_4[12];
+} or_verifier_key;
+/* slots in the order q_m, q_l, q_r, q_o, q_4, q_c, q_hl, q_hr, q_h4, q_arith,
+ * range, logic, fixed_group_add, variable_group_add, left/right/out/fourth
+ * sigma, q_lookup, table_1..4 */
+void or_vk_slots(or_verifier_key *vk, uint64_t (*dst[OR_VK_POLYS])[12]);
+void or_verifier_key_from_coeffs(or_verifier_key *vk, uint64_t n, const uint64_t *srs,
+                                 const uint64_t *const coeffs[OR_VK_POLYS]);
+/* the two KZG openings reduced to G1: out = {L_aw, W_aw, L_saw, W_saw} with
+ * L = sum ch^i C_i - (sum ch^i v_i) G + x W; accept iff e(L, H) = e(W, [tau]H) */
+int or_verify_kzg_points(const or_verifier_key *vk, const ProofC *p, const char *label,
+                         uint64_t n_pi, const uint64_t *pi_pos, const uint64_t *pi_canon,
+                         uint64_t out[4][12]);
+/* 1 = accept, 0 = reject; the pairing check decided with the SRS trapdoor
+ * (L == tau W) */
+int or_verify(const or_verifier_key *vk, const ProofC *p, const char *label, uint64_t n_pi,
+              const uint64_t *pi_pos, const uint64_t *pi_canon, const uint64_t tau_mont[4]);
 
 /* threads used by the OpenMP loops (for cpu_baseline.cores) */
 int or_num_threads(void);

@@ -186,6 +186,33 @@ void or_transcript_append_point(or_transcript *t, const char *label, const uint6
     or_transcript_append_message(t, label, buf, 48);
 }
 
+/* PublicInputs (pi.rs:16-22) serialised as its BTreeMap<usize, F>
+ * (ark-serialize 0.3: u64 length, then (u64 key, 32-byte canonical value)
+ * per entry in key order); zero values are never inserted (pi.rs:39-46). */
+void or_transcript_append_pis(or_transcript *t, const char *label, uint64_t k,
+                              const uint64_t *pos, const uint64_t *vals_canon) {
+    uint64_t len = 0;
+    for (uint64_t i = 0; i < k; i++) {
+        uint64_t m[4];
+        or_fr_to_mont(m, vals_canon + 4 * i);
+        len += !or_fr_is_zero(m);
+    }
+    uint8_t *buf = (uint8_t *)malloc(8 + 40 * (len ? len : 1));
+    memcpy(buf, &len, 8);
+    size_t at = 8;
+    for (uint64_t i = 0; i < k; i++) {
+        uint64_t m[4], c[4];
+        or_fr_to_mont(m, vals_canon + 4 * i);
+        if (or_fr_is_zero(m)) continue;
+        or_fr_from_mont(c, m);
+        memcpy(buf + at, pos + i, 8);
+        memcpy(buf + at + 8, c, 32);
+        at += 40;
+    }
+    or_transcript_append_message(t, label, buf, at);
+    free(buf);
+}
+
 void or_transcript_append_pi(or_transcript *t, const char *label,
                              const uint64_t pi_canon[4], uint64_t pos) {
     uint8_t buf[48];

@@ -298,3 +298,74 @@ class Inputs:
         rc = lib.or_gen_proof(C.byref(self.circuit), C.byref(self.pk), C.byref(self.ck), C.byref(out))
         assert rc == 0, rc
         return out
+
+
+# ------------------------------------------------------------------ verifier
+# or_verifier_key (oracle/pnp_oracle.h): n, g[12], then 23 commitments of 12 u64
+VK_POLYS = ("q_m", "q_l", "q_r", "q_o", "q_4", "q_c", "q_hl", "q_hr", "q_h4", "q_arith",
+            "range_selector", "logic_selector", "fixed_group_add_selector",
+            "variable_group_add_selector", "left_sigma", "right_sigma", "out_sigma",
+            "fourth_sigma", "q_lookup", "table1", "table2", "table3", "table4")
+VK_WORDS = 1 + 12 + 12 * len(VK_POLYS)
+
+
+def _sig_verifier(lib):
+    if getattr(lib, "_vk_sig", False):
+        return
+    vp_ = C.c_void_p
+    lib.or_verifier_key_from_coeffs.argtypes = [vp_, C.c_uint64, vp_, C.c_void_p * len(VK_POLYS)]
+    lib.or_verify_kzg_points.argtypes = [vp_, vp_, C.c_char_p, C.c_uint64, vp_, vp_, vp_]
+    lib.or_verify_kzg_points.restype = C.c_int
+    lib.or_verify.argtypes = [vp_, vp_, C.c_char_p, C.c_uint64, vp_, vp_, vp_]
+    lib.or_verify.restype = C.c_int
+    lib._vk_sig = True
+
+
+def verifier_key(coeffs: dict, n: int, srs: np.ndarray) -> np.ndarray:
+    """Commitments to the preprocessed polynomials (the VerifierKey that
+    Circuit::compile returns, circuit.rs:232-264); coeffs maps a VK_POLYS name
+    to its n Montgomery coefficients, absent = the zero polynomial."""
+    lib = oracle()
+    _sig_verifier(lib)
+    vk = np.zeros(VK_WORDS, dtype=np.uint64)
+    keep = [np.ascontiguousarray(coeffs[k]) if k in coeffs else None for k in VK_POLYS]
+    ptrs = (C.c_void_p * len(VK_POLYS))(*[C.c_void_p(a.ctypes.data) if a is not None else None
+                                          for a in keep])
+    lib.or_verifier_key_from_coeffs(vp(vk), n, vp(np.ascontiguousarray(srs)), ptrs)
+    return vk
+
+
+def _pi_args(pis):
+    pos = np.array([p for p, _ in pis], dtype=np.uint64)
+    vals = np.array([to_limbs(v, 4) for _, v in pis], dtype=np.uint64).reshape(-1, 4)
+    return pos, vals
+
+
+def verify(vk: np.ndarray, proof: abi.ProofC, pis, tau_mont, label=b"Merkle tree") -> bool:
+    """Oracle verifier (proof.rs:123-431) deciding the KZG checks with the SRS
+    trapdoor tau; pis = [(pos, canonical value)]."""
+    lib = oracle()
+    _sig_verifier(lib)
+    pos, vals = _pi_args(pis)
+    tau = np.ascontiguousarray(np.asarray(tau_mont, dtype=np.uint64).reshape(4))
+    return lib.or_verify(vp(vk), C.byref(proof), label, len(pis), vp(pos), vp(vals), vp(tau)) == 1
+
+
+def kzg_points(vk: np.ndarray, proof: abi.ProofC, pis, label=b"Merkle tree"):
+    """(L_aw, W_aw, L_saw, W_saw) affine: accept iff e(L, H) = e(W, [tau] H)."""
+    lib = oracle()
+    _sig_verifier(lib)
+    pos, vals = _pi_args(pis)
+    out = np.zeros((4, 12), dtype=np.uint64)
+    rc = lib.or_verify_kzg_points(vp(vk), C.byref(proof), label, len(pis), vp(pos), vp(vals), vp(out))
+    return rc, out
+
+
+def inputs_vk(inp: "Inputs") -> np.ndarray:
+    a = inp.arrays
+    coeffs = {k: a[k + "_coeffs"] for k in VK_POLYS if k + "_coeffs" in a}
+    return verifier_key(coeffs, inp.n, a["srs"])
+
+
+def inputs_pis(inp: "Inputs"):
+    return [(inp.pi_pos, from_limbs(inp.arrays["pi"]))]
