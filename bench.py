@@ -14,13 +14,16 @@ points and Z_H values; SRS = [tau^i] G.
     python bench.py [--gpus N --steps K --warmup W]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
 
-N > 1: one process per GPU; all ranks prove the SAME instance together: the
-non-MSM pipeline is replicated (deterministic, every rank holds the same
-transcript) and every batched MSM's virtual windows are split across the ranks,
-whose window sums meet in one RCCL in-place all-gather per batch
-(pnp.shard.WindowExchange -> pnp_set_msm_shard).  value = max over ranks of
-the per-proof time (strong scaling: one proof regardless of N).  Rank 0 prints
-ONE JSON line.
+N > 1: one process per GPU; all ranks prove the SAME instance together
+(DESIGN.md 6): every MSM is split by point ranges (rank r sums points
+[r n/N, (r+1) n/N) over all windows; the partial sums meet in one RCCL
+all-gather per batch), round 4 is split by coset blocks / coefficient ranges
+with one all-to-all, rounds 1-3 and the transcript are replicated.  value =
+max over ranks of the per-proof time (strong scaling: one proof regardless of
+N).  Rank 0 prints ONE JSON line.  Without WORLD_SIZE in the environment,
+`--gpus N` (N > 1) relaunches itself under torch.distributed.run with N ranks
+before touching the GPU, and refuses to run when fewer than N GPUs are
+visible; a world size different from --gpus is an error.
 """
 import argparse
 import ctypes as C
@@ -124,13 +127,31 @@ class Synthetic:
                                w_r=abi.ptr(w["w_r"]), w_o=abi.ptr(w["w_o"]), w_4=abi.ptr(w["w_4"]))
 
 
-# Integer-VALU (issue) ceiling of k_accumulate29: one XYZZ mixed addition in
-# radix-2^29 Fq (Y3 as a two-product sum) compiles to 3552 v_mad_u64_u32 +
-# 240 v_lshl_add_u64 + 235 v_lshrrev_b64 + 126 v_mul_lo_u32 + ... ; priced with
-# the per-wave64 issue costs of tools/ubench_ops.hip (VOP3 ~4.2, VOP1/2 ~2.2
-# cycles) by tools/isa_model.py: 19,761 SIMD cycles per 64 additions.
+# Roofline of k_accumulate29 (integer-VALU bound): every sorted
+# (point, window) entry is one XYZZ mixed addition = 8M + 2S = 10 Fq products;
+# the hardware bound is the v_mad_u64_u32 issue rate measured by
+# tools/ubench_ops.hip (profiles/r02_ubench_ops.txt: cycles per wave64
+# instruction per SIMD) over 288 = 2 x 12 x 12 32-bit multiply-adds per
+# 381-bit Montgomery product (the textbook CIOS count; this build's radix-2^29
+# product spends 392).  The issue-model ceiling (tools/isa_model.py: 19,761
+# SIMD cycles per 64 additions of the compiled code) is kept as a secondary.
+FQ_PRODUCTS_PER_MADD = 10
+MADS_PER_FQ_PRODUCT = 288
 MADD_ISSUE_CYCLES = 19761
 SIMDS, CLOCK_HZ = 256 * 4, 2.4e9
+UBENCH_FILE = os.path.join(REPO, "profiles", "r02_ubench_ops.txt")
+
+
+def mad_cycles():
+    """Measured cycles per wave64 v_mad_u64_u32 per SIMD (independent chains)."""
+    try:
+        with open(UBENCH_FILE) as f:
+            for line in f:
+                if line.startswith("v_mad_u64_u32(sdst)") and "cyc per wave64" in line:
+                    return float(line.split("=")[1].split()[0])
+    except OSError:
+        pass
+    return 4.1  # DESIGN.md 4 (round 1 measurement)
 
 
 PMC_FILE = os.path.join(REPO, "profiles", "r01_pmc", "accumulate_traffic.json")
@@ -147,21 +168,118 @@ def pmc_traffic():
         return None
 
 
+CPU_SCALING_FILE = os.path.join(REPO, "profiles", "r02_cpu_scaling.json")
+
+
+def cpu_exponent():
+    """Fitted exponent b of t = a n^b for the CPU restatement's gen_proof
+    (tools/cpu_scaling.py over 2^15 .. 2^22, profiles/r02_cpu_scaling.json)."""
+    try:
+        with open(CPU_SCALING_FILE) as f:
+            return float(json.load(f)["fit"]["exponent"])
+    except (OSError, ValueError, KeyError):
+        return None
+
+
 def cpu_baseline(lg: int, seconds_budget: float):
     """Time the CPU restatement (oracle/, test infrastructure) on one bounded
-    gen_proof sample of the same circuit shape; rank 0 only."""
+    gen_proof sample of the bench's own instance shape (tests/synth_cpu.py =
+    bench.Synthetic on the CPU); rank 0 only."""
     sys.path.insert(0, os.path.join(REPO, "tests"))
-    from pnp_testlib import Inputs, oracle
+    from pnp_testlib import oracle
+    from synth_cpu import SyntheticCPU
     lib = oracle()
-    inp = Inputs(lg, 7, n_gates=int(HEIGHT15_GATES / (1 << 22) * (1 << lg)))
+    gates = int(HEIGHT15_GATES / (1 << 22) * (1 << lg))
+    syn = SyntheticCPU(lg, gates, seed=1)
     t0 = time.perf_counter()
-    inp.oracle_proof()
+    syn.oracle_proof()
     dt = time.perf_counter() - t0
-    return {"value": round(dt, 3), "unit": f"s per gen_proof at n=2^{lg}",
-            "cores": int(lib.or_num_threads()), "kind": "port",
-            "sample": f"one gen_proof of the same circuit shape at n=2^{lg} "
-                      f"({inp.n_gates} gates) with the C restatement (oracle/, OpenMP)",
-            "extrapolated_full_s": round(dt * (1 << (22 - lg)) * 22 / lg, 1)}
+    b = cpu_exponent()
+    out = {"value": round(dt, 3), "unit": f"s per gen_proof at n=2^{lg}",
+           "cores": int(lib.or_num_threads()), "kind": "port",
+           "sample": f"one gen_proof of bench.Synthetic's shape at n=2^{lg} ({gates} gates) with "
+                     f"the C restatement (oracle/, OpenMP), instance generation excluded"}
+    if b is not None:
+        out["extrapolated_full_s"] = round(dt * (2.0 ** ((22 - lg) * b)), 1)
+        out["extrapolation"] = f"t ~ n^{b:.3f} fitted over measured 2^15..2^22 (profiles/r02_cpu_scaling.json)"
+    return out
+
+
+def drop_in(ctx, syn, steps: int, v1: bool):
+    """What a drop-in Rust caller pays, measured after the
+    headline: (a) v2 pnp_prove with the witness in HOST memory (CircuitC as
+    prove_pnp builds it, prover.rs:727-762: ~4 x 3.16 M x 32 B over PCIe,
+    inside the timed call); (b) the v1 symbol gen_proof with every key in host
+    memory: its first call copies the keys and builds the folded table, later
+    calls reuse them (key fingerprint, csrc/abi.cpp) and pay only the witness
+    upload.  Not `value`: the headline has inputs already in HBM."""
+    import numpy as np
+    import torch
+    from pnp import abi
+    host = {}
+
+    def h(addr):
+        if addr not in host:
+            for t in syn.keep.values():
+                if t.data_ptr() == addr:
+                    host[addr] = np.ascontiguousarray(t.cpu().numpy())
+                    break
+        return host[addr]
+
+    def hp(p):
+        return abi.ptr(h(C.cast(p, C.c_void_p).value).ctypes.data)
+
+    cs = syn.cs
+    cs_h = abi.CircuitC(n=cs.n, lookup_len=cs.lookup_len, intended_pi_pos=cs.intended_pi_pos,
+                        q_lookup=hp(cs.q_lookup), pi=cs.pi, w_l=hp(cs.w_l), w_r=hp(cs.w_r),
+                        w_o=hp(cs.w_o), w_4=hp(cs.w_4))
+    out = {}
+    ctx.prove(cs_h, device_ptrs=False)
+    ctx.sync()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        ctx.prove(cs_h, device_ptrs=False)
+    ctx.sync()
+    out["v2_host_witness_s"] = round((time.perf_counter() - t0) / steps, 4)
+    out["v2_host_witness_inputs_ms"] = round(dict(ctx.stage_times()).get("inputs", 0.0), 2)
+    if v1:
+        pk_h = abi.ProverKeyC()
+        for f in abi.PK_FIELDS:
+            setattr(pk_h, f, hp(getattr(syn.pk, f)))
+        ck_h = abi.CommitKeyC(powers_of_g=hp(syn.ck.powers_of_g),
+                              powers_of_gamma_g=hp(syn.ck.powers_of_gamma_g))
+        lib = ctx.lib
+        t0 = time.perf_counter()
+        first = lib.gen_proof(cs_h, pk_h, ck_h)
+        out["v1_first_call_s"] = round(time.perf_counter() - t0, 3)
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            p = lib.gen_proof(cs_h, pk_h, ck_h)
+        out["v1_gen_proof_s"] = round((time.perf_counter() - t0) / steps, 4)
+        ref = ctx.prove(syn.cs, device_ptrs=True)
+        out["v1_equals_v2"] = (abi.proof_to_bytes(p) == abi.proof_to_bytes(ref) ==
+                               abi.proof_to_bytes(first))
+    torch.cuda.synchronize()
+    return out
+
+
+def relaunch(n: int) -> int:
+    """Start N ranks (one per GPU) under torch.distributed.run as a CHILD
+    process; this process never initialises the GPU (device_count() does not
+    on this image)."""
+    import subprocess
+    import torch
+    have = torch.cuda.device_count()
+    if have < n:
+        log(f"bench: --gpus {n} but only {have} GPU(s) visible")
+        return 2
+    import socket
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)]
+    return subprocess.call(cmd + sys.argv[1:])
 
 
 def main():
@@ -171,13 +289,20 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--lg", type=int, default=22, help="log2 domain (22 = HEIGHT 15)")
     ap.add_argument("--gates", type=int, default=HEIGHT15_GATES)
-    ap.add_argument("--cpu-lg", type=int, default=15, help="CPU baseline sample size; 0 = skip")
+    ap.add_argument("--cpu-lg", type=int, default=17, help="CPU baseline sample size; 0 = skip")
     ap.add_argument("--stages", action="store_true", help="print per-stage ms to stderr")
+    ap.add_argument("--drop-in", default="v1", choices=("", "v2", "v1"),
+                    help="also time the host-witness v2 call ('v2') and the v1 symbol ('v1')")
     args = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        return relaunch(args.gpus)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log(f"bench: WORLD_SIZE={world} but --gpus {args.gpus}")
+        return 2
     import torch
     import torch.distributed as dist
     torch.cuda.set_device(local)
@@ -238,6 +363,10 @@ def main():
         # mixed additions = sorted (point, window) entries, counted by the library
         madds_per_s = entries / (acc_ms / 1e3) if acc_ms > 0 else 0.0
         valu_peak = SIMDS * CLOCK_HZ * 64 / MADD_ISSUE_CYCLES
+        mad_rate = SIMDS * CLOCK_HZ * 64 / mad_cycles()          # v_mad_u64_u32 / s
+        fq_peak = mad_rate / MADS_PER_FQ_PRODUCT                 # Fq products / s
+        fq_achieved = madds_per_s * FQ_PRODUCTS_PER_MADD
+        traffic = pmc_traffic()
         q_gbs = q_bytes / (q_ms / 1e3) / 1e9 if q_ms > 0 else 0.0
         out = {
             "metric": METRIC,
@@ -255,23 +384,36 @@ def main():
             "config": {"workload": f"HEIGHT=15 gen_proof: {gates} gates, domain 2^{args.lg}, "
                                    f"quotient on 2^{args.lg + 3} coset, pk+SRS+witness HBM-resident",
                        "domain_log2": args.lg, "gates": gates,
-                       "parallelism": f"msm-window-shard x{world}" if world > 1 else "single"},
-            "roofline": {"bound": "hbm", "kernel": "k_accumulate29 (MSM bucket accumulation)",
-                         "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": pmc_traffic(),
-                         "note": "k_accumulate is integer-VALU bound (XYZZ mixed adds), not "
-                                 "HBM bound; algorithmic bytes = points*(96+32) per window "
-                                 "sweep (SURVEY 8d); 'valu' gives the binding ceiling",
+                       "parallelism": (f"msm-point-range-shard + round4-block-shard x{world}"
+                                       if world > 1 else "single")},
+            "roofline": {"bound": "valu", "kernel": "k_accumulate29 (MSM bucket accumulation)",
+                         "achieved": round(fq_achieved / 1e9, 2), "peak": round(fq_peak / 1e9, 2),
+                         "unit": "G Fq-mul/s", "frac": round(fq_achieved / fq_peak, 4),
+                         "traffic": traffic,
+                         "traffic_over_algorithmic": (round(traffic / (acc_bytes / max(acc_n, 1)), 2)
+                                                      if traffic and acc_bytes else None),
+                         "work": "library-counted mixed additions x 10 Fq products (8M+2S) / "
+                                 "average launch duration (HIP events on the library stream)",
+                         "peak_basis": f"{mad_cycles():.2f} cycles per wave64 v_mad_u64_u32 per "
+                                       f"SIMD (profiles/r02_ubench_ops.txt) x 1024 SIMDs x 2.4 GHz "
+                                       f"/ {MADS_PER_FQ_PRODUCT} mads per Fq product",
                          "launch_ms": round(acc_avg_s * 1e3, 3),
                          "bytes_per_launch": round(acc_bytes / max(acc_n, 1)),
-                         "valu": {"achieved_gmadd_s": round(madds_per_s / 1e9, 3),
-                                  "peak_gmadd_s": round(valu_peak / 1e9, 3),
-                                  "frac": round(madds_per_s / valu_peak, 4)},
+                         "madds_per_s": round(madds_per_s / 1e9, 3),
+                         "issue_model": {"peak_gmadd_s": round(valu_peak / 1e9, 3),
+                                         "frac": round(madds_per_s / valu_peak, 4),
+                                         "basis": "tools/isa_model.py: 19,761 SIMD cycles per 64 "
+                                                  "mixed additions of the compiled kernel"},
+                         "hbm": {"achieved_gbs": round(achieved, 1), "peak_gbs": HBM_PEAK_GBS,
+                                 "frac": round(achieved / HBM_PEAK_GBS, 5),
+                                 "basis": "algorithmic bytes n*(96+32) per window sweep"},
                          "quotient": {"bound": "hbm", "achieved": round(q_gbs, 1),
                                       "peak": HBM_PEAK_GBS, "frac": round(q_gbs / HBM_PEAK_GBS, 4),
                                       "launch_ms": round(q_ms / max(q_n, 1), 3)}},
             "stages_ms": {k: round(v, 2) for k, v in stages},
         }
+        if args.drop_in and world == 1:
+            out["drop_in"] = drop_in(ctx, syn, args.steps, v1=args.drop_in == "v1")
         if args.cpu_lg:
             try:
                 out["cpu_baseline"] = cpu_baseline(args.cpu_lg, 30.0)
@@ -284,4 +426,4 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main() or 0)

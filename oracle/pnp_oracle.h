@@ -114,6 +114,12 @@ int or_verify_kzg_points(const or_verifier_key *vk, const ProofC *p, const char 
 int or_verify(const or_verifier_key *vk, const ProofC *p, const char *label, uint64_t n_pi,
               const uint64_t *pi_pos, const uint64_t *pi_canon, const uint64_t tau_mont[4]);
 
+/* ---- synthetic instances: CPU mirror of csrc/synth.hip (inputs, not reference) ---- */
+void or_synth_random_fr(uint64_t *d, uint64_t n, uint64_t seed);
+void or_synth_circuit(uint64_t *const w[4], uint64_t *const sel[9], uint64_t *const sigma[4],
+                      uint64_t n, uint64_t ng, uint64_t pi_pos, const uint64_t pi_canon[4]);
+void or_synth_coset_consts(uint64_t *vh, uint64_t *x, uint32_t lg);
+
 /* threads used by the OpenMP loops (for cpu_baseline.cores) */
 int or_num_threads(void);
 

@@ -135,6 +135,8 @@ def test_constants():
     assert (QINV * Q) % 2**29 == 2**29 - 1
     assert val(C["F29_ONE"]) == R406 % Q
     assert val(C["F29_C384"]) == 2**384 % Q and val(C["F29_C428"]) == 2**428 % Q
+    # zero29 (msm.hip) tests ZZ = 0 mod q against 0, q and 2q limb for limb
+    assert val(C["F29_Q2"]) == 2 * Q and all(x <= M29 for x in C["F29_Q2"])
     for k, lo in (("F29_KA", 386), ("F29_KB", 389)):
         v = val(C[k])
         assert v % Q == 0 and 2**lo <= v < 2**(lo + 1)
@@ -241,15 +243,23 @@ def xadd29(p, q):
     KA, KB = C["F29_KA"], C["F29_KB"]
     X1, Y1, ZZ1, ZZZ1 = p
     X2, Y2, ZZ2, ZZZ2 = q
+    for v in (X1, Y1, X2, Y2):  # stored coordinates (same bounds as madd29)
+        assert val(v) < 2**389
+    for v in (ZZ1, ZZZ1, ZZ2, ZZZ2):  # product outputs
+        assert val(v) < 2**382
     u1, u2 = mul29(X1, ZZ2), mul29(X2, ZZ1)
     s1, s2 = mul29(Y1, ZZZ2), mul29(Y2, ZZZ1)
     P, R = sub29(u2, u1, KB), sub29(s2, s1, KB)
+    assert val(P) < 2**391 and val(R) < 2**391  # product inputs
     pp = sqr29(P)
     ppp = mul29(P, pp)
     q_ = mul29(u1, pp)
     x3 = sub29(sub29(sub29(sqr29(R), ppp, KA), q_, KA), q_, KA)
     assert val(x3) < 2**389
-    y3 = mul2_29(R, sub29(q_, x3, KB), s1, sub29([0] * 14, ppp, KA))
+    t = sub29(q_, x3, KB)
+    assert val(t) < 2**391
+    y3 = mul2_29(R, t, s1, sub29([0] * 14, ppp, KA))
+    assert val(y3) < 2**382
     return x3, y3, mul29(mul29(ZZ1, ZZ2), pp), mul29(mul29(ZZZ1, ZZZ2), ppp)
 
 
@@ -257,15 +267,22 @@ def xdbl29(p):
     """dbl-2008-s-1 (a = 0) on an XYZZ input."""
     KA, KB = C["F29_KA"], C["F29_KB"]
     X, Y, ZZ, ZZZ = p
+    assert val(X) < 2**389 and val(Y) < 2**389
+    assert val(ZZ) < 2**382 and val(ZZZ) < 2**382
     U = add29n(Y, Y)
+    assert val(U) < 2**391
     V = sqr29(U)
     W = mul29(U, V)
     S = mul29(X, V)
     xx = sqr29(X)
     M = add29n(add29n(xx, xx), xx)
+    assert val(M) < 2**391
     x3 = sub29(sub29(sqr29(M), S, KA), S, KA)
     assert val(x3) < 2**389
-    y3 = mul2_29(M, sub29(S, x3, KB), W, sub29([0] * 14, Y, KB))
+    t, ny = sub29(S, x3, KB), sub29([0] * 14, Y, KB)
+    assert val(t) < 2**391 and val(ny) < 2**391
+    y3 = mul2_29(M, t, W, ny)
+    assert val(y3) < 2**382
     return x3, y3, mul29(V, ZZ), mul29(W, ZZZ)
 
 
@@ -301,3 +318,22 @@ def test_xadd_xdbl():
     assert _aff(xdbl29(A)) == _dbl_aff(a)
     assert _aff(xadd29(AB, A)) == aff_add(aff_add(a, b), a)
     assert _aff(xdbl29(AB)) == _dbl_aff(aff_add(a, b))
+
+
+@pytest.mark.parametrize("seed", [11, 12])
+def test_xadd_xdbl_chain(seed):
+    """Long random mixes of general additions and doublings (the bucket
+    reduction's operation mix), every bound asserted at every step."""
+    rnd = random.Random(seed)
+    pts = [_mulg(rnd.randrange(1, 2**64)) for _ in range(6)]
+    X = [(to_m(x), to_m(y), to_m(1), to_m(1)) for x, y in pts]
+    ref = list(pts)
+    for _ in range(40):
+        i, j = rnd.randrange(len(X)), rnd.randrange(len(X))
+        if i == j or rnd.random() < 0.3:
+            X[i] = xdbl29(X[i])
+            ref[i] = _dbl_aff(ref[i])
+        else:
+            X[i] = xadd29(X[i], X[j])
+            ref[i] = aff_add(ref[i], ref[j])
+        assert _aff(X[i]) == ref[i]

@@ -127,6 +127,31 @@ def test_msm_folded_wide_windows(c, monkeypatch):
         ctx.close()
 
 
+def test_msm_folded_multi_tile_bins(monkeypatch):
+    """Buckets far larger than one k_fine_sort LDS tile (TILE_F = 8192
+    entries) and than one accumulate lane's segment: every scalar is one of
+    three values, so each window sends ~n/3 = 10000 entries to ONE bucket
+    (coarse bin): the multi-tile cursor path of the fine sort and the
+    many-piece merge run (at 2^22 each bin holds ~100K entries)."""
+    import pnp
+    monkeypatch.setenv("PNP_FOLD_C", "20")
+    ctx = pnp.Context(0)
+    try:
+        n = 30000
+        rng = np.random.default_rng(77)
+        lib = oracle()
+        tau = rand_fr_mont_arr(rng, 1)
+        pts = np.zeros((n, 12), dtype=np.uint64)
+        lib.or_srs(vp(pts), n, vp(tau))
+        vals = rand_fr_mont_arr(rng, 3)
+        sc = np.ascontiguousarray(vals[rng.integers(0, 3, size=n)])
+        exp = np.zeros(12, dtype=np.uint64)
+        lib.or_commit(vp(pts), vp(sc), n, vp(exp))
+        assert (_commit_ck(ctx, pts, sc) == exp).all()
+    finally:
+        ctx.close()
+
+
 def test_msm_edge_cases(ctx):
     lib = oracle()
     rng = np.random.default_rng(5)

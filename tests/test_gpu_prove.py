@@ -3,7 +3,7 @@ byte on the 2656-byte ProofC, through both the v1 symbol (host inputs, exactly
 as the Rust FFI calls it) and the v2 resident-key API."""
 import pytest
 
-from pnp_testlib import Inputs
+from pnp_testlib import Inputs, inputs_pis, inputs_vk, verify
 from pnp import abi
 
 pytestmark = pytest.mark.gpu
@@ -33,6 +33,8 @@ def test_gen_proof_v1_parity(lg, seed):
     got = lib.gen_proof(inp.circuit, inp.pk, inp.ck)
     assert _diff(got, exp) == []
     assert abi.proof_to_bytes(got) == abi.proof_to_bytes(exp)
+    # and the GPU proof is accepted by the restated reference verifier
+    assert verify(inputs_vk(inp), got, inputs_pis(inp), inp.tau_mont[0])
 
 
 @pytest.mark.parametrize("lookup_rows,extra", [(0, True), (17, False), (40, True)])

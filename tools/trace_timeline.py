@@ -1,26 +1,25 @@
 """Per-proof kernel timeline from a rocprofv3 kernel_trace.csv of a bench run:
     python tools/trace_timeline.py run_kernel_trace.csv [proof_index]
-A proof ends with its second MSM after the quotient (round-4 chunk commits,
-then the round-6 opening witnesses), i.e. at the second k_tree_roots after its
-k_quotient_; the next proof starts with the following kernel.  Prints the
-kernel totals and the GPU idle gaps (host time) of the chosen proof (default:
-the last complete one)."""
+Every proof starts with the marker kernel k_proof_begin (csrc/protocol.hip);
+a proof spans from its marker to the last kernel before the next marker (the
+last proof: to the last kernel of the trace), so setup work before the first
+marker (table build, synthetic inputs) is never counted.  Prints the kernel
+totals and the GPU idle gaps (host time) of the chosen proof (default: the
+last complete one)."""
 import csv
 import sys
 from collections import defaultdict
 
 rows = list(csv.DictReader(open(sys.argv[1])))
 ev = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]) for r in rows)
-qi = [i for i, e in enumerate(ev) if e[2].startswith("pnp::k_quotient_")]
-ends = []
-for q in qi:
-    roots = [i for i in range(q, len(ev)) if ev[i][2].startswith("pnp::k_tree_roots")]
-    if len(roots) >= 2:
-        ends.append(roots[1])
-which = int(sys.argv[2]) if len(sys.argv) > 2 else len(ends) - 1
-end = ends[which]
-start = ends[which - 1] + 1 if which > 0 else 0
-seg = ev[start:end + 1]
+marks = [i for i, e in enumerate(ev) if "k_proof_begin" in e[2]]
+if not marks:
+    sys.exit("no k_proof_begin markers in the trace (library older than round 2?)")
+bounds = [(m, (marks[k + 1] if k + 1 < len(marks) else len(ev))) for k, m in enumerate(marks)]
+# the last proof may be cut off by the end of the trace: default to the one before
+which = int(sys.argv[2]) if len(sys.argv) > 2 else max(0, len(bounds) - 2)
+start, stop = bounds[which]
+seg = ev[start:stop]
 t0, t1 = seg[0][0], seg[-1][1]
 tot = defaultdict(lambda: [0, 0])
 gaps, last_end = [], t0

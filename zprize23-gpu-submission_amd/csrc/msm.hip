@@ -89,18 +89,21 @@ struct KeyRows {
 };
 
 // ---------------------------------------------------------------- 2. coarse pass
-// Two-pass bucket sort.  Pass A sorts the entries by the top CB bits of the
-// bucket (NBc <= 128 coarse bins), pass B sorts each coarse bin (~2^19 entries
-// of a 2^22 MSM) by the remaining FB bits in one workgroup.  Few bins keep the
-// write fronts few; pass A also counting-sorts 4096-key tiles in LDS so each
-// bin's entries leave as one run (a one-pass scatter straight to 2^15 buckets
-// wrote ~8x its payload to HBM).  Keys, fine keys and entries are read four
-// per lane (8 / 4 / 16-byte loads).
+// Two-pass bucket sort.  Pass A sorts the entries by the top CB = 9 bits of
+// the bucket (NBc = 512 coarse bins), pass B sorts each coarse bin by the
+// remaining FB bits in one workgroup (folded c = 20 at 2^22: 2^19 buckets =
+// 512 bins x 1024 fine bins, ~13 x 2^22 / 512 = 106K entries per coarse bin,
+// ~104 per bucket).  Few bins keep the write fronts few; pass A also
+// counting-sorts 4096-key tiles in LDS so each bin's entries leave as one run
+// (a one-pass scatter straight to 2^15 buckets wrote ~8x its payload to HBM).
+// Keys, fine keys and entries are read four per lane (8 / 4 / 16-byte loads).
 #ifndef PNP_SORT_CB
 #define PNP_SORT_CB 9
 #endif
 constexpr int SORT_CB = PNP_SORT_CB;
 constexpr int SORT_FB_MAX = 11;
+// three 2^CB-entry u32 LDS arrays + the 2 x 16 KiB tile of k_coarse_scatter
+static_assert(SORT_CB >= 1 && SORT_CB <= 12, "PNP_SORT_CB out of range (LDS budget of k_coarse_scatter)");
 __global__ __launch_bounds__(1024) void k_coarse_hist(const uint32_t *keys, KeyRows kr, int fb,
                                                       int NBc, uint64_t chunk, int nch,
                                                       uint32_t *counts) {
@@ -286,11 +289,17 @@ __global__ __launch_bounds__(1024) void k_coarse_scatter(const uint32_t *keys, K
 // pass B: one workgroup per (virtual window, coarse bin) = bucket range
 // [p << fb, (p + 1) << fb); writes every bucket's start and the sorted entries
 // Histogram first (bucket starts), then tiles of 8192 entries counting-sorted
-// in LDS and written out one run per fine bin (~32 entries at 2^22).
+// in LDS and written out one run per fine bin (~8 entries per fine bin and
+// tile at 2^22: 8192 entries over 1024 fine bins; a coarse bin of ~106K
+// entries takes ~13 tiles, the cursor h[] carrying over between them).
 #ifndef PNP_TILE_F
 #define PNP_TILE_F 8192
 #endif
 constexpr int TILE_F = PNP_TILE_F;
+// PER = TILE_F / 1024 entries per lane per tile: a tile must be whole lanes,
+// and st_e / st_f (6 B per entry) plus three 2^11 u32 arrays must fit in LDS
+static_assert(TILE_F % 1024 == 0 && TILE_F >= 1024 && TILE_F <= 16384,
+              "PNP_TILE_F must be a multiple of 1024 in [1024, 16384]");
 __global__ __launch_bounds__(1024) void k_fine_sort(const uint32_t *ent, const uint16_t *fk,
                                                     const uint32_t *coffs, int nch, int fb,
                                                     uint32_t *bstart, uint32_t *sorted) {

@@ -65,5 +65,7 @@ bool k_any_diff(const uint64_t *a, const uint64_t *b, uint64_t words, DevBuf &sc
 void k_affine(uint64_t *out, const uint64_t *in, const Fr &a, const Fr &b, uint64_t n, hipStream_t s);
 void k_quotient(const QuotArgs &q, uint64_t N8, uint64_t *out, hipStream_t s);
 void k_lincomb(const LinArgs &a, uint64_t n, uint64_t *out, hipStream_t s);
+// empty kernel marking the start of a proof in kernel traces
+void k_proof_marker(hipStream_t s);
 
 }  // namespace pnp

@@ -295,3 +295,13 @@ void k_lincomb(const LinArgs &a, uint64_t n, uint64_t *out, hipStream_t s) {
 }
 
 }  // namespace pnp
+
+namespace pnp {
+// one-lane no-op launched first in every proof: a stable boundary for
+// per-proof kernel timelines (tools/trace_timeline.py)
+__global__ void k_proof_begin() {}
+void k_proof_marker(hipStream_t s) {
+    hipLaunchKernelGGL(k_proof_begin, dim3(1), dim3(1), 0, s);
+    PNP_HIP(hipGetLastError());
+}
+}  // namespace pnp

@@ -144,6 +144,7 @@ int prove_impl(pnp_ctx *ctx, const CircuitC *cs, int device_ptrs, ProofC *out) {
     const ProverKeyC &pk = ctx->pk_dev;
     Timer tm(ctx);
     auto &nt = ctx->ntt;
+    k_proof_marker(s);
 
     // ---------------- inputs: padded witness evaluations (pad_poly)
     uint64_t *wsc[4], *wpoly[4];
