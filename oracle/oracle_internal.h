@@ -41,4 +41,17 @@ void or_g1j_add_affine(or_g1j *r, const or_g1j *p, const uint64_t aff[12]);
 void or_g1j_to_affine(uint64_t aff[12], const or_g1j *p);
 void or_g1_msm(or_g1j *r, const uint64_t *points, const uint64_t *scalars_canon, uint64_t n);
 
+/* custom-gate constraints (widgets.c): wire values a..d, the next-row values
+ * and the q_l / q_r / q_c selector values at one point */
+typedef struct {
+    const uint64_t *a, *b, *c, *d;
+    const uint64_t *a_next, *b_next, *d_next, *q_l, *q_r, *q_c;
+} widget_vals;
+void or_w_range(uint64_t out[4], const uint64_t sep[4], const widget_vals *w);
+void or_w_logic(uint64_t out[4], const uint64_t sep[4], const widget_vals *w);
+void or_w_fbsm(uint64_t out[4], const uint64_t sep[4], const widget_vals *w);
+uint64_t *or_lookup_z2(uint32_t lg, const uint64_t *f, const uint64_t *t, const uint64_t *h1,
+                       const uint64_t *h2, const uint64_t delta[4], const uint64_t eps[4]);
+void or_w_cadd(uint64_t out[4], const uint64_t sep[4], const widget_vals *w);
+
 #endif

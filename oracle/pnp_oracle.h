@@ -84,6 +84,13 @@ void or_keccak_f1600(uint64_t st[25]);
 
 /* ---- full prover: gen_proof.cuh:10-489 ---- */
 int or_gen_proof(const CircuitC *cs, const ProverKeyC *pk, const CommitKeyC *ck, ProofC *out);
+/* prover.rs semantics with n_pi public inputs (positions, canonical values;
+ * any order, zeros dropped) and a transcript label */
+int or_gen_proof_ex(const CircuitC *cs, const ProverKeyC *pk, const CommitKeyC *ck, uint64_t n_pi,
+                    const uint64_t *pi_pos, const uint64_t *pi_canon, const char *label, ProofC *out);
+/* plookup: MultiSet::combine_split (multiset.rs:131) of t (n) and f (n) into
+ * h1, h2 (n each); PNP_E_ARG when a value of f is not in t */
+int or_combine_split(const uint64_t *t, const uint64_t *f, uint64_t n, uint64_t *h1, uint64_t *h2);
 
 /* ---- verifier: proof.rs:123-431 (Proof::verify), circuit.rs:325-344 ---- */
 /* commitments to the preprocessed polynomials, affine Montgomery, infinity

@@ -1,23 +1,26 @@
 /*
- * oracle/prover.c — CPU restatement of the reference gen_proof
- * (lib/hello.cu:4-6 -> lib/PLONK/src/gen_proof.cuh:10-489).
+ * oracle/prover.c — CPU restatement of gen_proof.
  * TEST INFRASTRUCTURE ONLY (see pnp_oracle.h).
  *
- * Follows the CUDA path's protocol order and formulas line by line, including
- * its circuit-class shortcuts (SURVEY.md §8a "parity envelope"):
- *   - transcript label "Merkle tree" (gen_proof.cuh:19-22);
- *   - combine_split skipped, h1 = h2 = 0 (gen_proof.cuh:107-119);
- *   - q_m / custom-selector / q_lookup coeffs treated as empty polynomials
- *     (gen_proof.cuh:277, 319-329), so their linearisation terms vanish;
- *   - one public input (transcript.cuh:39-44);
- *   - t_next / h1_next built with the reference's 8-byte shift
- *     (permutation/mod.cu:121-128);
- *   - linearisation lookup term uses (delta + h1_next_eval)
- *     (widget/lookup.cu:188) — only ever multiplied by h1_poly = 0.
- * The range / logic / fixed-base / variable-base quotient widgets
- * (widget/{range,logic,fixed_base_scalar_mul,curve_addition}.cu) multiply
- * their selector evaluations; this restatement requires those selectors to be
- * zero (as in the Merkle circuit) and returns PNP_E_ENVELOPE otherwise.
+ * Semantics: the ZK-Garage CPU prover Prover::prove_with_preprocessed
+ * (plonk-core/src/proof_system/prover.rs:171-660, quotient_poly.rs,
+ * linearisation_poly.rs, the widget sources, permutation/mod.rs:629-822), which the
+ * north star names as the parity target, in the protocol order of the GPU
+ * path it replaces (lib/PLONK/src/gen_proof.cuh:10-489).  On the reference's
+ * own circuit class (the Merkle circuit: no custom gates, no lookup tables,
+ * one public input) the two reference paths coincide, and so does this
+ * restatement.  Outside it the GPU path takes shortcuts that make its proofs
+ * fail verification (combine_split skipped, q_m / custom-
+ * selector / q_lookup coefficients treated as empty, the 8-byte t_next /
+ * h1_next shift, "delta + h1_next" in the linearisation); this restatement
+ * follows prover.rs there:
+ *   - h1, h2 from combine_split (lookup.c);
+ *   - z2 with t_next[i] = t[i+1], h1_next[i] = h1[i+1];
+ *   - custom-gate widgets in the quotient AND the linearisation; q_m and
+ *     q_lookup coefficients read whenever their evaluations are non-zero;
+ *   - any number of public inputs (BTreeMap order, zeros dropped).
+ * The transcript label is the caller's ("Merkle tree" for the v1 symbol,
+ * gen_proof.cuh:19-22).
  */
 #include "oracle_internal.h"
 #include <stdio.h>
@@ -143,53 +146,6 @@ static uint64_t *permutation_poly(uint32_t lg, uint64_t *const w[4], const uint6
     return num;
 }
 
-/* the reference's 8-byte shift (permutation/mod.cu:121-128), on u64 words */
-static uint64_t *shift8(const uint64_t *v, uint64_t n) {
-    uint64_t words = 4 * n;
-    uint64_t *r = vec_alloc(n);
-    memcpy(r, v + 1, 8 * (words - 1));
-    r[words - 1] = v[0];
-    return r;
-}
-
-/* compute_lookup_permutation_poly (permutation/mod.cu:111-144) + _lookup_ratio (:18-42) */
-static uint64_t *lookup_perm_poly(uint32_t lg, const uint64_t *f, const uint64_t *t,
-                                  const uint64_t *h1, const uint64_t *h2,
-                                  const uint64_t delta[4], const uint64_t eps[4]) {
-    uint64_t n = 1ULL << lg;
-    uint64_t *tn = shift8(t, n), *h1n = shift8(h1, n);
-    uint64_t opd[4], eopd[4];
-    or_fr_add(opd, delta, OR_FR_ONE);
-    or_fr_mul(eopd, eps, opd);
-    uint64_t *num = vec_alloc(n), *den = vec_alloc(n);
-#pragma omp parallel for schedule(static)
-    for (int64_t i = 0; i < (int64_t)n; i++) {
-        uint64_t m1[4], m2[4], m3[4], r[4], m6[4], m7[4], m8[4], m9[4], m10[4];
-        or_fr_add(m1, eps, E4(f, i));
-        or_fr_add(m2, eopd, E4(t, i));
-        or_fr_mul(m3, delta, E4(tn, i));
-        or_fr_add(m2, m2, m3);
-        or_fr_mul(m1, opd, m1);
-        or_fr_mul(r, m2, m1);
-        or_fr_mul(m6, E4(h2, i), delta);
-        or_fr_add(m7, eopd, E4(h1, i));
-        or_fr_add(m8, m6, m7);
-        or_fr_add(m9, eopd, E4(h2, i));
-        or_fr_mul(m10, E4(h1n, i), delta);
-        or_fr_add(m9, m9, m10);
-        or_fr_mul(m8, m8, m9);
-        fr_copy(E4(num, i), r);
-        fr_copy(E4(den, i), m8);
-    }
-    or_batch_inverse(den, n);
-#pragma omp parallel for schedule(static)
-    for (int64_t i = 0; i < (int64_t)n; i++) or_fr_mul(E4(num, i), E4(num, i), E4(den, i));
-    or_prefix_product(num, n);
-    or_ntt(num, lg, 1, 0);
-    free(tn); free(h1n); free(den);
-    return num;
-}
-
 static void fr_pow5(uint64_t r[4], const uint64_t a[4]) {
     uint64_t a2[4], a4[4];
     or_fr_mul(a2, a, a);
@@ -202,8 +158,14 @@ typedef struct {
     uint64_t range[4], logic[4], fixed[4], var[4], lsep[4];
 } challenges_t;
 
+/* selectors whose 8n evaluations are non-zero (the others are the zero
+ * polynomial: their Rust coefficient Vecs are empty and never read) */
+typedef struct {
+    int q_m, range, logic, fixed, var, q_lookup;
+} nz_t;
+
 /* compute_quotient_poly (proof_system/quotient.cu:142-376) */
-static uint64_t *quotient_poly(uint32_t lg, const ProverKeyC *pk, const challenges_t *ch,
+static uint64_t *quotient_poly(uint32_t lg, const ProverKeyC *pk, const challenges_t *ch, const nz_t *nz,
                                const uint64_t *z_poly, const uint64_t *z2_poly,
                                uint64_t *const wpoly[4], const uint64_t *pi_poly,
                                const uint64_t *f_poly, const uint64_t *table_poly,
@@ -254,7 +216,32 @@ static uint64_t *quotient_poly(uint32_t lg, const ProverKeyC *pk, const challeng
         fr_pow5(t, d); or_fr_mul(t, t, E4(pk->q_h4_evals, i)); or_fr_add(acc, acc, t);
         or_fr_add(acc, acc, E4(pk->q_c_evals, i));
         or_fr_mul(g, acc, E4(pk->q_arith_evals, i));
-        or_fr_add(g, g, E4(pi8, i));  /* + pi_eval_8n (quotient.cu:76-77) */
+        or_fr_add(g, g, E4(pi8, i));  /* + pi_eval_8n (quotient_poly.rs:240) */
+        /* custom gates (quotient_poly.rs:253-296): selector * constraints */
+        if (nz->range || nz->logic || nz->fixed || nz->var) {
+            widget_vals wv = {a, b, c, d, E4(w8[0], nx), E4(w8[1], nx), E4(w8[3], nx),
+                              E4(pk->q_l_evals, i), E4(pk->q_r_evals, i), E4(pk->q_c_evals, i)};
+            if (nz->range) {
+                or_w_range(t, ch->range, &wv);
+                or_fr_mul(t, t, E4(pk->range_selector_evals, i));
+                or_fr_add(g, g, t);
+            }
+            if (nz->logic) {
+                or_w_logic(t, ch->logic, &wv);
+                or_fr_mul(t, t, E4(pk->logic_selector_evals, i));
+                or_fr_add(g, g, t);
+            }
+            if (nz->fixed) {
+                or_w_fbsm(t, ch->fixed, &wv);
+                or_fr_mul(t, t, E4(pk->fixed_group_add_selector_evals, i));
+                or_fr_add(g, g, t);
+            }
+            if (nz->var) {
+                or_w_cadd(t, ch->var, &wv);
+                or_fr_mul(t, t, E4(pk->variable_group_add_selector_evals, i));
+                or_fr_add(g, g, t);
+            }
+        }
         /* permutation_compute_quotient (proof_system/permutation.cu:267-296) */
         const uint64_t *x = E4(pk->linear_evaluations, i);
         uint64_t pa[4], pb[4], pc[4];
@@ -333,22 +320,49 @@ static uint64_t *quotient_poly(uint32_t lg, const ProverKeyC *pk, const challeng
     return num;
 }
 
-int or_gen_proof(const CircuitC *cs, const ProverKeyC *pk, const CommitKeyC *ck, ProofC *out) {
+/* (pos, value) pairs in BTreeMap order; duplicate positions are an error
+ * (PublicInputs::insert panics, pi.rs:33-38) */
+typedef struct {
+    uint64_t pos, v[4];
+} pi_t;
+static int pi_cmp(const void *a, const void *b) {
+    uint64_t x = ((const pi_t *)a)->pos, y = ((const pi_t *)b)->pos;
+    return x < y ? -1 : x > y;
+}
+
+static int gen_proof_impl(const CircuitC *cs, const ProverKeyC *pk, const CommitKeyC *ck,
+                          uint64_t n_pi, const uint64_t *pi_pos, const uint64_t *pi_canon,
+                          const char *label, int v1, ProofC *out) {
     memset(out, 0, sizeof(*out));
     uint64_t n = next_pow2(cs->n > cs->lookup_len ? cs->n : cs->lookup_len);
     uint32_t lg = lg2(n);
     uint64_t N8 = 8 * n;
-    /* envelope: custom-gate selectors must be zero (see file header) */
-    if (!all_zero(pk->range_selector_evals, N8) || !all_zero(pk->logic_selector_evals, N8) ||
-        !all_zero(pk->fixed_group_add_selector_evals, N8) ||
-        !all_zero(pk->variable_group_add_selector_evals, N8))
-        return PNP_E_ENVELOPE;
+    pi_t *pis = (pi_t *)calloc(n_pi ? n_pi : 1, sizeof(pi_t));
+    for (uint64_t k = 0; k < n_pi; k++) {
+        pis[k].pos = pi_pos[k];
+        memcpy(pis[k].v, pi_canon + 4 * k, 32);
+        if (pi_pos[k] >= n) { free(pis); return PNP_E_ARG; }
+    }
+    qsort(pis, n_pi, sizeof(pi_t), pi_cmp);
+    for (uint64_t k = 1; k < n_pi; k++)
+        if (pis[k].pos == pis[k - 1].pos) { free(pis); return PNP_E_ARG; }
+    nz_t nz = {!all_zero(pk->q_m_evals, N8), !all_zero(pk->range_selector_evals, N8),
+               !all_zero(pk->logic_selector_evals, N8),
+               !all_zero(pk->fixed_group_add_selector_evals, N8),
+               !all_zero(pk->variable_group_add_selector_evals, N8), !all_zero(pk->q_lookup_evals, N8)};
 
     challenges_t ch;
-    or_transcript *tr = or_transcript_new("Merkle tree");
-    or_transcript_append_pi(tr, "pi", cs->pi, cs->intended_pi_pos);
+    or_transcript *tr = or_transcript_new(label);
+    if (v1) {
+        or_transcript_append_pi(tr, "pi", cs->pi, cs->intended_pi_pos);
+    } else {
+        uint64_t *pp = (uint64_t *)calloc(n_pi ? n_pi : 1, 8), *pv = vec_alloc(n_pi);
+        for (uint64_t k = 0; k < n_pi; k++) { pp[k] = pis[k].pos; fr_copy(E4(pv, k), pis[k].v); }
+        or_transcript_append_pis(tr, "pi", n_pi, pp, pv);
+        free(pp); free(pv);
+    }
 
-    /* 1. witness polynomials (gen_proof.cuh:25-50) */
+    /* 1. witness polynomials (prover.rs:192-228) */
     uint64_t *wsc[4], *wpoly[4];
     const uint64_t *wsrc[4] = {cs->w_l, cs->w_r, cs->w_o, cs->w_4};
     for (int j = 0; j < 4; j++) {
@@ -360,7 +374,7 @@ int or_gen_proof(const CircuitC *cs, const ProverKeyC *pk, const CommitKeyC *ck,
     for (int j = 0; j < 4; j++) commit_aff(ck, wpoly[j], n, wc[j]);
     for (int j = 0; j < 4; j++) append_comm(tr, wl[j], wc[j]);
 
-    /* 2. lookup polynomials (gen_proof.cuh:52-125) */
+    /* 2. lookup polynomials (prover.rs:230-329) */
     or_transcript_challenge_scalar(tr, "zeta", ch.zeta);
     or_transcript_append_scalar(tr, "zeta", ch.zeta);
     uint64_t *tc = vec_alloc(n);
@@ -369,7 +383,7 @@ int or_gen_proof(const CircuitC *cs, const ProverKeyC *pk, const CommitKeyC *ck,
     uint64_t *qlk = pad(cs->q_lookup, cs->n, n);
     uint64_t *fs[4];
     for (int j = 0; j < 4; j++) fs[j] = vec_alloc(n);
-    for (uint64_t i = 0; i < n; i++) {  /* compute_query_table_poly */
+    for (uint64_t i = 0; i < n; i++) {  /* query table: prover.rs:264-283 */
         if (or_fr_is_zero(E4(qlk, i))) {
             fr_copy(E4(fs[0], i), tc);
         } else {
@@ -382,13 +396,20 @@ int or_gen_proof(const CircuitC *cs, const ProverKeyC *pk, const CommitKeyC *ck,
     commit_aff(ck, f_poly, n, &out->f_comm);
     append_comm(tr, "f", &out->f_comm);
     uint64_t *h1 = vec_alloc(n), *h2 = vec_alloc(n);
+    int rc = or_combine_split(tc, fc, n, h1, h2);  /* prover.rs:305-307 */
+    if (rc != PNP_OK) {
+        or_transcript_free(tr);
+        for (int j = 0; j < 4; j++) { free(wsc[j]); free(wpoly[j]); free(fs[j]); }
+        free(tc); free(table_poly); free(qlk); free(fc); free(f_poly); free(h1); free(h2); free(pis);
+        return rc;
+    }
     uint64_t *h1_poly = intt_copy(h1, lg), *h2_poly = intt_copy(h2, lg);
     commit_aff(ck, h1_poly, n, &out->h_1_comm);
     commit_aff(ck, h2_poly, n, &out->h_2_comm);
     append_comm(tr, "h1", &out->h_1_comm);
     append_comm(tr, "h2", &out->h_2_comm);
 
-    /* 3. permutation polynomials (gen_proof.cuh:127-208) */
+    /* 3. permutation polynomials (prover.rs:331-400) */
     or_transcript_challenge_scalar(tr, "beta", ch.beta);
     or_transcript_append_scalar(tr, "beta", ch.beta);
     or_transcript_challenge_scalar(tr, "gamma", ch.gamma);
@@ -402,14 +423,18 @@ int or_gen_proof(const CircuitC *cs, const ProverKeyC *pk, const CommitKeyC *ck,
     uint64_t *z_poly = permutation_poly(lg, wsc, ch.beta, ch.gamma, sigc);
     commit_aff(ck, z_poly, n, &out->z_comm);
     append_comm(tr, "z", &out->z_comm);
-    uint64_t *z2_poly = lookup_perm_poly(lg, fc, tc, h1, h2, ch.delta, ch.eps);
-    commit_aff(ck, z2_poly, n, &out->z_2_comm);  /* not appended (gen_proof.cuh:200-205) */
-    /* pi poly (pi.cu:11-15) */
+    uint64_t *z2_poly = or_lookup_z2(lg, fc, tc, h1, h2, ch.delta, ch.eps);
+    commit_aff(ck, z2_poly, n, &out->z_2_comm);  /* not appended (prover.rs:394-397) */
+    /* pi poly (pi.rs:76-86) */
     uint64_t *pie = vec_alloc(n);
-    or_fr_to_mont(E4(pie, cs->intended_pi_pos), cs->pi);
+    if (v1) {
+        or_fr_to_mont(E4(pie, cs->intended_pi_pos), cs->pi);
+    } else {
+        for (uint64_t k = 0; k < n_pi; k++) or_fr_to_mont(E4(pie, pis[k].pos), pis[k].v);
+    }
     uint64_t *pi_poly = intt_copy(pie, lg);
 
-    /* 4. quotient (gen_proof.cuh:209-267) */
+    /* 4. quotient (prover.rs:402-489) */
     or_transcript_challenge_scalar(tr, "alpha", ch.alpha);
     or_transcript_append_scalar(tr, "alpha", ch.alpha);
     or_transcript_challenge_scalar(tr, "range separation challenge", ch.range);
@@ -422,7 +447,7 @@ int or_gen_proof(const CircuitC *cs, const ProverKeyC *pk, const CommitKeyC *ck,
     or_transcript_append_scalar(tr, "variable base separation challenge", ch.var);
     or_transcript_challenge_scalar(tr, "lookup separation challenge", ch.lsep);
     or_transcript_append_scalar(tr, "lookup separation challenge", ch.lsep);
-    uint64_t *t_poly = quotient_poly(lg, pk, &ch, z_poly, z2_poly, wpoly, pi_poly, f_poly,
+    uint64_t *t_poly = quotient_poly(lg, pk, &ch, &nz, z_poly, z2_poly, wpoly, pi_poly, f_poly,
                                      table_poly, h1_poly, h2_poly);
     CommitmentC *tcm[8] = {&out->t_1_comm, &out->t_2_comm, &out->t_3_comm, &out->t_4_comm,
                            &out->t_5_comm, &out->t_6_comm, &out->t_7_comm, &out->t_8_comm};
@@ -433,7 +458,7 @@ int or_gen_proof(const CircuitC *cs, const ProverKeyC *pk, const CommitKeyC *ck,
         append_comm(tr, lab, tcm[k]);
     }
 
-    /* 5. linearisation (linearisation.cu:73-306) */
+    /* 5. linearisation (linearisation_poly.rs:123-360) */
     uint64_t zc[4];
     or_transcript_challenge_scalar(tr, "z", zc);
     or_transcript_append_scalar(tr, "z", zc);
@@ -459,7 +484,8 @@ int or_gen_proof(const CircuitC *cs, const ProverKeyC *pk, const CommitKeyC *ck,
     or_poly_eval(z_poly, n, zw, ev->perm_evals.permutation_eval);
     CustomEvaluationsC *cu = &ev->custom_evals;
     or_poly_eval(pk->q_arith_coeffs, n, zc, cu->q_arith_eval);
-    memset(ev->lookup_evals.q_lookup_eval, 0, 32);  /* q_lookup coeffs empty */
+    LookupEvaluationsC *lk = &ev->lookup_evals;
+    if (nz.q_lookup) or_poly_eval(pk->q_lookup_coeffs, n, zc, lk->q_lookup_eval);
     or_poly_eval(pk->q_c_coeffs, n, zc, cu->q_c_eval);
     or_poly_eval(pk->q_l_coeffs, n, zc, cu->q_l_eval);
     or_poly_eval(pk->q_r_coeffs, n, zc, cu->q_r_eval);
@@ -469,7 +495,6 @@ int or_gen_proof(const CircuitC *cs, const ProverKeyC *pk, const CommitKeyC *ck,
     or_poly_eval(pk->q_hl_coeffs, n, zc, cu->q_hl_eval);
     or_poly_eval(pk->q_hr_coeffs, n, zc, cu->q_hr_eval);
     or_poly_eval(pk->q_h4_coeffs, n, zc, cu->q_h4_eval);
-    LookupEvaluationsC *lk = &ev->lookup_evals;
     or_poly_eval(z2_poly, n, zw, lk->z2_next_eval);
     or_poly_eval(h1_poly, n, zc, lk->h1_eval);
     or_poly_eval(h1_poly, n, zw, lk->h1_next_eval);
@@ -480,20 +505,32 @@ int or_gen_proof(const CircuitC *cs, const ProverKeyC *pk, const CommitKeyC *ck,
 
     const uint64_t *ae = ev->wire_evals.a_eval, *be = ev->wire_evals.b_eval,
                    *ce = ev->wire_evals.c_eval, *de = ev->wire_evals.d_eval;
-    /* scalar coefficients s_k of r(X) = sum s_k P_k(X) */
-    uint64_t s_ql[4], s_qr[4], s_qo[4], s_q4[4], s_qhl[4], s_qhr[4], s_qh4[4], s_qc[4];
-    uint64_t s_z[4], s_s4[4], s_z2[4], s_h1[4], s_t[8][4], tmp[4], tmp2[4];
-    /* compute_linearisation_arithmetic (widget/arithmetic.cu:47-80) */
+    /* r(X) = sum_k S[k] P[k](X) */
+    const uint64_t *P[32];
+    uint64_t S[32][4], tmp[4], tmp2[4];
+    int K = 0;
+#define TERM(poly) (P[K] = (poly), S[K++])
+    /* arithmetic (widget/arithmetic.rs:82-100) */
     const uint64_t *qae = cu->q_arith_eval;
-    or_fr_mul(s_ql, ae, qae);
-    or_fr_mul(s_qr, be, qae);
-    or_fr_mul(s_qo, ce, qae);
-    or_fr_mul(s_q4, de, qae);
-    fr_pow5(tmp, ae); or_fr_mul(s_qhl, tmp, qae);
-    fr_pow5(tmp, be); or_fr_mul(s_qhr, tmp, qae);
-    fr_pow5(tmp, de); or_fr_mul(s_qh4, tmp, qae);
-    fr_copy(s_qc, qae);
-    /* compute_linearisation_permutation (proof_system/permutation.cu:231-265) */
+    if (nz.q_m) { or_fr_mul(tmp, ae, be); or_fr_mul(TERM(pk->q_m_coeffs), tmp, qae); }
+    or_fr_mul(TERM(pk->q_l_coeffs), ae, qae);
+    or_fr_mul(TERM(pk->q_r_coeffs), be, qae);
+    or_fr_mul(TERM(pk->q_o_coeffs), ce, qae);
+    or_fr_mul(TERM(pk->q_4_coeffs), de, qae);
+    fr_pow5(tmp, ae); or_fr_mul(TERM(pk->q_hl_coeffs), tmp, qae);
+    fr_pow5(tmp, be); or_fr_mul(TERM(pk->q_hr_coeffs), tmp, qae);
+    fr_pow5(tmp, de); or_fr_mul(TERM(pk->q_h4_coeffs), tmp, qae);
+    fr_copy(TERM(pk->q_c_coeffs), qae);
+    /* custom gates (linearisation_poly.rs:396-430): selector * constraints(evals) */
+    {
+        widget_vals wv = {ae, be, ce, de, cu->a_next_eval, cu->b_next_eval, cu->d_next_eval,
+                          cu->q_l_eval, cu->q_r_eval, cu->q_c_eval};
+        if (nz.range) or_w_range(TERM(pk->range_selector_coeffs), ch.range, &wv);
+        if (nz.logic) or_w_logic(TERM(pk->logic_selector_coeffs), ch.logic, &wv);
+        if (nz.fixed) or_w_fbsm(TERM(pk->fixed_group_add_selector_coeffs), ch.fixed, &wv);
+        if (nz.var) or_w_cadd(TERM(pk->variable_group_add_selector_coeffs), ch.var, &wv);
+    }
+    /* permutation (proof_system/permutation.rs compute_linearisation) */
     {
         uint64_t bz[4], acc[4], ks[4];
         or_fr_mul(bz, ch.beta, zc);
@@ -511,7 +548,7 @@ int or_gen_proof(const CircuitC *cs, const ProverKeyC *pk, const CommitKeyC *ck,
         uint64_t a2[4], l1z[4];
         or_fr_mul(a2, ch.alpha, ch.alpha);
         or_fr_mul(l1z, l1e, a2);         /* check_is_one: l_1(z) alpha^2 */
-        or_fr_add(s_z, acc, l1z);
+        or_fr_add(TERM(z_poly), acc, l1z);
         /* copy range check */
         const uint64_t *sv[3] = {ev->perm_evals.left_sigma_eval, ev->perm_evals.right_sigma_eval,
                                  ev->perm_evals.out_sigma_eval};
@@ -526,15 +563,23 @@ int or_gen_proof(const CircuitC *cs, const ProverKeyC *pk, const CommitKeyC *ck,
         or_fr_mul(tmp, ch.beta, ev->perm_evals.permutation_eval);
         or_fr_mul(acc, acc, tmp);
         or_fr_mul(acc, acc, ch.alpha);
-        or_fr_neg(s_s4, acc);
+        or_fr_neg(TERM(pk->fourth_sigma_coeffs), acc);
     }
-    /* compute_linearisation_lookup (widget/lookup.cu:136-199) */
+    /* lookup (widget/lookup.rs:137-182) */
     {
-        uint64_t opd[4], eopd[4], sep2[4], sep3[4], b0[4], b1[4], c0[4], c1[4];
+        uint64_t opd[4], eopd[4], sep2[4], sep3[4], b0[4], b1[4], c1[4];
         or_fr_mul(sep2, ch.lsep, ch.lsep);
         or_fr_mul(sep3, sep2, ch.lsep);
         or_fr_add(opd, ch.delta, OR_FR_ONE);
         or_fr_mul(eopd, ch.eps, opd);
+        if (nz.q_lookup) {  /* a: q_lookup (lc(a, b, c, d; zeta) - f_eval) sep */
+            fr_copy(tmp, de);
+            or_fr_mul(tmp, tmp, ch.zeta); or_fr_add(tmp, tmp, ce);
+            or_fr_mul(tmp, tmp, ch.zeta); or_fr_add(tmp, tmp, be);
+            or_fr_mul(tmp, tmp, ch.zeta); or_fr_add(tmp, tmp, ae);
+            or_fr_sub(tmp, tmp, lk->f_eval);
+            or_fr_mul(TERM(pk->q_lookup_coeffs), tmp, ch.lsep);
+        }
         or_fr_add(b0, ch.eps, lk->f_eval);
         or_fr_add(b1, eopd, lk->table_eval);
         or_fr_mul(tmp, ch.delta, lk->table_next_eval);
@@ -543,43 +588,36 @@ int or_gen_proof(const CircuitC *cs, const ProverKeyC *pk, const CommitKeyC *ck,
         or_fr_mul(tmp2, opd, b0);
         or_fr_mul(tmp2, tmp2, b1);
         or_fr_mul(tmp2, tmp2, sep2);
-        or_fr_add(s_z2, tmp2, tmp);
-        or_fr_neg(c0, lk->z2_next_eval);
-        or_fr_mul(c0, c0, sep2);
+        or_fr_add(TERM(z2_poly), tmp2, tmp);
+        /* c: h1 (-z2_next sep^2)(eps(1+delta) + h2_eval + delta h1_next_eval) */
+        or_fr_neg(tmp, lk->z2_next_eval);
+        or_fr_mul(tmp, tmp, sep2);
         or_fr_add(c1, eopd, lk->h2_eval);
-        or_fr_add(tmp, ch.delta, lk->h1_next_eval);  /* reference: add_mod (lookup.cu:188) */
-        or_fr_add(c1, c1, tmp);
-        or_fr_mul(s_h1, c0, c1);
+        or_fr_mul(tmp2, ch.delta, lk->h1_next_eval);
+        or_fr_add(c1, c1, tmp2);
+        or_fr_mul(TERM(h1_poly), tmp, c1);
     }
-    /* - Z_H(z) * sum_k z^(kn) t_{k+1} (linearisation.cu:250-292) */
+    /* - Z_H(z) * sum_k z^(kn) t_{k+1} (linearisation_poly.rs:311-337) */
     {
-        uint64_t p[4], nv[4];
-        or_fr_neg(nv, vh);
-        fr_copy(p, nv);
+        uint64_t p[4];
+        or_fr_neg(p, vh);
         for (int k = 0; k < 8; k++) {
-            fr_copy(s_t[k], p);
+            fr_copy(TERM(E4(t_poly, k * n)), p);
             or_fr_mul(p, p, zn);
         }
     }
+#undef TERM
     uint64_t *lin = vec_alloc(n);
-    {
-        const uint64_t *P[12 + 8] = {pk->q_l_coeffs, pk->q_r_coeffs, pk->q_o_coeffs, pk->q_4_coeffs,
-                                     pk->q_hl_coeffs, pk->q_hr_coeffs, pk->q_h4_coeffs, pk->q_c_coeffs,
-                                     z_poly, pk->fourth_sigma_coeffs, z2_poly, h1_poly};
-        const uint64_t *S[12 + 8] = {s_ql, s_qr, s_qo, s_q4, s_qhl, s_qhr, s_qh4, s_qc,
-                                     s_z, s_s4, s_z2, s_h1};
-        for (int k = 0; k < 8; k++) { P[12 + k] = E4(t_poly, k * n); S[12 + k] = s_t[k]; }
 #pragma omp parallel for schedule(static)
-        for (int64_t i = 0; i < (int64_t)n; i++) {
-            uint64_t acc[4] = {0, 0, 0, 0}, t[4];
-            for (int k = 0; k < 20; k++) {
-                or_fr_mul(t, E4(P[k], i), S[k]);
-                or_fr_add(acc, acc, t);
-            }
-            fr_copy(E4(lin, i), acc);
+    for (int64_t i = 0; i < (int64_t)n; i++) {
+        uint64_t acc[4] = {0, 0, 0, 0}, t[4];
+        for (int k = 0; k < K; k++) {
+            or_fr_mul(t, E4(P[k], i), S[k]);
+            or_fr_add(acc, acc, t);
         }
+        fr_copy(E4(lin, i), acc);
     }
-    /* transcript appends (gen_proof.cuh:373-403) */
+    /* transcript appends (prover.rs:532-572) */
     or_transcript_append_scalar(tr, "a_eval", ae);
     or_transcript_append_scalar(tr, "b_eval", be);
     or_transcript_append_scalar(tr, "c_eval", ce);
@@ -605,7 +643,7 @@ int or_gen_proof(const CircuitC *cs, const ProverKeyC *pk, const CommitKeyC *ck,
     or_transcript_append_scalar(tr, "b_next_eval", cu->b_next_eval);
     or_transcript_append_scalar(tr, "d_next_eval", cu->d_next_eval);
 
-    /* 6. KZG openings (gen_proof.cuh:405-463, kzg10.cu:116-145) */
+    /* 6. KZG openings (prover.rs:574-636, kzg10.cu:116-145) */
     uint64_t aw[4], saw[4];
     or_transcript_challenge_scalar(tr, "aggregate_witness", aw);
     const uint64_t *awp[11] = {lin, pk->left_sigma_coeffs, pk->right_sigma_coeffs,
@@ -651,6 +689,19 @@ int or_gen_proof(const CircuitC *cs, const ProverKeyC *pk, const CommitKeyC *ck,
     for (int j = 0; j < 4; j++) { free(wsc[j]); free(wpoly[j]); free(fs[j]); }
     free(tc); free(table_poly); free(qlk); free(fc); free(f_poly); free(h1); free(h2);
     free(h1_poly); free(h2_poly); free(z_poly); free(z2_poly); free(pie); free(pi_poly);
-    free(t_poly); free(lin); free(comb);
+    free(t_poly); free(lin); free(comb); free(pis);
     return PNP_OK;
+}
+
+/* the v1 symbol (lib.rs:237-239): one public input, label "Merkle tree" */
+int or_gen_proof(const CircuitC *cs, const ProverKeyC *pk, const CommitKeyC *ck, ProofC *out) {
+    if (cs->intended_pi_pos >= next_pow2(cs->n > cs->lookup_len ? cs->n : cs->lookup_len))
+        return PNP_E_ARG;
+    return gen_proof_impl(cs, pk, ck, 1, &cs->intended_pi_pos, cs->pi, "Merkle tree", 1, out);
+}
+
+/* any number of public inputs (canonical values) and a transcript label */
+int or_gen_proof_ex(const CircuitC *cs, const ProverKeyC *pk, const CommitKeyC *ck, uint64_t n_pi,
+                    const uint64_t *pi_pos, const uint64_t *pi_canon, const char *label, ProofC *out) {
+    return gen_proof_impl(cs, pk, ck, n_pi, pi_pos, pi_canon, label ? label : "Merkle tree", 0, out);
 }
