@@ -201,7 +201,8 @@ ProofC gen_proof(CircuitC circuit, ProverKeyC pk, CommitKeyC ck);
 #define PNP_E_ARG          -1   /* bad argument / size                      */
 #define PNP_E_DEVICE       -2   /* HIP runtime error                        */
 #define PNP_E_NOKEY        -3   /* prover / commit key not loaded           */
-#define PNP_E_ENVELOPE     -4   /* input outside the supported circuit class */
+#define PNP_E_ENVELOPE     -4   /* input outside the supported circuit class (unused since
+                                       the general prover: kept for ABI stability) */
 #define PNP_E_NOMEM        -5   /* device allocation failed                 */
 
 typedef struct pnp_ctx pnp_ctx;
@@ -225,6 +226,19 @@ int pnp_load_commit_key(pnp_ctx *ctx, const CommitKeyC *ck, uint64_t n_points,
 /* Prove with the resident keys.  `device_ptrs`: the CircuitC witness pointers
  * (q_lookup, w_*) are HBM pointers; pi is always a host pointer. */
 int pnp_prove(pnp_ctx *ctx, const CircuitC *cs, int device_ptrs, ProofC *out);
+
+/* pnp_prove with the general public-input set and transcript label of the
+ * ZK-Garage prover (Prover::prove_with_preprocessed, prover.rs:171-190: the
+ * transcript holds the PublicInputs BTreeMap, pi.rs:16-86), which the v1 ABI
+ * cannot carry (CircuitC has one pi / intended_pi_pos, prover.rs:717-725).
+ * n_pi pairs (pi_pos[k], pi_canon[4k..4k+4)) — canonical (non-Montgomery)
+ * values, host memory, any order; zero values are dropped like
+ * PublicInputs::insert; positions must be distinct and < domain size.
+ * cs->pi / cs->intended_pi_pos are ignored.  label = NULL is "Merkle tree".
+ * With n_pi = 1, a non-zero value and the default label the proof equals
+ * pnp_prove's. */
+int pnp_prove_ex(pnp_ctx *ctx, const CircuitC *cs, int device_ptrs, uint64_t n_pi,
+                 const uint64_t *pi_pos, const uint64_t *pi_canon, const char *label, ProofC *out);
 
 /* Per-stage wall-clock (ms) of the last pnp_prove, for the bench/profiles.
  * Writes up to `cap` doubles and their names; returns the stage count. */

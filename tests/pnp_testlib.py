@@ -245,13 +245,26 @@ class Inputs:
         for name in PK_ZERO_EVALS:
             a[name] = np.zeros((N8, 4), dtype=np.uint64)
         if qm_qlookup_evals:
-            a["q_m_evals"] = rand_fr_mont_arr(rng, N8)
-            a["q_lookup_evals"] = rand_fr_mont_arr(rng, N8)
-        if lookup_rows:
-            rows = rng.choice(ng, size=min(lookup_rows, ng), replace=False)
-            a["q_lookup"][rows] = rand_fr_mont_arr(rng, len(rows))
+            # live q_m / q_lookup selectors (consistent coefficients + LDE)
+            for sel in ("q_m", "q_lookup"):
+                c = rand_fr_mont_arr(rng, n)
+                e = np.zeros((N8, 4), dtype=np.uint64)
+                lib.or_coset_lde8(vp(c), vp(e), lg_n)
+                a[sel + "_coeffs"] = c
+                a[sel + "_evals"] = e
         for t in ("table1", "table2", "table3", "table4"):
             a[t] = np.zeros((n, 4), dtype=np.uint64)
+        if lookup_rows:
+            # non-zero query rows; the table holds their wire tuples (so every
+            # query is in the table, combine_split is defined), padded with
+            # its first row (MultiSet::pad)
+            rows = np.sort(rng.choice(ng, size=min(lookup_rows, ng), replace=False))
+            a["q_lookup"][rows] = rand_fr_mont_arr(rng, len(rows))
+            for j, (t, w) in enumerate(zip(("table1", "table2", "table3", "table4"),
+                                           ("w_l", "w_r", "w_o", "w_4"))):
+                col = a[w][rows[::-1]]
+                a[t][:len(rows)] = col
+                a[t][len(rows):] = col[0]
         # linear_evaluations = coset points g*w^i; v_h = (g w^i)^n - 1
         w8 = fr_root(lg_n + 3)
         xs, vh = [], []

@@ -39,9 +39,10 @@ def test_gen_proof_v1_parity(lg, seed):
 
 @pytest.mark.parametrize("lookup_rows,extra", [(0, True), (17, False), (40, True)])
 def test_gen_proof_general_lookup_and_selectors(lookup_rows, extra):
-    """Branches outside the lookup-trivial fast path: non-zero q_lookup witness
-    (f != 0, z2 a real grand product, z2 committed by MSM) and live q_m /
-    q_lookup quotient terms."""
+    """Random (unsatisfied) inputs outside the lookup-trivial fast path:
+    non-zero q_lookup witness rows whose wire tuples form the lookup table
+    (f != 0, t != 0: combine_split, h1 / h2 committed, z2 a real grand
+    product) and live q_m / q_lookup selectors (coefficients + evaluations)."""
     import pnp
     inp = Inputs(8, 30 + lookup_rows, lookup_rows=lookup_rows, qm_qlookup_evals=extra)
     exp = inp.oracle_proof()
@@ -52,6 +53,7 @@ def test_gen_proof_general_lookup_and_selectors(lookup_rows, extra):
     assert _diff(got, exp) == []
     if lookup_rows:
         assert any(v != 0 for v in exp.f_comm.x)
+        assert any(v != 0 for v in exp.h_1_comm.x)
     ctx.close()
 
 

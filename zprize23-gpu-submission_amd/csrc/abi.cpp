@@ -304,20 +304,27 @@ int pnp_synth_coset_consts(pnp_ctx *ctx, uint64_t *d_vh, uint64_t *d_x, uint32_t
 // ---------------------------------------------------------------- keys + prove
 namespace {
 
-enum FieldKind { kSkip, kEvals8, kCoeffs, kCheckZero8, kTableZero };
+enum FieldKind { kSkip, kEvals8, kCoeffs, kSelEvals8, kSelCoeffs, kTable };
 
-// ProverKeyC field order (lib.rs:157-223) -> how gen_proof uses it
+// ProverKeyC field order (lib.rs:157-223) -> how gen_proof uses it.  The
+// q_m, custom-gate and q_lookup selectors (kSel*) are read only when their 8n
+// evaluations are non-zero: for the zero polynomial the Rust prover key holds
+// EMPTY coefficient Vecs (prover.rs:765-808 passes their dangling pointers),
+// so those coefficients are never touched.
 const FieldKind kPkKinds[44] = {
-    kSkip, kEvals8,                                   // q_m coeffs (empty) / evals
+    kSelCoeffs, kSelEvals8,                           // q_m
     kCoeffs, kEvals8, kCoeffs, kEvals8, kCoeffs, kEvals8, kCoeffs, kEvals8,  // q_l q_r q_o q_4
     kCoeffs, kEvals8, kCoeffs, kEvals8, kCoeffs, kEvals8, kCoeffs, kEvals8,  // q_c q_hl q_hr q_h4
     kCoeffs, kEvals8,                                 // q_arith
-    kSkip, kCheckZero8, kSkip, kCheckZero8,           // range, logic selectors
-    kSkip, kCheckZero8, kSkip, kCheckZero8,           // fixed / variable group add selectors
-    kSkip, kEvals8,                                   // q_lookup coeffs (empty) / evals
-    kTableZero, kTableZero, kTableZero, kTableZero,   // table1..4
+    kSelCoeffs, kSelEvals8, kSelCoeffs, kSelEvals8,   // range, logic selectors
+    kSelCoeffs, kSelEvals8, kSelCoeffs, kSelEvals8,   // fixed / variable group add selectors
+    kSelCoeffs, kSelEvals8,                           // q_lookup
+    kTable, kTable, kTable, kTable,                   // table1..4 (n each, MultiSet::pad)
     kCoeffs, kEvals8, kCoeffs, kEvals8, kCoeffs, kEvals8, kCoeffs, kEvals8,  // sigmas
     kEvals8, kEvals8};                                // linear_evaluations, v_h_coset_8n
+// selector fields (coefficients index; evaluations follow): q_m, range,
+// logic, fixed group add, variable group add, q_lookup
+const int kSelField[6] = {0, 20, 22, 24, 26, 28};
 
 bool host_all_zero(const uint64_t *p, uint64_t words) {
     uint64_t acc = 0;
@@ -338,24 +345,27 @@ int pnp_load_prover_key(pnp_ctx *ctx, const ProverKeyC *pk, uint64_t D, int devi
         ProverKeyC dev{};
         uint64_t *const *src = reinterpret_cast<uint64_t *const *>(pk);
         uint64_t **dst = reinterpret_cast<uint64_t **>(&dev);
-        for (int f = 0; f < 44; f++) {
-            FieldKind k = kPkKinds[f];
-            dst[f] = nullptr;
-            if (k == kSkip) continue;
-            uint64_t elems = (k == kEvals8 || k == kCheckZero8) ? 8 * D : D;
+        // non-zero selectors first: they decide which coefficient Vecs exist
+        bool sel_nz[44] = {};
+        for (int k = 0; k < 6; k++) {
+            const int f = kSelField[k] + 1;
             if (!src[f]) {
                 set_error("prover key field %d is null", f);
                 throw Error(PNP_E_ARG);
             }
-            if (k == kCheckZero8 || k == kTableZero) {
-                bool nz = device_ptrs ? pnp::k_any_nonzero(src[f], 4 * elems, ctx->scratch_b, ctx->stream)
-                                      : !host_all_zero(src[f], 4 * elems);
-                if (nz) {
-                    set_error("prover key field %d is non-zero: custom-gate selectors and lookup "
-                              "tables must be zero (reference parity envelope, SURVEY.md 8a)", f);
-                    throw Error(PNP_E_ENVELOPE);
-                }
-                if (k == kCheckZero8) continue;
+            const uint64_t words = 4 * 8 * D;
+            const bool nz = device_ptrs ? pnp::k_any_nonzero(src[f], words, ctx->scratch_b, ctx->stream)
+                                        : !host_all_zero(src[f], words);
+            sel_nz[f] = sel_nz[f - 1] = nz;
+        }
+        for (int f = 0; f < 44; f++) {
+            FieldKind k = kPkKinds[f];
+            dst[f] = nullptr;
+            if (k == kSkip || ((k == kSelEvals8 || k == kSelCoeffs) && !sel_nz[f])) continue;
+            uint64_t elems = (k == kEvals8 || k == kSelEvals8) ? 8 * D : D;
+            if (!src[f]) {
+                set_error("prover key field %d is null", f);
+                throw Error(PNP_E_ARG);
             }
             if (device_ptrs) {
                 dst[f] = src[f];
@@ -370,9 +380,12 @@ int pnp_load_prover_key(pnp_ctx *ctx, const ProverKeyC *pk, uint64_t D, int devi
         // zero-selector flags (the quotient kernel skips known-zero selectors)
         // and the sigma n-domain evaluations (gen_proof.cuh:159-165 recomputes
         // NTT.forward(sigma_coeffs) every proof)
-        ctx->pk_qm_zero = !pnp::k_any_nonzero(dev.q_m_evals, 4 * 8 * D, ctx->scratch_b, ctx->stream);
-        ctx->pk_qlookup_zero =
-            !pnp::k_any_nonzero(dev.q_lookup_evals, 4 * 8 * D, ctx->scratch_b, ctx->stream);
+        ctx->pk_qm_zero = dev.q_m_evals == nullptr;
+        ctx->pk_qlookup_zero = dev.q_lookup_evals == nullptr;
+        ctx->pk_custom_nz[0] = dev.range_selector_evals != nullptr;
+        ctx->pk_custom_nz[1] = dev.logic_selector_evals != nullptr;
+        ctx->pk_custom_nz[2] = dev.fixed_group_add_selector_evals != nullptr;
+        ctx->pk_custom_nz[3] = dev.variable_group_add_selector_evals != nullptr;
         const uint64_t *sigc[4] = {dev.left_sigma_coeffs, dev.right_sigma_coeffs,
                                    dev.out_sigma_coeffs, dev.fourth_sigma_coeffs};
         uint32_t lg = 0;
@@ -426,6 +439,10 @@ int pnp_load_prover_key(pnp_ctx *ctx, const ProverKeyC *pk, uint64_t D, int devi
         };
         if (!ctx->pk_qm_zero) blk("q_m", dev.q_m_evals);
         if (!ctx->pk_qlookup_zero) blk("q_lookup", dev.q_lookup_evals);
+        if (ctx->pk_custom_nz[0]) blk("range", dev.range_selector_evals);
+        if (ctx->pk_custom_nz[1]) blk("logic", dev.logic_selector_evals);
+        if (ctx->pk_custom_nz[2]) blk("fixed_add", dev.fixed_group_add_selector_evals);
+        if (ctx->pk_custom_nz[3]) blk("var_add", dev.variable_group_add_selector_evals);
         blk("q_l", dev.q_l_evals);
         blk("q_r", dev.q_r_evals);
         blk("q_o", dev.q_o_evals);
@@ -484,6 +501,17 @@ int pnp_prove(pnp_ctx *ctx, const CircuitC *cs, int device_ptrs, ProofC *out) {
     }
 }
 
+int pnp_prove_ex(pnp_ctx *ctx, const CircuitC *cs, int device_ptrs, uint64_t n_pi, const uint64_t *pi_pos,
+                 const uint64_t *pi_canon, const char *label, ProofC *out) {
+    if (!ctx || !cs || !out || (n_pi && (!pi_pos || !pi_canon))) return PNP_E_ARG;
+    ProveOpts o{n_pi, pi_pos, pi_canon, label ? label : "Merkle tree"};
+    try {
+        return prove_impl(ctx, cs, device_ptrs, out, &o);
+    } catch (const Error &e) {
+        return e.code;
+    }
+}
+
 int pnp_last_stage_times(pnp_ctx *ctx, double *ms, const char **names, int cap) {
     if (!ctx) return 0;
     int k = 0;
@@ -526,8 +554,10 @@ uint64_t pk_fingerprint(const ProverKeyC &pk, uint64_t D) {
     for (int i = 0; i < 44; i++) {
         h = mix64(h, reinterpret_cast<uintptr_t>(f[i]));
         FieldKind k = kPkKinds[i];
-        if (k == kSkip || !f[i]) continue;
-        const uint64_t elems = (k == kEvals8 || k == kCheckZero8) ? 8 * D : D;
+        // selector coefficients may be empty Vecs: pointer only (their
+        // evaluations, sampled, decide whether they are read)
+        if (k == kSkip || k == kSelCoeffs || !f[i]) continue;
+        const uint64_t elems = (k == kEvals8 || k == kSelEvals8) ? 8 * D : D;
         h = sample_words(h, f[i], 4 * elems);
     }
     return h;

@@ -19,6 +19,7 @@ struct pnp_ctx {
     std::vector<pnp::DevBuf> pk_owned;     // copies (device_ptrs == 0)
     ProverKeyC pk_dev{};                   // HBM pointers for every field
     bool pk_qm_zero = false, pk_qlookup_zero = false;  // all-zero 8n selector evaluations
+    bool pk_custom_nz[4] = {};  // range, logic, fixed-base, curve-add selectors non-zero
     pnp::DevBuf pk_sigma_n[4];             // sigma evaluations on the n-domain
     // The quotient's 8n-point arrays in block layout (ntt.hip: point 8j + m
     // -> block m, index j), blocks pk_mb0 .. pk_mb0 + pk_nb - 1 only:
@@ -63,5 +64,13 @@ void commit_affine(pnp_ctx *ctx, const uint64_t *d_scalars, uint64_t n, Commitme
 // local: on a multi-GPU run the scalars hold only this rank's point range
 void commit_affine_batch(pnp_ctx *ctx, const uint64_t *const *d_scalars, int B, uint64_t n,
                          CommitmentC *const *out, bool local = false);
-int prove_impl(pnp_ctx *ctx, const CircuitC *cs, int device_ptrs, ProofC *out);
+// v2 options of pnp_prove_ex: public inputs (positions, canonical values) and
+// the transcript label; nullptr = the v1 contract (one PI from the circuit,
+// label "Merkle tree")
+struct ProveOpts {
+    uint64_t n_pi;
+    const uint64_t *pi_pos, *pi_canon;
+    const char *label;
+};
+int prove_impl(pnp_ctx *ctx, const CircuitC *cs, int device_ptrs, ProofC *out, const ProveOpts *opt = nullptr);
 }  // namespace pnp

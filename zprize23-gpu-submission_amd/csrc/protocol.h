@@ -40,7 +40,18 @@ struct QuotArgs {
     Fr bk[4], opd, eopd, sep2, sep3;
 };
 
-constexpr int LIN_MAX = 24;
+// custom-gate quotient terms (k_widgets): block-layout arrays as QuotArgs;
+// sel = range, logic, fixed-base scalar mul, curve addition selector
+// evaluations (nullptr = zero selector), sep = their separation challenges
+struct WidgetArgs {
+    const uint64_t *w8[4], *q_l, *q_r, *q_c, *vh_inv;
+    const uint64_t *sel[4];
+    Fr sep[4];
+    uint64_t n;
+    uint32_t lg_n;
+};
+
+constexpr int LIN_MAX = 32;
 struct LinArgs {
     int k;
     const uint64_t *p[LIN_MAX];
@@ -65,6 +76,12 @@ bool k_any_diff(const uint64_t *a, const uint64_t *b, uint64_t words, DevBuf &sc
 void k_affine(uint64_t *out, const uint64_t *in, const Fr &a, const Fr &b, uint64_t n, hipStream_t s);
 void k_quotient(const QuotArgs &q, uint64_t N8, uint64_t *out, hipStream_t s);
 void k_lincomb(const LinArgs &a, uint64_t n, uint64_t *out, hipStream_t s);
+void k_widgets(const WidgetArgs &g, uint64_t N8, uint64_t *out, hipStream_t s);
+// MultiSet::combine_split (lookup/multiset.rs:131-180) of the compressed table
+// t and query f (n each, Montgomery) into h1, h2 (n each); false when a value
+// of f does not occur in t (lookup.hip)
+bool combine_split(pnp_ctx *ctx, const uint64_t *t, const uint64_t *f, uint64_t n, uint64_t *h1,
+                   uint64_t *h2, hipStream_t s);
 // empty kernel marking the start of a proof in kernel traces
 void k_proof_marker(hipStream_t s);
 

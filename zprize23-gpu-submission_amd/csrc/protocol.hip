@@ -16,6 +16,7 @@
 //                  polynomial, KZG opening combine) KZG/kzg10.cu:116-145
 #include "pnp_internal.h"
 #include "protocol.h"
+#include "widgets.cuh"
 #include <vector>
 
 namespace pnp {
@@ -93,22 +94,17 @@ void k_perm_numden(uint64_t *num, uint64_t *den, const PermArgs &a, uint64_t n, 
     PNP_HIP(hipGetLastError());
 }
 
-// _lookup_ratio with the reference's 8-byte shifted t_next / h1_next words
-__device__ __forceinline__ Fr load_shift8(const uint64_t *v, uint64_t i, uint64_t n) {
-    uint64_t w[4];
-    w[0] = v[4 * i + 1];
-    w[1] = v[4 * i + 2];
-    w[2] = v[4 * i + 3];
-    w[3] = i + 1 < n ? v[4 * (i + 1)] : v[0];
-    return from_u64_limbs_dev(w);
-}
+// lookup_ratio (permutation/mod.rs:754-822): t_next[i] = t[i + 1], h1_next[i]
+// = h1[i + 1], wrapping.  (The reference GPU path shifts by 8 bytes instead,
+// permutation/mod.cu:121-128; that only agrees on its f = t = h = 0 class.)
 __global__ void k_lookup_nd_(uint64_t *num, uint64_t *den, const uint64_t *f, const uint64_t *t,
                              const uint64_t *h1, const uint64_t *h2, Fr delta, Fr eps, uint64_t n) {
     uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
     if (i >= n) return;
     Fr opd = delta + Fr::one();
     Fr eopd = eps * opd;
-    Fr tn = load_shift8(t, i, n), h1n = load_shift8(h1, i, n);
+    const uint64_t nx = (i + 1) & (n - 1);
+    Fr tn = load_fr(t, nx), h1n = load_fr(h1, nx);
     Fr fi = load_fr(f, i), ti = load_fr(t, i), h1i = load_fr(h1, i), h2i = load_fr(h2, i);
     Fr r = (eopd + ti + delta * tn) * (opd * (eps + fi));
     Fr d = (h2i * delta + (eopd + h1i)) * ((eopd + h2i) + h1n * delta);
@@ -214,17 +210,19 @@ __device__ __forceinline__ Fr pow5(const Fr &a) {
     return a2 * a2 * a;
 }
 
+// the coset point w_8n^8 further: index j + 1 of the same block, at its
+// bit-reversed position (block-bitrev layout, ntt.hip lde_blocks)
+__device__ __forceinline__ uint64_t next_in_block(uint64_t i, uint64_t n, uint32_t lg_n) {
+    const uint64_t jp = i & (n - 1);
+    if (!lg_n) return i;
+    const uint32_t j = __brev((uint32_t)jp) >> (32 - lg_n);
+    return i - jp + (__brev((j + 1) & (uint32_t)(n - 1)) >> (32 - lg_n));
+}
+
 __global__ __launch_bounds__(256) void k_quotient_(QuotArgs q, uint64_t N8, uint64_t *out) {
     uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
     if (i >= N8) return;
-    // the coset point w_8n^8 further: index j + 1 of the same block, at its
-    // bit-reversed position (block-bitrev layout, ntt.hip lde_blocks)
-    const uint64_t jp = i & (q.n - 1);
-    uint64_t nx = i;
-    if (q.lg_n) {
-        const uint32_t j = __brev((uint32_t)jp) >> (32 - q.lg_n);
-        nx = i - jp + (__brev((j + 1) & (uint32_t)(q.n - 1)) >> (32 - q.lg_n));
-    }
+    const uint64_t nx = next_in_block(i, q.n, q.lg_n);
     Fr a = load_fr(q.w8[0], i), b = load_fr(q.w8[1], i), c = load_fr(q.w8[2], i), d = load_fr(q.w8[3], i);
     // compute_quotient_i (widget/arithmetic.cu:7-45) + pi; sums of two
     // products share one Montgomery reduction (fr_mul2)
@@ -278,6 +276,36 @@ __global__ __launch_bounds__(256) void k_quotient_(QuotArgs q, uint64_t N8, uint
 }
 void k_quotient(const QuotArgs &q, uint64_t N8, uint64_t *out, hipStream_t s) {
     hipLaunchKernelGGL(k_quotient_, dim3(nblk(N8)), dim3(256), 0, s, q, N8, out);
+    PNP_HIP(hipGetLastError());
+}
+
+// custom gates (quotient_poly.rs:253-296): out += sum_g selector_g * constraints_g
+// * v_h^-1, one more pass over the blocks, launched only when a custom-gate
+// selector is non-zero (the Merkle circuit has none)
+__global__ __launch_bounds__(256) void k_widgets_(WidgetArgs g, uint64_t N8, uint64_t *out) {
+    uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    if (i >= N8) return;
+    const uint64_t nx = next_in_block(i, g.n, g.lg_n);
+    WidgetVals w;
+    w.a = load_fr(g.w8[0], i);
+    w.b = load_fr(g.w8[1], i);
+    w.c = load_fr(g.w8[2], i);
+    w.d = load_fr(g.w8[3], i);
+    w.a_next = load_fr(g.w8[0], nx);
+    w.b_next = load_fr(g.w8[1], nx);
+    w.d_next = load_fr(g.w8[3], nx);
+    w.q_l = load_fr(g.q_l, i);
+    w.q_r = load_fr(g.q_r, i);
+    w.q_c = load_fr(g.q_c, i);
+    Fr acc = Fr::zero();
+    if (g.sel[0]) acc += load_fr(g.sel[0], i) * w_range(g.sep[0], w);
+    if (g.sel[1]) acc += load_fr(g.sel[1], i) * w_logic(g.sep[1], w);
+    if (g.sel[2]) acc += load_fr(g.sel[2], i) * w_fbsm(g.sep[2], w);
+    if (g.sel[3]) acc += load_fr(g.sel[3], i) * w_cadd(g.sep[3], w);
+    store_fr(out, i, load_fr(out, i) + acc * load_fr(g.vh_inv, i));
+}
+void k_widgets(const WidgetArgs &g, uint64_t N8, uint64_t *out, hipStream_t s) {
+    hipLaunchKernelGGL(k_widgets_, dim3(nblk(N8)), dim3(256), 0, s, g, N8, out);
     PNP_HIP(hipGetLastError());
 }
 

@@ -1,12 +1,17 @@
 // prover.cpp — gen_proof orchestration on one MI355X.
 //
-// Protocol order, transcript labels and formulas follow the reference's
-// prove() (lib/PLONK/src/gen_proof.cuh:10-489) step by step, including its
-// circuit-class shortcuts: transcript "Merkle tree", h1 = h2 =
-// 0 (combine_split skipped), empty q_m / custom-selector / q_lookup coeffs, one
-// public input, the 8-byte t_next / h1_next shift.  Inputs outside that class
-// (non-zero custom-gate selectors or lookup tables) are rejected with
-// PNP_E_ENVELOPE instead of silently diverging.
+// Protocol order and transcript labels follow the reference's prove()
+// (lib/PLONK/src/gen_proof.cuh:10-489); the semantics are the ZK-Garage
+// prover's (prover.rs:171-660), which the GPU path reproduces on its own
+// circuit class (the Merkle circuit: no custom gates, no lookup tables, one
+// public input) and abandons outside it (combine_split
+// skipped, empty q_m / custom-selector / q_lookup coefficients, the 8-byte
+// t_next / h1_next shift — proofs its verifier rejects).  Here, for any
+// circuit: h1 / h2 from combine_split (lookup.hip), z2 with the true next
+// row, the range / logic / fixed-base / curve-add widgets in the quotient
+// (k_widgets) and the linearisation, q_m and q_lookup terms, and any number
+// of public inputs (pnp_prove_ex).  On the Merkle class every extra term is
+// zero and is skipped without a launch.
 //
 // What differs is HOW it runs on MI355X:
 //   * the prover key and SRS are HBM-resident (pnp_load_*), no per-proof H2D
@@ -25,6 +30,8 @@
 #include "context.h"
 #include "protocol.h"
 #include "transcript.h"
+#include "widgets.cuh"
+#include <algorithm>
 
 namespace pnp {
 
@@ -114,7 +121,7 @@ void div_linear_range(pnp_ctx *ctx, uint64_t *d, uint64_t len, const Fr &z, bool
 
 }  // namespace
 
-int prove_impl(pnp_ctx *ctx, const CircuitC *cs, int device_ptrs, ProofC *out) {
+int prove_impl(pnp_ctx *ctx, const CircuitC *cs, int device_ptrs, ProofC *out, const ProveOpts *opt) {
     if (!ctx->pk_loaded || !ctx->ck_loaded) {
         set_error("prover key / commit key not loaded");
         return PNP_E_NOKEY;
@@ -136,9 +143,37 @@ int prove_impl(pnp_ctx *ctx, const CircuitC *cs, int device_ptrs, ProofC *out) {
                   (unsigned long long)n);
         return PNP_E_ARG;
     }
-    if (cs->intended_pi_pos >= n || !cs->pi) {
-        set_error("public input position out of range");
-        return PNP_E_ARG;
+    // public inputs: v1 = the circuit's one (pi, intended_pi_pos), appended as
+    // the reference GPU path does (transcript.cuh:39-44); v2 = a PublicInputs
+    // map (pi.rs:16-86): BTreeMap order, zero values dropped
+    std::vector<uint64_t> pi_pos;
+    std::vector<Fr> pi_val;  // Montgomery
+    if (!opt) {
+        if (cs->intended_pi_pos >= n || !cs->pi) {
+            set_error("public input position out of range");
+            return PNP_E_ARG;
+        }
+        pi_pos.push_back(cs->intended_pi_pos);
+        pi_val.push_back(to_mont(from_u64_limbs<FrP>(cs->pi)));
+    } else {
+        std::vector<std::pair<uint64_t, Fr>> v;
+        for (uint64_t k = 0; k < opt->n_pi; k++) {
+            if (opt->pi_pos[k] >= n) {
+                set_error("public input position %llu out of range", (unsigned long long)opt->pi_pos[k]);
+                return PNP_E_ARG;
+            }
+            v.emplace_back(opt->pi_pos[k], to_mont(from_u64_limbs<FrP>(opt->pi_canon + 4 * k)));
+        }
+        std::sort(v.begin(), v.end(), [](const auto &a, const auto &b) { return a.first < b.first; });
+        for (size_t k = 0; k < v.size(); k++) {
+            if (k && v[k].first == v[k - 1].first) {
+                set_error("public input position %llu given twice", (unsigned long long)v[k].first);
+                return PNP_E_ARG;
+            }
+            if (v[k].second.is_zero()) continue;
+            pi_pos.push_back(v[k].first);
+            pi_val.push_back(v[k].second);
+        }
     }
     const uint64_t N8 = 8 * n, ng = cs->n;
     const ProverKeyC &pk = ctx->pk_dev;
@@ -160,8 +195,14 @@ int prove_impl(pnp_ctx *ctx, const CircuitC *cs, int device_ptrs, ProofC *out) {
     PNP_HIP(hipMemcpyAsync(qlk, cs->q_lookup, 32 * ng, kind, s));
     tm.mark("inputs");
 
-    Transcript tr("Merkle tree");
-    tr.append_pi("pi", cs->pi, cs->intended_pi_pos);
+    Transcript tr(opt ? opt->label : "Merkle tree");
+    if (!opt) {
+        tr.append_pi("pi", cs->pi, cs->intended_pi_pos);
+    } else {
+        std::vector<uint64_t> canon(4 * pi_val.size());
+        for (size_t k = 0; k < pi_val.size(); k++) to_u64_limbs(from_mont(pi_val[k]), &canon[4 * k]);
+        tr.append_pis("pi", pi_pos.size(), pi_pos.data(), canon.data());
+    }
 
     // ---------------- round 1: witness polynomials (gen_proof.cuh:25-50)
     for (int j = 0; j < 4; j++) {
@@ -194,13 +235,45 @@ int prove_impl(pnp_ctx *ctx, const CircuitC *cs, int device_ptrs, ProofC *out) {
     PNP_HIP(hipMemcpyAsync(f_poly, fc, 32 * n, hipMemcpyDeviceToDevice, s));
     if (!table_zero) ntt_run(nt, table_poly, lg, true, false, s);
     if (!f_zero) ntt_run(nt, f_poly, lg, true, false, s);
-    if (f_zero) set_infinity(&out->f_comm); else commit_affine(ctx, f_poly, n, &out->f_comm);
+    // s = sorted concatenation of f and t, halves h1 / h2 (prover.rs:304-329).
+    // f = t = 0 (the Merkle circuit): h1 = h2 = 0, commitments at infinity.
+    // The f, h1, h2 MSMs are independent of the transcript in between, so
+    // they run as one batch.
+    const bool h_zero = f_zero && table_zero;
+    uint64_t *h1 = ctx->buf("h1", n), *h2 = ctx->buf("h2", n);
+    uint64_t *h1_poly = ctx->buf("h1_poly", n), *h2_poly = ctx->buf("h2_poly", n);
+    {
+        const uint64_t *sc[3];
+        CommitmentC *oc[3];
+        int nc = 0;
+        if (f_zero) {
+            set_infinity(&out->f_comm);
+        } else {
+            sc[nc] = f_poly;
+            oc[nc++] = &out->f_comm;
+        }
+        if (h_zero) {
+            PNP_HIP(hipMemsetAsync(h1, 0, 32 * n, s));
+            PNP_HIP(hipMemsetAsync(h2, 0, 32 * n, s));
+            set_infinity(&out->h_1_comm);
+            set_infinity(&out->h_2_comm);
+        } else {
+            if (!combine_split(ctx, tc, fc, n, h1, h2, s)) {
+                set_error("lookup: a query value is not in the lookup table (Error::ElementNotIndexed)");
+                return PNP_E_ARG;
+            }
+            PNP_HIP(hipMemcpyAsync(h1_poly, h1, 32 * n, hipMemcpyDeviceToDevice, s));
+            PNP_HIP(hipMemcpyAsync(h2_poly, h2, 32 * n, hipMemcpyDeviceToDevice, s));
+            ntt_run(nt, h1_poly, lg, true, false, s);
+            ntt_run(nt, h2_poly, lg, true, false, s);
+            sc[nc] = h1_poly;
+            oc[nc++] = &out->h_1_comm;
+            sc[nc] = h2_poly;
+            oc[nc++] = &out->h_2_comm;
+        }
+        if (nc) commit_affine_batch(ctx, sc, nc, n, oc);
+    }
     append_comm(tr, "f", out->f_comm);
-    // h1 = h2 = 0 (combine_split skipped): commitments are the point at infinity
-    uint64_t *zero_n = ctx->buf("zero_n", n);
-    PNP_HIP(hipMemsetAsync(zero_n, 0, 32 * n, s));
-    set_infinity(&out->h_1_comm);
-    set_infinity(&out->h_2_comm);
     append_comm(tr, "h1", out->h_1_comm);
     append_comm(tr, "h2", out->h_2_comm);
     tm.mark("r2_lookup");
@@ -243,11 +316,11 @@ int prove_impl(pnp_ctx *ctx, const CircuitC *cs, int device_ptrs, ProofC *out) {
     tm.mark("r3_z");
     commit_affine(ctx, z_poly, n, &out->z_comm);
     append_comm(tr, "z", out->z_comm);
-    // lookup grand product (permutation/mod.cu:111-144), h1 = h2 = 0
+    // lookup grand product (permutation/mod.rs:754-822)
     uint64_t *z2_poly = ctx->buf("z2_poly", n);
     // lookup-trivial case (f = t = h1 = h2 = 0): every ratio is
     // (1+d) e (e(1+d)) / (e(1+d))^2 = 1, so z2 = 1 and its coefficients are [1, 0, ...]
-    const bool z2_one = f_zero && table_zero;
+    const bool z2_one = h_zero;
     if (z2_one) {
         uint64_t one[4];
         to_u64_limbs(Fr::one(), one);
@@ -255,7 +328,7 @@ int prove_impl(pnp_ctx *ctx, const CircuitC *cs, int device_ptrs, ProofC *out) {
         PNP_HIP(hipMemcpyAsync(z2_poly, one, 32, hipMemcpyHostToDevice, s));
         PNP_HIP(hipStreamSynchronize(s));
     } else {
-        k_lookup_nd(num, den, fc, tc, zero_n, zero_n, delta, eps, n, s);
+        k_lookup_nd(num, den, fc, tc, h1, h2, delta, eps, n, s);
         k_batch_inverse(den, n, ctx->scratch_a, s);
         k_mul_inplace(num, den, n, s);
         k_prefix_product(num, n, ctx->scratch_a, s);
@@ -280,22 +353,32 @@ int prove_impl(pnp_ctx *ctx, const CircuitC *cs, int device_ptrs, ProofC *out) {
     uint64_t q0 = 0, q1 = n;
     if (dist) msm_point_range(n, ctx->msm.rank, world, q0, q1);
     const uint64_t len = q1 - q0;
-    const Fr pi_v = to_mont(from_u64_limbs<FrP>(cs->pi));
-    const bool closed = ctx->pk_std_coset;  // L1, PI on the coset in closed form
+    const bool closed = ctx->pk_std_coset;  // L1 (and one PI) on the coset in closed form
+    const bool pi_closed = closed && pi_pos.size() == 1;
     uint64_t *pi_poly = nullptr;
-    if (!closed) {
+    if (pi_pos.size() == 1 && !closed) {
         pi_poly = ctx->buf("pi_poly", n);
-        Fr w_inv_pos = pow_u64(inverse(root_of_unity(lg)), cs->intended_pi_pos);
-        k_geometric(pi_poly, n, pi_v * n_inv, w_inv_pos, s);
-    } else if (ctx->pk_pinv_pos != cs->intended_pi_pos) {
+        Fr w_inv_pos = pow_u64(inverse(root_of_unity(lg)), pi_pos[0]);
+        k_geometric(pi_poly, n, pi_val[0] * n_inv, w_inv_pos, s);
+    } else if (pi_pos.size() > 1) {  // iNTT of the sparse evaluations (pi.rs:76-86)
+        pi_poly = ctx->buf("pi_poly", n);
+        PNP_HIP(hipMemsetAsync(pi_poly, 0, 32 * n, s));
+        std::vector<uint64_t> limbs(4 * pi_val.size());
+        for (size_t k = 0; k < pi_val.size(); k++) to_u64_limbs(pi_val[k], &limbs[4 * k]);
+        for (size_t k = 0; k < pi_val.size(); k++)
+            PNP_HIP(hipMemcpyAsync(pi_poly + 4 * pi_pos[k], &limbs[4 * k], 32, hipMemcpyHostToDevice, s));
+        PNP_HIP(hipStreamSynchronize(s));
+        ntt_run(nt, pi_poly, lg, true, false, s);
+    }
+    if (pi_closed && ctx->pk_pinv_pos != pi_pos[0]) {
         // 1 / (x_i - w^pos) on this rank's blocks, kept across proofs with the
         // same PI position
         ctx->pk_pinv_pos = ~0ULL;
         if (ctx->pk_pinv.bytes < 32 * NB) ctx->pk_pinv.alloc(32 * NB);
-        Fr wpos = pow_u64(root_of_unity(lg), cs->intended_pi_pos);
+        Fr wpos = pow_u64(root_of_unity(lg), pi_pos[0]);
         k_affine(ctx->pk_pinv.u64(), ctx->blk("lin"), Fr::one(), neg(wpos), NB, s);
         k_batch_inverse(ctx->pk_pinv.u64(), NB, ctx->scratch_a, s);
-        ctx->pk_pinv_pos = cs->intended_pi_pos;
+        ctx->pk_pinv_pos = pi_pos[0];
     }
     tm.mark("r3_z2_pi");
 
@@ -326,11 +409,11 @@ int prove_impl(pnp_ctx *ctx, const CircuitC *cs, int device_ptrs, ProofC *out) {
     q.z8 = z8;
     q.pi8 = nullptr;
     q.l18 = q.l1v = q.pinv = nullptr;
-    if (closed) {
-        q.l1v = ctx->blk("l1v");
+    if (closed) q.l1v = ctx->blk("l1v");
+    if (pi_closed) {
         q.pinv = ctx->pk_pinv.u64();
-        q.c_pi = pi_v * pow_u64(root_of_unity(lg), cs->intended_pi_pos) * n_inv;
-    } else {
+        q.c_pi = pi_val[0] * pow_u64(root_of_unity(lg), pi_pos[0]) * n_inv;
+    } else if (pi_poly) {
         uint64_t *pi8 = ctx->buf("pi8", NB);
         lde(pi_poly, pi8);
         q.pi8 = pi8;
@@ -352,6 +435,13 @@ int prove_impl(pnp_ctx *ctx, const CircuitC *cs, int device_ptrs, ProofC *out) {
         q.t8 = t8;
     }
     q.h18 = q.h28 = nullptr;  // h1 = h2 = 0
+    if (!h_zero) {
+        uint64_t *h18 = ctx->buf("h18", NB), *h28 = ctx->buf("h28", NB);
+        lde(h1_poly, h18);
+        lde(h2_poly, h28);
+        q.h18 = h18;
+        q.h28 = h28;
+    }
     // compute_first_lagrange_poly_scaled(n, alpha^2) and (n, 1) (quotient.cu:3-8):
     // one LDE of L1 (coefficients n^-1, no iNTT); alpha^2 is applied in the kernel
     Fr alpha2 = alpha * alpha;
@@ -405,6 +495,25 @@ int prove_impl(pnp_ctx *ctx, const CircuitC *cs, int device_ptrs, ProofC *out) {
     hipEvent_t qe0 = nullptr;
     ctx->ktimer.begin("quotient", s, qe0);
     k_quotient(q, NB, t_blk, s);
+    if (ctx->pk_custom_nz[0] || ctx->pk_custom_nz[1] || ctx->pk_custom_nz[2] || ctx->pk_custom_nz[3]) {
+        WidgetArgs g;
+        for (int j = 0; j < 4; j++) g.w8[j] = q.w8[j];
+        g.q_l = q.q_l;
+        g.q_r = q.q_r;
+        g.q_c = q.q_c;
+        g.vh_inv = q.vh_inv;
+        g.sel[0] = ctx->blk("range");
+        g.sel[1] = ctx->blk("logic");
+        g.sel[2] = ctx->blk("fixed_add");
+        g.sel[3] = ctx->blk("var_add");
+        g.sep[0] = range_c;
+        g.sep[1] = logic_c;
+        g.sep[2] = fixed_c;
+        g.sep[3] = var_c;
+        g.n = n;
+        g.lg_n = lg;
+        k_widgets(g, NB, t_blk, s);
+    }
     {
         // algorithmic bytes: every coset array the kernel reads (nullptr = known
         // zero, not read) plus t, 32 B per point each
@@ -526,6 +635,13 @@ int prove_impl(pnp_ctx *ctx, const CircuitC *cs, int device_ptrs, ProofC *out) {
         Fr z2n = Fr::one();
         if (!z2_one) k_poly_eval(z2_poly, n, zw, ctx->scratch_a, &z2n, s);
         Fr f_eval = Fr::zero(), t_eval = Fr::zero(), t_next = Fr::zero();
+        Fr ql_eval = Fr::zero(), h1_eval = Fr::zero(), h1_next = Fr::zero(), h2_eval = Fr::zero();
+        if (!ctx->pk_qlookup_zero) k_poly_eval(pk.q_lookup_coeffs, n, zc, ctx->scratch_a, &ql_eval, s);
+        if (!h_zero) {
+            k_poly_eval(h1_poly, n, zc, ctx->scratch_a, &h1_eval, s);
+            k_poly_eval(h1_poly, n, zw, ctx->scratch_a, &h1_next, s);
+            k_poly_eval(h2_poly, n, zc, ctx->scratch_a, &h2_eval, s);
+        }
         if (!f_zero) k_poly_eval(f_poly, n, zc, ctx->scratch_a, &f_eval, s);
         if (!table_zero) {
             k_poly_eval(table_poly, n, zc, ctx->scratch_a, &t_eval, s);
@@ -550,7 +666,11 @@ int prove_impl(pnp_ctx *ctx, const CircuitC *cs, int device_ptrs, ProofC *out) {
         store_fr_host(cu->a_next_eval, rw[1]);
         store_fr_host(cu->b_next_eval, rw[2]);
         store_fr_host(cu->d_next_eval, rw[3]);
-        LookupEvaluationsC *lk = &ev->lookup_evals;  // q_lookup, h1, h1_next, h2 evals = 0
+        LookupEvaluationsC *lk = &ev->lookup_evals;
+        store_fr_host(lk->q_lookup_eval, ql_eval);
+        store_fr_host(lk->h1_eval, h1_eval);
+        store_fr_host(lk->h1_next_eval, h1_next);
+        store_fr_host(lk->h2_eval, h2_eval);
         store_fr_host(lk->z2_next_eval, z2n);
         store_fr_host(lk->f_eval, f_eval);
         store_fr_host(lk->table_eval, t_eval);
@@ -571,7 +691,8 @@ int prove_impl(pnp_ctx *ctx, const CircuitC *cs, int device_ptrs, ProofC *out) {
     };
     auto push = [&](const uint64_t *p, const Fr &sc) { push_local(p + 4 * q0, sc); };
     auto p5 = [](const Fr &x) { Fr x2 = x * x; return x2 * x2 * x; };
-    // compute_linearisation_arithmetic (widget/arithmetic.cu:47-80), q_m coeffs empty
+    // arithmetic (widget/arithmetic.rs:82-100)
+    if (!ctx->pk_qm_zero) push(pk.q_m_coeffs, ae * be * qae);
     push(pk.q_l_coeffs, ae * qae);
     push(pk.q_r_coeffs, be * qae);
     push(pk.q_o_coeffs, ce * qae);
@@ -580,6 +701,25 @@ int prove_impl(pnp_ctx *ctx, const CircuitC *cs, int device_ptrs, ProofC *out) {
     push(pk.q_hr_coeffs, p5(be) * qae);
     push(pk.q_h4_coeffs, p5(de) * qae);
     push(pk.q_c_coeffs, qae);
+    // custom gates (linearisation_poly.rs:396-430): selector * constraints(evals)
+    {
+        const CustomEvaluationsC *ce_ = &ev->custom_evals;
+        WidgetVals wv;
+        wv.a = ae;
+        wv.b = be;
+        wv.c = ce;
+        wv.d = de;
+        wv.a_next = ld(ce_->a_next_eval);
+        wv.b_next = ld(ce_->b_next_eval);
+        wv.d_next = ld(ce_->d_next_eval);
+        wv.q_l = ld(ce_->q_l_eval);
+        wv.q_r = ld(ce_->q_r_eval);
+        wv.q_c = ld(ce_->q_c_eval);
+        if (ctx->pk_custom_nz[0]) push(pk.range_selector_coeffs, w_range(range_c, wv));
+        if (ctx->pk_custom_nz[1]) push(pk.logic_selector_coeffs, w_logic(logic_c, wv));
+        if (ctx->pk_custom_nz[2]) push(pk.fixed_group_add_selector_coeffs, w_fbsm(fixed_c, wv));
+        if (ctx->pk_custom_nz[3]) push(pk.variable_group_add_selector_coeffs, w_cadd(var_c, wv));
+    }
     // compute_linearisation_permutation (proof_system/permutation.cu:231-265)
     {
         Fr bz = beta * zc;
@@ -592,14 +732,19 @@ int prove_impl(pnp_ctx *ctx, const CircuitC *cs, int device_ptrs, ProofC *out) {
                (beta * pe) * alpha;
         push(pk.fourth_sigma_coeffs, neg(b));
     }
-    // compute_linearisation_lookup (widget/lookup.cu:136-199); q_lookup coeffs empty,
-    // the h1_poly term is identically zero (h1 = 0)
+    // lookup (widget/lookup.rs:137-182)
     {
         const LookupEvaluationsC *lk = &ev->lookup_evals;
         Fr sep2 = lsep * lsep, sep3 = sep2 * lsep, opd = delta + Fr::one(), eopd = eps * opd;
+        if (!ctx->pk_qlookup_zero) {
+            Fr ct = ((de * zeta + ce) * zeta + be) * zeta + ae;
+            push(pk.q_lookup_coeffs, (ct - ld(lk->f_eval)) * lsep);
+        }
         Fr b0 = eps + ld(lk->f_eval);
         Fr b1 = eopd + ld(lk->table_eval) + delta * ld(lk->table_next_eval);
         push(z2_poly, opd * b0 * b1 * sep2 + l1e * sep3);
+        if (!h_zero)
+            push(h1_poly, neg(ld(lk->z2_next_eval)) * sep2 * (eopd + ld(lk->h2_eval) + delta * ld(lk->h1_next_eval)));
     }
     // - Z_H(z) * sum_k z^(kn) t_(k+1)  (linearisation.cu:250-292)
     {
@@ -650,13 +795,13 @@ int prove_impl(pnp_ctx *ctx, const CircuitC *cs, int device_ptrs, ProofC *out) {
     Fr saw = tr.challenge_scalar("aggregate_witness");
     {
         const uint64_t *awp[11] = {lin, pk.left_sigma_coeffs, pk.right_sigma_coeffs,
-                                   pk.out_sigma_coeffs, f_poly, zero_n /* h2 */, table_poly,
+                                   pk.out_sigma_coeffs, f_poly, h2_poly, table_poly,
                                    wpoly[0], wpoly[1], wpoly[2], wpoly[3]};
         LinArgs oa;
         oa.k = 0;
         Fr p = Fr::one();
         for (int k = 0; k < 11; k++) {
-            bool skip = (k == 4 && f_zero) || k == 5 || (k == 6 && table_zero);
+            bool skip = (k == 4 && f_zero) || (k == 5 && h_zero) || (k == 6 && table_zero);
             if (!skip) {
                 oa.p[oa.k] = k == 0 ? awp[k] : awp[k] + 4 * q0;  // lin is range-local
                 oa.s[oa.k] = p;
@@ -668,13 +813,12 @@ int prove_impl(pnp_ctx *ctx, const CircuitC *cs, int device_ptrs, ProofC *out) {
         div_linear_range(ctx, comb, len, zc, dist);
     }
     {
-        const uint64_t *sawp[7] = {z_poly, wpoly[0], wpoly[1], wpoly[3], zero_n /* h1 */, z2_poly,
-                                   table_poly};
+        const uint64_t *sawp[7] = {z_poly, wpoly[0], wpoly[1], wpoly[3], h1_poly, z2_poly, table_poly};
         LinArgs oa;
         oa.k = 0;
         Fr p = Fr::one();
         for (int k = 0; k < 7; k++) {
-            bool skip = k == 4 || (k == 6 && table_zero);
+            bool skip = (k == 4 && h_zero) || (k == 6 && table_zero);
             if (!skip) {
                 oa.p[oa.k] = sawp[k] + 4 * q0;
                 oa.s[oa.k] = p;

@@ -1,5 +1,6 @@
 // transcript.cpp — see transcript.h for the reference mapping.
 #include "transcript.h"
+#include <vector>
 #include <string.h>
 
 namespace pnp {
@@ -147,6 +148,18 @@ void Transcript::append_pi(const char *label, const uint64_t pi_canon[4], uint64
     memcpy(b + 8, &pos, 8);
     memcpy(b + 16, c, 32);
     append_message(label, b, 48);
+}
+
+void Transcript::append_pis(const char *label, uint64_t k, const uint64_t *pos, const uint64_t *vals_canon) {
+    std::vector<uint8_t> b(8 + 40 * k);
+    memcpy(b.data(), &k, 8);
+    for (uint64_t i = 0; i < k; i++) {
+        uint64_t c[4];
+        to_u64_limbs(from_mont(to_mont(from_u64_limbs<FrP>(vals_canon + 4 * i))), c);
+        memcpy(b.data() + 8 + 40 * i, pos + i, 8);
+        memcpy(b.data() + 16 + 40 * i, c, 32);
+    }
+    append_message(label, b.data(), b.size());
 }
 
 }  // namespace pnp

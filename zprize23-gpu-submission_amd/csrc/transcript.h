@@ -18,6 +18,10 @@ class Transcript {
     // affine Montgomery point; (0, one) is the point at infinity
     void append_point(const char *label, const uint64_t x[6], const uint64_t y[6]);
     void append_pi(const char *label, const uint64_t pi_canon[4], uint64_t pos);
+    // PublicInputs (pi.rs:16-22) as its BTreeMap<usize, F>: u64 length, then
+    // (u64 position, 32-byte canonical value) per entry; positions strictly
+    // increasing, zero values already dropped (pi.rs:33-46)
+    void append_pis(const char *label, uint64_t k, const uint64_t *pos, const uint64_t *vals_canon);
     void challenge_bytes(const char *label, uint8_t *out, size_t len);
     Fr challenge_scalar(const char *label);
 

@@ -27,7 +27,8 @@ ERRORS = {-1: "PNP_E_ARG", -2: "PNP_E_DEVICE", -3: "PNP_E_NOKEY", -4: "PNP_E_ENV
 
 # exported symbols declared by include/pnp_plonk.h (checked by tests/test_abi.py)
 SYMBOLS = ("gen_proof", "pnp_last_error", "pnp_ctx_create", "pnp_ctx_destroy",
-           "pnp_load_prover_key", "pnp_load_commit_key", "pnp_prove", "pnp_last_stage_times",
+           "pnp_load_prover_key", "pnp_load_commit_key", "pnp_prove", "pnp_prove_ex",
+           "pnp_last_stage_times",
            "pnp_kernel_timing", "pnp_kernel_stats", "pnp_kernel_bytes", "pnp_set_msm_shard",
            "pnp_set_exchange_a2a",
            "pnp_sync", "pnp_ntt", "pnp_coset_lde8", "pnp_commit", "pnp_commit_ck", "pnp_poly_eval",
@@ -71,6 +72,8 @@ def load(path: str = LIB_PATH):
     lib.pnp_load_prover_key.argtypes = [vp, C.POINTER(abi.ProverKeyC), u64, i32]
     lib.pnp_load_commit_key.argtypes = [vp, C.POINTER(abi.CommitKeyC), u64, i32]
     lib.pnp_prove.argtypes = [vp, C.POINTER(abi.CircuitC), i32, C.POINTER(abi.ProofC)]
+    lib.pnp_prove_ex.argtypes = [vp, C.POINTER(abi.CircuitC), i32, u64, vp, vp, C.c_char_p,
+                                 C.POINTER(abi.ProofC)]
     lib.pnp_last_stage_times.argtypes = [vp, C.POINTER(C.c_double), C.POINTER(C.c_char_p), i32]
     lib.pnp_kernel_timing.argtypes = [vp, i32]
     lib.pnp_kernel_stats.argtypes = [vp, C.c_char_p, C.POINTER(C.c_double), C.POINTER(C.c_int)]
@@ -136,6 +139,19 @@ class Context:
     def prove(self, cs: abi.CircuitC, device_ptrs: bool) -> abi.ProofC:
         out = abi.ProofC()
         check(self.lib.pnp_prove(self.h, C.byref(cs), int(device_ptrs), C.byref(out)), "pnp_prove")
+        return out
+
+    def prove_ex(self, cs: abi.CircuitC, device_ptrs: bool, pis, label: bytes = b"Merkle tree"):
+        """pnp_prove_ex: pis = [(position, canonical value int)], any order."""
+        k = len(pis)
+        pos = (C.c_uint64 * max(k, 1))(*[p for p, _ in pis])
+        vals = (C.c_uint64 * max(4 * k, 1))()
+        for i, (_, v) in enumerate(pis):
+            for j in range(4):
+                vals[4 * i + j] = (v >> (64 * j)) & 0xFFFFFFFFFFFFFFFF
+        out = abi.ProofC()
+        check(self.lib.pnp_prove_ex(self.h, C.byref(cs), int(device_ptrs), k, pos, vals, label,
+                                    C.byref(out)), "pnp_prove_ex")
         return out
 
     def stage_times(self):
