@@ -112,6 +112,17 @@ void commit_affine_batch(pnp_ctx *ctx, const uint64_t *const *d_scalars, int B, 
 
 }  // namespace pnp
 
+hipStream_t pnp_ctx::side_stream() {
+    if (!stream_lo) {
+        int lo = 0, hi = 0;
+        PNP_HIP(hipDeviceGetStreamPriorityRange(&lo, &hi));  // lo = least priority
+        PNP_HIP(hipStreamCreateWithPriority(&stream_lo, hipStreamNonBlocking, lo));
+        for (hipEvent_t *e : {&ev_fork, &ev_w8, &ev_z8})
+            PNP_HIP(hipEventCreateWithFlags(e, hipEventDisableTiming));
+    }
+    return stream_lo;
+}
+
 uint64_t *pnp_ctx::buf(const std::string &name, size_t elems_fr) {
     auto &b = work[name];
     if (b.bytes < elems_fr * 32) b.alloc(elems_fr * 32);
@@ -161,6 +172,11 @@ void pnp_ctx_destroy(pnp_ctx *ctx) {
     }
     for (hipEvent_t e : ctx->msm.ev)
         if (e) (void)hipEventDestroy(e);
+    if (ctx->stream_lo) {
+        (void)hipStreamSynchronize(ctx->stream_lo);
+        (void)hipStreamDestroy(ctx->stream_lo);
+        for (hipEvent_t e : {ctx->ev_fork, ctx->ev_w8, ctx->ev_z8}) (void)hipEventDestroy(e);
+    }
     (void)hipStreamDestroy(ctx->stream);
     delete ctx;
 }

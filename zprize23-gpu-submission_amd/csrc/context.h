@@ -9,6 +9,11 @@
 struct pnp_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
+    // low-priority side stream for challenge-independent work overlapped with
+    // the MSMs (prover.cpp), created on first use, and its events
+    hipStream_t stream_lo = nullptr;
+    hipEvent_t ev_fork = nullptr, ev_w8 = nullptr, ev_z8 = nullptr;
+    hipStream_t side_stream();
     pnp::NttTables ntt;
     pnp::MsmWork msm;
     pnp::DevBuf scratch_a, scratch_b;

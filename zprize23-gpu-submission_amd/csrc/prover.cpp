@@ -180,6 +180,33 @@ int prove_impl(pnp_ctx *ctx, const CircuitC *cs, int device_ptrs, ProofC *out, c
     Timer tm(ctx);
     auto &nt = ctx->ntt;
     k_proof_marker(s);
+    // round-4 distribution (pnp_set_exchange_a2a, fixed at key load): this
+    // rank's coset blocks [mb0, mb0 + nb) and coefficient range [q0, q0 + len)
+    const int world = ctx->msm.world;
+    if (ctx->pk_blk_world != world || ctx->pk_blk_rank != ctx->msm.rank) {
+        set_error("sharding changed after pnp_load_prover_key");
+        return PNP_E_ARG;
+    }
+    const int mb0 = ctx->pk_mb0, nb = ctx->pk_nb;
+    const bool dist = nb < 8;
+    const uint64_t NB = (uint64_t)nb * n;
+    uint64_t q0 = 0, q1 = n;
+    if (dist) msm_point_range(n, ctx->msm.rank, world, q0, q1);
+    const uint64_t len = q1 - q0;
+    // The round-4 coset LDEs of the wires and of z depend on no challenge:
+    // they run on a low-priority side stream beside the round-1 / round-3
+    // MSMs, whose sort, merge and tree phases leave most SIMDs idle, and the
+    // quotient waits for them (PNP_NO_OVERLAP=1: in round 4, as before).
+    static const bool overlap = getenv("PNP_NO_OVERLAP") == nullptr;
+    hipStream_t s_lo = overlap ? ctx->side_stream() : s;
+    auto lde_on = [&](hipStream_t st, const uint64_t *coeffs, uint64_t *dst) {
+        lde_blocks(nt, coeffs, dst, lg, mb0, nb, st);
+    };
+    auto fork = [&]() {
+        if (!overlap) return;
+        PNP_HIP(hipEventRecord(ctx->ev_fork, s));
+        PNP_HIP(hipStreamWaitEvent(s_lo, ctx->ev_fork, 0));
+    };
 
     // ---------------- inputs: padded witness evaluations (pad_poly)
     uint64_t *wsc[4], *wpoly[4];
@@ -210,6 +237,11 @@ int prove_impl(pnp_ctx *ctx, const CircuitC *cs, int device_ptrs, ProofC *out, c
         ntt_run(nt, wpoly[j], lg, true, false, s);
     }
     tm.mark("r1_intt");
+    uint64_t *w8buf[4];
+    for (int j = 0; j < 4; j++) w8buf[j] = ctx->buf("w8_" + std::to_string(j), NB);
+    fork();
+    for (int j = 0; j < 4; j++) lde_on(s_lo, wpoly[j], w8buf[j]);
+    if (overlap) PNP_HIP(hipEventRecord(ctx->ev_w8, s_lo));
     CommitmentC *wc[4] = {&out->a_comm, &out->b_comm, &out->c_comm, &out->d_comm};
     {
         const uint64_t *sc[4] = {wpoly[0], wpoly[1], wpoly[2], wpoly[3]};
@@ -314,6 +346,10 @@ int prove_impl(pnp_ctx *ctx, const CircuitC *cs, int device_ptrs, ProofC *out, c
     PNP_HIP(hipMemcpyAsync(z_poly, num, 32 * n, hipMemcpyDeviceToDevice, s));
     ntt_run(nt, z_poly, lg, true, false, s);
     tm.mark("r3_z");
+    uint64_t *z8 = ctx->buf("z8", NB);
+    fork();
+    lde_on(s_lo, z_poly, z8);
+    if (overlap) PNP_HIP(hipEventRecord(ctx->ev_z8, s_lo));
     commit_affine(ctx, z_poly, n, &out->z_comm);
     append_comm(tr, "z", out->z_comm);
     // lookup grand product (permutation/mod.rs:754-822)
@@ -340,19 +376,6 @@ int prove_impl(pnp_ctx *ctx, const CircuitC *cs, int device_ptrs, ProofC *out, c
     // public input poly (pi.cu:11-15)
     // = iNTT of the evaluations v * e_pos, in closed form: v n^-1 w^(-pos j)
     const Fr n_inv = inverse(fr_from_u64(n));
-    // round-4 distribution (pnp_set_exchange_a2a, fixed at key load): this
-    // rank's coset blocks [mb0, mb0 + nb) and coefficient range [q0, q0 + len)
-    const int world = ctx->msm.world;
-    if (ctx->pk_blk_world != world || ctx->pk_blk_rank != ctx->msm.rank) {
-        set_error("sharding changed after pnp_load_prover_key");
-        return PNP_E_ARG;
-    }
-    const int mb0 = ctx->pk_mb0, nb = ctx->pk_nb;
-    const bool dist = nb < 8;
-    const uint64_t NB = (uint64_t)nb * n;
-    uint64_t q0 = 0, q1 = n;
-    if (dist) msm_point_range(n, ctx->msm.rank, world, q0, q1);
-    const uint64_t len = q1 - q0;
     const bool closed = ctx->pk_std_coset;  // L1 (and one PI) on the coset in closed form
     const bool pi_closed = closed && pi_pos.size() == 1;
     uint64_t *pi_poly = nullptr;
@@ -398,14 +421,9 @@ int prove_impl(pnp_ctx *ctx, const CircuitC *cs, int device_ptrs, ProofC *out, c
 
     QuotArgs q;
     // coset evaluations in block layout, this rank's blocks only
-    auto lde = [&](const uint64_t *coeffs, uint64_t *dst) { lde_blocks(nt, coeffs, dst, lg, mb0, nb, s); };
-    for (int j = 0; j < 4; j++) {
-        uint64_t *w8 = ctx->buf("w8_" + std::to_string(j), NB);
-        lde(wpoly[j], w8);
-        q.w8[j] = w8;
-    }
-    uint64_t *z8 = ctx->buf("z8", NB), *z28 = ctx->buf("z28", NB);
-    lde(z_poly, z8);
+    auto lde = [&](const uint64_t *coeffs, uint64_t *dst) { lde_on(s, coeffs, dst); };
+    for (int j = 0; j < 4; j++) q.w8[j] = w8buf[j];
+    uint64_t *z28 = ctx->buf("z28", NB);
     q.z8 = z8;
     q.pi8 = nullptr;
     q.l18 = q.l1v = q.pinv = nullptr;
@@ -490,6 +508,10 @@ int prove_impl(pnp_ctx *ctx, const CircuitC *cs, int device_ptrs, ProofC *out, c
     q.eopd = eps * q.opd;
     q.sep2 = lsep * lsep;
     q.sep3 = q.sep2 * lsep;
+    if (overlap) {  // the side-stream LDEs of the wires and z
+        PNP_HIP(hipStreamWaitEvent(s, ctx->ev_w8, 0));
+        PNP_HIP(hipStreamWaitEvent(s, ctx->ev_z8, 0));
+    }
     tm.mark("r4_lde");
     uint64_t *t_blk = ctx->buf("t_blk", NB);
     hipEvent_t qe0 = nullptr;
