@@ -249,3 +249,32 @@ def test_synth_srs_and_coset_consts(ctx):
     vals = from_dev(r)
     assert all(from_limbs(v) < R_MOD for v in vals[:256])
     assert len({tuple(v) for v in vals}) == 4096
+
+
+@pytest.mark.parametrize("c", [13, 20])
+def test_msm_folded_equal_pieces_exact_fallback(c, monkeypatch):
+    """Every point the same P and every scalar the same s: each window puts
+    all n entries into one bucket, split across many accumulate lanes whose
+    pieces are equal multiples of P, so the radix-2^29 merge meets equal
+    operands (an exceptional addition, ec29.cuh) and the group must take the
+    exact 32-bit fallback (reduce_group_exact); result n s P vs the oracle."""
+    import pnp
+    monkeypatch.setenv("PNP_FOLD_C", str(c))
+    ctx = pnp.Context(0)
+    try:
+        n = 6000
+        rng = np.random.default_rng(c + 1)
+        lib = oracle()
+        tau = rand_fr_mont_arr(rng, 1)
+        pts = np.zeros((n, 12), dtype=np.uint64)
+        lib.or_srs(vp(pts), 2, vp(tau))
+        pts[:] = pts[1]
+        sc = rand_fr_mont_arr(rng, 1).repeat(n, axis=0)
+        exp = np.zeros(12, dtype=np.uint64)
+        lib.or_commit(vp(pts), vp(sc), n, vp(exp))
+        ctx.kernel_timing(True)
+        assert (_commit_ck(ctx, pts, sc) == exp).all()
+        assert ctx.kernel_bytes("msm_exact_fallback") >= 1  # the fallback really ran
+        ctx.kernel_timing(False)
+    finally:
+        ctx.close()

@@ -38,7 +38,7 @@
 #include <algorithm>
 #include "msm_internal.h"
 #include "ec.cuh"
-#include "field29.cuh"
+#include "ec29.cuh"
 
 namespace pnp {
 
@@ -444,20 +444,7 @@ __global__ __launch_bounds__(256) void k_accumulate_flat(const uint64_t *points,
 
 // ---- radix-2^29 accumulation (field29.cuh) over the folded table in F29 form
 // (28 u32 per point: x, y in R = 2^406 Montgomery, < 2q)
-__device__ __forceinline__ F29 load29(const uint32_t *p) {
-    const uint4 *q = reinterpret_cast<const uint4 *>(p);
-    uint4 a = q[0], b = q[1], c = q[2];
-    uint2 d = *reinterpret_cast<const uint2 *>(p + 12);
-    F29 r;
-    r.l[0] = a.x; r.l[1] = a.y; r.l[2] = a.z; r.l[3] = a.w;
-    r.l[4] = b.x; r.l[5] = b.y; r.l[6] = b.z; r.l[7] = b.w;
-    r.l[8] = c.x; r.l[9] = c.y; r.l[10] = c.z; r.l[11] = c.w;
-    r.l[12] = d.x; r.l[13] = d.y;
-    return r;
-}
-struct Xyzz29 {
-    F29 x, y, zz, zzz;
-};
+// (load29, Xyzz29: ec29.cuh)
 // P += (x2, y2), madd-2008-s.  Bounds (see field29.cuh): products < 2^382,
 // stored coordinates < 2^389, every product input < 2^391 (Y3 < 2^382 comes
 // from mul2_29).  No equal /
@@ -479,27 +466,8 @@ __device__ __forceinline__ void madd29(Xyzz29 &p, const F29 &x2, const F29 &y2) 
     p.y = y3;
 }
 // Pieces leave the accumulation in raw radix-2^29 form (56 u32 per XYZZ
-// point, 4 x 14 limbs): the conversion to R384 (4 products) happens once per
-// piece in k_merge_pieces29, not on the divergent boundary path of this loop.
-__device__ __forceinline__ void store_f29(uint32_t *dst, const F29 &a) {
-    uint4 *q = reinterpret_cast<uint4 *>(dst);
-    q[0] = make_uint4(a.l[0], a.l[1], a.l[2], a.l[3]);
-    q[1] = make_uint4(a.l[4], a.l[5], a.l[6], a.l[7]);
-    q[2] = make_uint4(a.l[8], a.l[9], a.l[10], a.l[11]);
-    *reinterpret_cast<uint2 *>(dst + 12) = make_uint2(a.l[12], a.l[13]);
-}
-// ZZ is a product output (< 2^382 < 3q) with normalised limbs: zero mod q
-// iff it equals 0, q or 2q limb for limb
-__device__ __forceinline__ bool zero29(const F29 &v) {
-    uint32_t z = 0, a = 0, b = 0;
-#pragma unroll
-    for (int i = 0; i < 14; i++) {
-        z |= v.l[i];
-        a |= v.l[i] ^ F29_Q[i];
-        b |= v.l[i] ^ F29_Q2[i];
-    }
-    return z == 0 || a == 0 || b == 0;
-}
+// point, 4 x 14 limbs, ec29.cuh) and stay in it through the merge and the
+// reduction tree (msm_reduce.hip); only the roots are converted to R384.
 // raw store; false when ZZ = 0 mod q (a degenerate step in the piece)
 __device__ __forceinline__ bool store29(uint32_t *dst, const Xyzz29 &p) {
     store_f29(dst, p.x);
@@ -854,7 +822,13 @@ static void accumulate_group(MsmWork &wk, MsmGroup &gb, const GroupPlan &gp, con
         hipLaunchKernelGGL(k_accumulate_redo, dim3((uint32_t)((nthr + 63) / 64)), dim3(64), 0, s, t29,
                            sorted, bstart, WB, S, bk29, head, tail, redo, nredo);
         PNP_HIP(hipGetLastError());
-        msm_merge_pieces29(bstart, WB, S, (uint32_t)(nent / WB / S + 1), bk29, head, tail, bk, s);
+        // every bucket into bk29 (in place, F29), reduced by msm_reduce29
+        need(gb.exc, 16);
+        PNP_HIP(hipMemsetAsync(gb.exc.p, 0, 4, s));
+        gb.S = S;
+        gb.pieces = (uint32_t)(nent / WB / S + 1);
+        gb.nthr = nthr;
+        msm_merge_pieces29(bstart, WB, S, gb.pieces, bk29, head, tail, static_cast<uint32_t *>(gb.exc.p), s);
     } else {
         need(gb.seg, nthr * 2 * 24 * 8);
         uint64_t *head = gb.seg.u64(), *tail = head + nthr * 24;
@@ -871,9 +845,26 @@ static void accumulate_group(MsmWork &wk, MsmGroup &gb, const GroupPlan &gp, con
     }
 }
 
-static const uint64_t *reduce_group(MsmGroup &gb, const GroupPlan &gp, const MsmCfg &g, hipStream_t s) {
+static const uint64_t *reduce_group(MsmGroup &gb, const GroupPlan &gp, const MsmCfg &g, hipStream_t s,
+                                    bool folded) {
     const uint64_t WB = (uint64_t)gp.nv * g.NB;
     uint64_t *bk = gb.buckets.u64();
+    if (folded)  // radix-2^29 buckets in gb.seg, the tree in gb.buckets
+        return msm_reduce29(static_cast<const uint32_t *>(gb.seg.p), (uint64_t)gp.nv, g.NB,
+                            reinterpret_cast<uint32_t *>(bk), static_cast<uint32_t *>(gb.exc.p), s);
+    return msm_reduce(bk, (uint64_t)gp.nv, g.NB, bk + WB * 24, s);
+}
+
+// the exact 32-bit merge + reduction of a folded group whose F29 pass met an
+// exceptional addition (equal / opposite operands: repeated bases, crafted
+// scalars); same inputs, left untouched by the F29 pass
+static const uint64_t *reduce_group_exact(MsmGroup &gb, const GroupPlan &gp, const MsmCfg &g, hipStream_t s) {
+    const uint64_t WB = (uint64_t)gp.nv * g.NB;
+    uint64_t *bk = gb.buckets.u64();
+    const uint32_t *bk29 = static_cast<const uint32_t *>(gb.seg.p);
+    const uint32_t *head = bk29 + 56 * WB, *tail = head + 56 * gb.nthr;
+    msm_merge_pieces29_exact(static_cast<const uint32_t *>(gb.offsets.p), WB, gb.S, gb.pieces, bk29, head, tail,
+                             bk, s);
     return msm_reduce(bk, (uint64_t)gp.nv, g.NB, bk + WB * 24, s);
 }
 
@@ -945,7 +936,7 @@ static void msm_local_batch(MsmWork &wk, const uint64_t *d_points, const uint64_
     if (ng == 1) {
         sort_group(wk, wk.grp[0], keys, gp[0], g, s);
         accumulate_group(wk, wk.grp[0], gp[0], g, pts, table, s);
-        res[0] = reduce_group(wk.grp[0], gp[0], g, s);
+        res[0] = reduce_group(wk.grp[0], gp[0], g, s, folded);
     } else {
         if (!wk.s2) PNP_HIP(hipStreamCreateWithFlags(&wk.s2, hipStreamNonBlocking));
         hipEvent_t evD = ev_get(wk, 0), evS1 = ev_get(wk, 1), evA0 = ev_get(wk, 2), evR0 = ev_get(wk, 3);
@@ -957,19 +948,28 @@ static void msm_local_batch(MsmWork &wk, const uint64_t *d_points, const uint64_
         accumulate_group(wk, wk.grp[0], gp[0], g, pts, table, s);
         PNP_HIP(hipEventRecord(evA0, s));
         PNP_HIP(hipStreamWaitEvent(wk.s2, evA0, 0));
-        res[0] = reduce_group(wk.grp[0], gp[0], g, wk.s2);
+        res[0] = reduce_group(wk.grp[0], gp[0], g, wk.s2, folded);
         PNP_HIP(hipEventRecord(evR0, wk.s2));
         PNP_HIP(hipStreamWaitEvent(s, evS1, 0));
         accumulate_group(wk, wk.grp[1], gp[1], g, pts, table, s);
-        res[1] = reduce_group(wk.grp[1], gp[1], g, s);
+        res[1] = reduce_group(wk.grp[1], gp[1], g, s, folded);
         PNP_HIP(hipStreamWaitEvent(s, evR0, 0));
     }
     std::vector<uint64_t> win[2];
+    uint32_t exc[2] = {0, 0};
     for (int k = 0; k < ng; k++) {
         win[k].resize((size_t)gp[k].nv * 24);
         PNP_HIP(hipMemcpyAsync(win[k].data(), res[k], win[k].size() * 8, hipMemcpyDeviceToHost, s));
+        if (folded) PNP_HIP(hipMemcpyAsync(&exc[k], wk.grp[k].exc.p, 4, hipMemcpyDeviceToHost, s));
     }
     PNP_HIP(hipStreamSynchronize(s));
+    for (int k = 0; k < ng; k++) {
+        if (!exc[k]) continue;
+        if (wk.timer) wk.timer->credit("msm_exact_fallback", 1);
+        res[k] = reduce_group_exact(wk.grp[k], gp[k], g, s);
+        PNP_HIP(hipMemcpyAsync(win[k].data(), res[k], win[k].size() * 8, hipMemcpyDeviceToHost, s));
+        PNP_HIP(hipStreamSynchronize(s));
+    }
     if (wk.timer) wk.timer->collect();
     for (int b = 0; b < B; b++) put_xyzz(Xyzz::inf(), h_xyzz + 24 * b);
     for (int k = 0; k < ng; k++) {

@@ -33,11 +33,16 @@ inline MsmCfg msm_cfg(uint64_t n, int c = 0, bool folded = false) {
 void msm_merge_pieces(const uint32_t *offs, int nch, uint64_t U, uint32_t S, uint32_t pieces,
                       const uint64_t *head, const uint64_t *tail, uint64_t *bk, hipStream_t s);
 
-// the same over raw radix-2^29 pieces (folded layout, 56 u32 each), bk29 =
-// buckets inside one lane's segment; writes every bucket of bk (R384)
-void msm_merge_pieces29(const uint32_t *offs, uint64_t U, uint32_t S, uint32_t pieces,
-                        const uint32_t *bk29, const uint32_t *head, const uint32_t *tail, uint64_t *bk,
-                        hipStream_t s);
+// the same over raw radix-2^29 pieces (folded layout, 56 u32 each, ec29.cuh):
+// bk29 holds the buckets inside one lane's segment on entry and EVERY bucket
+// (F29, infinity = zero limbs) on exit
+// (an equal / opposite pair of operands sets *exc: see msm_reduce29)
+void msm_merge_pieces29(const uint32_t *offs, uint64_t U, uint32_t S, uint32_t pieces, uint32_t *bk29,
+                        const uint32_t *head, const uint32_t *tail, uint32_t *exc, hipStream_t s);
+// exact fallback: the same pieces summed in 32-bit Fq into bk (R384)
+void msm_merge_pieces29_exact(const uint32_t *offs, uint64_t U, uint32_t S, uint32_t pieces,
+                              const uint32_t *bk29, const uint32_t *head, const uint32_t *tail, uint64_t *bk,
+                              hipStream_t s);
 
 // Sum_b (b+1) * B_b for each of `nwin` consecutive groups of NB XYZZ buckets
 // (bk[0 .. nwin*NB), NB a power of two); `scratch` must hold 72*nwin*NB u64.
@@ -45,5 +50,12 @@ void msm_merge_pieces29(const uint32_t *offs, uint64_t U, uint32_t S, uint32_t p
 
 const uint64_t *msm_reduce(const uint64_t *bk, uint64_t nwin, int NB, uint64_t *scratch,
                            hipStream_t s);
+// the same over radix-2^29 buckets (56 u32 each); `scratch` must hold
+// 126 * nwin * NB + 48 * nwin u32 (NB >= 4); results R384.  *exc is set when
+// an addition met equal or opposite operands (never for random inputs): the
+// results are then wrong and the caller redoes the group with
+// msm_merge_pieces29_exact + msm_reduce (32-bit, exact)
+const uint64_t *msm_reduce29(const uint32_t *bk29, uint64_t nwin, int NB, uint32_t *scratch, uint32_t *exc,
+                             hipStream_t s);
 
 }  // namespace pnp

@@ -17,7 +17,7 @@
 // sum.  One launch per level, one lane per node.
 #include "msm_internal.h"
 #include "ec.cuh"
-#include "field29.cuh"
+#include "ec29.cuh"
 
 namespace pnp {
 
@@ -126,33 +126,64 @@ void msm_merge_pieces(const uint32_t *offs, int nch, uint64_t U, uint32_t S, uin
     PNP_HIP(hipGetLastError());
 }
 
-// Folded layout: the pieces are raw radix-2^29 XYZZ points (56 u32, see
-// msm.hip store29); a bucket inside one lane's segment is bk29[u], else
-// tail29[t0] + head29[t0+1] + ... + head29[t1].  Every piece is converted to
-// R384 here; every non-empty bucket is written to bk, empty ones as infinity.
-__device__ __forceinline__ F29 ld29(const uint32_t *p) {
-    const uint4 *q = reinterpret_cast<const uint4 *>(p);
-    uint4 a = q[0], b = q[1], c = q[2];
-    uint2 d = *reinterpret_cast<const uint2 *>(p + 12);
-    F29 r;
-    r.l[0] = a.x; r.l[1] = a.y; r.l[2] = a.z; r.l[3] = a.w;
-    r.l[4] = b.x; r.l[5] = b.y; r.l[6] = b.z; r.l[7] = b.w;
-    r.l[8] = c.x; r.l[9] = c.y; r.l[10] = c.z; r.l[11] = c.w;
-    r.l[12] = d.x; r.l[13] = d.y;
-    return r;
-}
-__device__ __forceinline__ Xyzz piece29(const uint32_t *p) {
-    Xyzz r;
-    r.x = to_fq32(ld29(p));
-    r.y = to_fq32(ld29(p + 14));
-    r.zz = to_fq32(ld29(p + 28));
-    r.zzz = to_fq32(ld29(p + 42));
-    return r;
-}
+// Folded layout: the pieces are raw radix-2^29 XYZZ points (56 u32, msm.hip
+// store29) and stay in radix 2^29 (ec29.cuh: shorter dependent chains than
+// the 32-bit Fq products, no per-piece conversion).  A bucket inside one
+// lane's segment is already bk29[u]; else tail29[t0] + head29[t0+1] + ... +
+// head29[t1] is written to bk29[u] (in place); empty buckets become infinity
+// (zero limbs).
 __global__ __launch_bounds__(256) void k_merge_pieces29(const uint32_t *offs, uint64_t U, uint32_t S,
-                                                        int G, const uint32_t *bk29,
-                                                        const uint32_t *head, const uint32_t *tail,
-                                                        uint64_t *bk) {
+                                                        int G, uint32_t *bk29, const uint32_t *head,
+                                                        const uint32_t *tail, uint32_t *exc) {
+    __shared__ uint32_t lds[256 * 56];
+    const uint64_t g = (blockIdx.x * (uint64_t)blockDim.x + threadIdx.x) / G;
+    const int j = threadIdx.x % G;
+    bool live = false;  // a bucket split across lanes: this group sums its pieces
+    Xyzz29 acc = inf29();
+    if (g < U) {
+        const uint32_t s0 = offs[g], e0 = offs[g + 1];
+        if (s0 == e0) {
+            if (j == 0) store_xyzz29(bk29 + 56 * g, inf29());
+        } else {
+            const uint32_t t0 = s0 / S, t1 = (e0 - 1) / S;
+            if (t0 != t1) {
+                live = true;
+#pragma unroll 1
+                for (uint32_t k = j; k <= t1 - t0; k += G)
+                    acc = xadd29_inf(acc, load_xyzz29(k == 0 ? tail + 56ULL * t0 : head + 56ULL * (t0 + k)), exc);
+            }
+        }
+    }
+    uint32_t *mine = lds + 56 * threadIdx.x;
+    for (int h = G / 2; h >= 1; h /= 2) {
+        store_xyzz29(mine, acc);
+        __syncthreads();
+        if (live && j < h) acc = xadd29_inf(acc, load_xyzz29(mine + 56 * h), exc);
+        __syncthreads();
+    }
+    if (live && j == 0) store_xyzz29(bk29 + 56 * g, acc);
+}
+
+void msm_merge_pieces29(const uint32_t *offs, uint64_t U, uint32_t S, uint32_t pieces, uint32_t *bk29,
+                        const uint32_t *head, const uint32_t *tail, uint32_t *exc, hipStream_t s) {
+    int G = 1;
+    while (G < 8 && (uint32_t)G * 8 <= pieces) G *= 2;
+    const uint64_t blocks = (U * G + 255) / 256;
+    hipLaunchKernelGGL(k_merge_pieces29, dim3((uint32_t)blocks), dim3(256), 0, s, offs, U, S, G, bk29, head,
+                       tail, exc);
+    PNP_HIP(hipGetLastError());
+}
+
+// The exact fallback of the F29 merge + tree (an exceptional addition was
+// flagged): every piece converted to R384 and summed with ec.cuh's add; a
+// bucket inside one lane's segment is bk29[u] as the accumulation left it
+// (the F29 merge writes only split and empty buckets).  Writes bk (R384) for
+// the 32-bit msm_reduce.
+__device__ __forceinline__ Xyzz piece29(const uint32_t *p) { return to32(load_xyzz29(p)); }
+__global__ __launch_bounds__(256) void k_merge_pieces29_exact(const uint32_t *offs, uint64_t U, uint32_t S,
+                                                              int G, const uint32_t *bk29,
+                                                              const uint32_t *head, const uint32_t *tail,
+                                                              uint64_t *bk) {
     __shared__ uint64_t lds[256 * 24];
     const uint64_t g = (blockIdx.x * (uint64_t)blockDim.x + threadIdx.x) / G;
     const int j = threadIdx.x % G;
@@ -184,15 +215,89 @@ __global__ __launch_bounds__(256) void k_merge_pieces29(const uint32_t *offs, ui
     if (live && j == 0) store_xyzz(bk + 24 * g, acc);
 }
 
-void msm_merge_pieces29(const uint32_t *offs, uint64_t U, uint32_t S, uint32_t pieces,
-                        const uint32_t *bk29, const uint32_t *head, const uint32_t *tail, uint64_t *bk,
-                        hipStream_t s) {
+void msm_merge_pieces29_exact(const uint32_t *offs, uint64_t U, uint32_t S, uint32_t pieces,
+                              const uint32_t *bk29, const uint32_t *head, const uint32_t *tail, uint64_t *bk,
+                              hipStream_t s) {
     int G = 1;
     while (G < 8 && (uint32_t)G * 8 <= pieces) G *= 2;
     const uint64_t blocks = (U * G + 255) / 256;
-    hipLaunchKernelGGL(k_merge_pieces29, dim3((uint32_t)blocks), dim3(256), 0, s, offs, U, S, G, bk29,
+    hipLaunchKernelGGL(k_merge_pieces29_exact, dim3((uint32_t)blocks), dim3(256), 0, s, offs, U, S, G, bk29,
                        head, tail, bk);
     PNP_HIP(hipGetLastError());
+}
+
+// radix-2^29 tree: the (S, T, D) nodes of k_tree_leafw / k_tree_level, 168
+// u32 per node
+template <int LW>
+__global__ __launch_bounds__(256) void k_tree_leafw29(const uint32_t *bk, uint64_t nout, uint32_t *out,
+                                                      uint32_t *exc) {
+    uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    if (t >= nout) return;
+    const uint32_t *b = bk + 56ULL * LW * t;
+    Xyzz29 S = load_xyzz29(b + 56 * (LW - 1)), T = S;
+#pragma unroll 1
+    for (int k = LW - 2; k >= 0; k--) {
+        S = xadd29_inf(S, load_xyzz29(b + 56 * k), exc);
+        T = xadd29_inf(T, S, exc);
+    }
+    uint32_t *o = out + 168 * t;
+    store_xyzz29(o, S);
+    store_xyzz29(o + 56, T);
+    Xyzz29 D = S;
+#pragma unroll 1
+    for (int k = 1; k < LW; k *= 2) D = xdbl29_inf(D);
+    store_xyzz29(o + 112, D);
+}
+
+__global__ __launch_bounds__(256) void k_tree_level29(const uint32_t *in, uint64_t nout, uint32_t *out,
+                                                      uint32_t *exc) {
+    const uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    if (t >= nout) return;
+    const int c = (int)blockIdx.y;
+    const uint32_t *L = in + 336 * t, *R = L + 168;
+    Xyzz29 r;
+    if (c == 0) {
+        r = xadd29_inf(load_xyzz29(L), load_xyzz29(R), exc);
+    } else if (c == 1) {
+        r = xadd29_inf(xadd29_inf(load_xyzz29(L + 56), load_xyzz29(R + 56), exc), load_xyzz29(R + 112), exc);
+    } else {
+        r = xdbl29_inf(xadd29_inf(load_xyzz29(L + 112), load_xyzz29(R + 112), exc));
+    }
+    store_xyzz29(out + 168 * t + 56 * c, r);
+}
+
+// the roots' T in R384 (the host's 24-u64 XYZZ)
+__global__ void k_tree_roots29(const uint32_t *in, uint64_t n, uint64_t *out) {
+    uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    if (t < n) store_xyzz(out + 24 * t, to32(load_xyzz29(in + 168 * t + 56)));
+}
+
+const uint64_t *msm_reduce29(const uint32_t *bk29, uint64_t nwin, int NB, uint32_t *scratch, uint32_t *exc,
+                             hipStream_t s) {
+    // leaves of PNP_LEAF_W buckets (pairs for the small windows of small MSMs)
+    const int LW = NB >= 2 * PNP_LEAF_W ? PNP_LEAF_W : 2;
+    if (NB < 2 * LW) {
+        set_error("msm_reduce29: %d buckets per window", NB);
+        throw Error(PNP_E_ARG);
+    }
+    uint64_t m = nwin * (uint64_t)NB / LW;
+    uint32_t *a = scratch, *b = scratch + 168 * m;
+    uint64_t *roots = reinterpret_cast<uint64_t *>(scratch + 252 * m);
+    const dim3 lgrid((uint32_t)((m + 255) / 256));
+    if (LW == 2)
+        hipLaunchKernelGGL(k_tree_leafw29<2>, lgrid, dim3(256), 0, s, bk29, m, a, exc);
+    else
+        hipLaunchKernelGGL(k_tree_leafw29<PNP_LEAF_W>, lgrid, dim3(256), 0, s, bk29, m, a, exc);
+    PNP_HIP(hipGetLastError());
+    while (m > nwin) {
+        m /= 2;
+        hipLaunchKernelGGL(k_tree_level29, dim3((uint32_t)((m + 255) / 256), 3), dim3(256), 0, s, a, m, b, exc);
+        PNP_HIP(hipGetLastError());
+        std::swap(a, b);
+    }
+    hipLaunchKernelGGL(k_tree_roots29, dim3((uint32_t)((nwin + 255) / 256)), dim3(256), 0, s, a, nwin, roots);
+    PNP_HIP(hipGetLastError());
+    return roots;
 }
 
 // ---------------------------------------------------------------- tree

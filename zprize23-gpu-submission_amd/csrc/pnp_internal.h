@@ -111,6 +111,9 @@ struct KernelTimer {
 // back to the exact path)
 struct MsmGroup {
     DevBuf counts, offsets, scan_tmp, ent, fkey, sorted, buckets, seg, redo;
+    DevBuf exc;  // folded: an F29 merge / tree addition met equal or opposite operands
+    uint32_t S = 0, pieces = 0;  // folded: accumulate segment length, pieces per bucket
+    uint64_t nthr = 0;           // folded: accumulate lanes (head / tail slots)
 };
 struct MsmWork {
     DevBuf digits;  // u32 keys of every (MSM, window, point)
