@@ -102,11 +102,11 @@ void commit_affine_batch(pnp_ctx *ctx, const uint64_t *const *d_scalars, int B, 
     std::vector<uint64_t> xyzz((size_t)B * 24);
     msm_run_batch(ctx->msm, ctx->ck_dev, d_scalars, B, n, xyzz.data(), ctx->stream,
                   commit_table(ctx, n), local);
+    std::vector<uint64_t> aff((size_t)B * 12);
+    xyzz_to_affine_batch_host(xyzz.data(), B, aff.data());
     for (int b = 0; b < B; b++) {
-        uint64_t aff[12];
-        xyzz_to_affine_host(xyzz.data() + 24 * b, aff);
-        memcpy(out[b]->x, aff, 48);
-        memcpy(out[b]->y, aff + 6, 48);
+        memcpy(out[b]->x, &aff[12 * b], 48);
+        memcpy(out[b]->y, &aff[12 * b + 6], 48);
     }
 }
 

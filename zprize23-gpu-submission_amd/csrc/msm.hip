@@ -1044,12 +1044,33 @@ void msm_run(MsmWork &wk, const uint64_t *d_points, const uint64_t *d_scalars, u
     msm_run_batch(wk, d_points, sc, 1, n, h_xyzz, s, table);
 }
 
-void xyzz_to_affine_host(const uint64_t *xyzz, uint64_t *aff12) {
-    Xyzz p = get_xyzz(xyzz);
-    Fq x, y;
-    xyzz_to_affine(p, x, y);
-    to_u64_limbs(x, aff12);
-    to_u64_limbs(y, aff12 + 6);
+void xyzz_to_affine_host(const uint64_t *xyzz, uint64_t *aff12) { xyzz_to_affine_batch_host(xyzz, 1, aff12); }
+
+// B results at once with ONE Fq inversion (Montgomery's trick over ZZ ZZZ;
+// 1/ZZ = ZZZ / (ZZ ZZZ), 1/ZZZ = ZZ / (ZZ ZZZ)): the host converts every
+// batch of commitments between two GPU phases, and a Fermat inversion costs
+// tens of microseconds on the CPU
+void xyzz_to_affine_batch_host(const uint64_t *xyzz, int B, uint64_t *aff12) {
+    std::vector<Xyzz> p(B);
+    std::vector<Fq> pre(B + 1);
+    pre[0] = Fq::one();
+    for (int b = 0; b < B; b++) {
+        p[b] = get_xyzz(xyzz + 24 * b);
+        pre[b + 1] = p[b].is_inf() ? pre[b] : pre[b] * (p[b].zz * p[b].zzz);
+    }
+    Fq inv = inverse(pre[B]);  // 1 / prod(ZZ ZZZ) over the finite points
+    for (int b = B - 1; b >= 0; b--) {
+        uint64_t *o = aff12 + 12 * b;
+        if (p[b].is_inf()) {  // (0, one) as the reference's to_affine (point.cu:29-36)
+            to_u64_limbs(Fq::zero(), o);
+            to_u64_limbs(Fq::one(), o + 6);
+            continue;
+        }
+        const Fq d = inv * pre[b];  // 1 / (ZZ ZZZ)
+        inv = inv * (p[b].zz * p[b].zzz);
+        to_u64_limbs(p[b].x * (p[b].zzz * d), o);
+        to_u64_limbs(p[b].y * (p[b].zz * d), o + 6);
+    }
 }
 
 }  // namespace pnp

@@ -150,6 +150,8 @@ void msm_point_range(uint64_t n, int rank, int world, uint64_t &p0, uint64_t &p1
 void msm_build_table(DevBuf &tab, const uint64_t *d_points, uint64_t n, int c, hipStream_t s);
 // host: XYZZ -> affine Montgomery (inf -> (0, one))
 void xyzz_to_affine_host(const uint64_t *xyzz, uint64_t *aff12);
+// B points (24 u64 each) -> B affine (12 u64 each), one inversion
+void xyzz_to_affine_batch_host(const uint64_t *xyzz, int B, uint64_t *aff12);
 
 // ---- poly / elementwise (poly.hip) ----
 void k_from_mont(uint64_t *d, uint64_t n, hipStream_t s);
