@@ -31,10 +31,13 @@ def test_general_gpu_equals_oracle(kind):
     exp = inp.oracle_proof()
     ctx = _ctx(inp)
     try:
+        ctx.kernel_timing(True)
         got = ctx.prove_ex(inp.circuit, False, pis_of(inp))
         assert _diff(got, exp) == []
         assert abi.proof_to_bytes(got) == abi.proof_to_bytes(exp)
         check_accepts(inp, got)
+        # every gate family keeps deg t < 6n: the 6-block round 4 suffices
+        assert ctx.kernel_bytes("quotient_all_blocks") == 0
     finally:
         ctx.close()
 

@@ -49,11 +49,35 @@ def test_gen_proof_general_lookup_and_selectors(lookup_rows, extra):
     ctx = pnp.Context(0)
     ctx.load_prover_key(inp.pk, inp.n, device_ptrs=False)
     ctx.load_commit_key(inp.ck, inp.n, device_ptrs=False)
+    ctx.kernel_timing(True)
     got = ctx.prove(inp.circuit, device_ptrs=False)
     assert _diff(got, exp) == []
     if lookup_rows:
         assert any(v != 0 for v in exp.f_comm.x)
         assert any(v != 0 for v in exp.h_1_comm.x)
+    # random q_m / q_lookup evaluations leave the circuit unsatisfied: the
+    # 6-block round 4 fails the identity at z and is redone on all 8 blocks
+    if extra:
+        assert ctx.kernel_bytes("quotient_all_blocks") == 1
+    ctx.close()
+
+
+@pytest.mark.parametrize("lg,seed", [(6, 4), (10, 5)])
+def test_gen_proof_unsatisfied_witness_all_blocks(lg, seed):
+    """Independent random witness / selectors / sigmas: the reference's t
+    pieces t_7 / t_8 are non-zero, so only the 8-block round 4 reproduces
+    them; the proof is still byte-identical to the oracle's."""
+    import pnp
+    inp = Inputs(lg, seed, satisfying=False)
+    exp = inp.oracle_proof()
+    assert any(v != 0 for v in exp.t_8_comm.x)
+    ctx = pnp.Context(0)
+    ctx.load_prover_key(inp.pk, inp.n, device_ptrs=False)
+    ctx.load_commit_key(inp.ck, inp.n, device_ptrs=False)
+    ctx.kernel_timing(True)
+    got = ctx.prove(inp.circuit, device_ptrs=False)
+    assert abi.proof_to_bytes(got) == abi.proof_to_bytes(exp)
+    assert ctx.kernel_bytes("quotient_all_blocks") == 1
     ctx.close()
 
 
@@ -64,11 +88,14 @@ def test_gen_proof_v2_resident(tmp_path):
     ctx = pnp.Context(0)
     ctx.load_prover_key(inp.pk, inp.n, device_ptrs=False)
     ctx.load_commit_key(inp.ck, inp.n, device_ptrs=False)
+    ctx.kernel_timing(True)
     for _ in range(2):  # resident keys are reused across proofs
         got = ctx.prove(inp.circuit, device_ptrs=False)
         assert abi.proof_to_bytes(got) == abi.proof_to_bytes(exp)
     names = [n for n, _ in ctx.stage_times()]
     assert "r4_quotient" in names
+    # satisfying circuit: round 4 on 6 coset blocks, identity check passed
+    assert ctx.kernel_bytes("quotient_all_blocks") == 0
     ctx.close()
 
 
@@ -130,9 +157,11 @@ def test_full_size_height15_properties():
     syn = Synthetic(ctx, 22, HEIGHT15_GATES, seed=5)
     ctx.load_prover_key(syn.pk, syn.n, device_ptrs=True)
     ctx.load_commit_key(syn.ck, syn.n, device_ptrs=True)
+    ctx.kernel_timing(True)
     p1 = ctx.prove(syn.cs, device_ptrs=True)
     p2 = ctx.prove(syn.cs, device_ptrs=True)
     assert abi.proof_to_bytes(p1) == abi.proof_to_bytes(p2)
+    assert ctx.kernel_bytes("quotient_all_blocks") == 0  # the 6-block round 4
     inf = lambda c: all(v == 0 for v in c.x)
     assert inf(p1.t_7_comm) and inf(p1.t_8_comm)
     assert not any(inf(getattr(p1, f"t_{k}_comm")) for k in range(1, 7))

@@ -347,19 +347,21 @@ __global__ void k_mul_table(uint64_t *d, const uint64_t *T, uint64_t N);
 __global__ void k_lde_twist(const uint64_t *in, const uint64_t *T, uint64_t *out, uint64_t n, uint64_t N);
 
 // DIF (natural -> bit-reversed) or DIT (bit-reversed -> natural) of size 2^lg
-// on each of the 2^(lg_total - lg) consecutive blocks of d
+// on each of `count` consecutive blocks of 2^lg elements (any count: the
+// round-4 coset blocks number 6 or 8)
 static void ntt_core(NttTables &t, uint64_t *d, uint32_t lg, bool inverse, bool dit, hipStream_t s,
-                     uint32_t lg_total = 0, const PassFuse &fz = PassFuse()) {
-    if (lg_total < lg) lg_total = lg;
-    const uint64_t N = 1ULL << lg_total;
+                     uint64_t count = 1, const PassFuse &fz = PassFuse()) {
+    const uint64_t N = count << lg;
     const uint64_t *tw = ntt_twiddles(t, lg, inverse, s);
-    if (lg_total < (uint32_t)LGTILE || (lg <= (uint32_t)LGTILE && lg_total == lg)) {
+    // LDS-tile passes need whole tiles (a tile holds TILE >> lg transforms when
+    // lg < LGTILE); otherwise one single-workgroup transform per block
+    if (N % TILE != 0 || (lg <= (uint32_t)LGTILE && count == 1)) {
         if (fz.src) {
             hipLaunchKernelGGL(k_lde_twist, dim3((uint32_t)((N + 255) / 256)), dim3(256), 0, s, fz.src,
                                fz.pre, d, fz.src_mask + 1, N);
             PNP_HIP(hipGetLastError());
         }
-        for (uint64_t b = 0; b < (1ULL << (lg_total - lg)); b++) {
+        for (uint64_t b = 0; b < count; b++) {
             if (dit)
                 hipLaunchKernelGGL(k_ntt_small<true>, dim3(1), dim3(NTT_THREADS), 0, s, d + 4 * (b << lg), tw, lg);
             else
@@ -412,9 +414,8 @@ static void ntt_core(NttTables &t, uint64_t *d, uint32_t lg, bool inverse, bool 
     }
 }
 
-static void dif(NttTables &t, uint64_t *d, uint32_t lg, bool inverse, hipStream_t s,
-                uint32_t lg_total = 0) {
-    ntt_core(t, d, lg, inverse, false, s, lg_total);
+static void dif(NttTables &t, uint64_t *d, uint32_t lg, bool inverse, hipStream_t s, uint64_t count = 1) {
+    ntt_core(t, d, lg, inverse, false, s, count);
 }
 
 static void bitrev(uint64_t *d, uint32_t lg, const Scale &sc, hipStream_t s, uint32_t nblocks = 1) {
@@ -490,7 +491,7 @@ void coset_lde8(NttTables &t, const uint64_t *in, uint64_t *out8, uint32_t lg_n,
     hipLaunchKernelGGL(k_lde_twist, dim3((uint32_t)((N + 255) / 256)), dim3(256), 0, s, in, T, out8,
                        n, N);
     PNP_HIP(hipGetLastError());
-    if (lg_n > 0) dif(t, out8, lg_n, false, s, lg_n + 3);
+    if (lg_n > 0) dif(t, out8, lg_n, false, s, 8);
     Scale sc{0, Fr::one(), nullptr, nullptr};
     bitrev(out8, lg_n + 3, sc, s);
 }
@@ -521,14 +522,11 @@ static const uint64_t *block_twist_table(NttTables &t, uint32_t lg_n, bool inver
     return p;
 }
 
-static uint32_t lg_blocks(int nb) {
-    uint32_t l = 0;
-    while ((1 << l) < nb) l++;
-    if ((1 << l) != nb) {
-        set_error("block count %d is not a power of two", nb);
+static void check_blocks(int m0, int nb) {
+    if (m0 < 0 || nb < 1 || m0 + nb > 8) {
+        set_error("coset blocks [%d, %d) outside [0, 8)", m0, m0 + nb);
         throw Error(PNP_E_ARG);
     }
-    return l;
 }
 
 // out[b n + brev(j)] = f(g w_8n^(8 j + m0 + b)), b < nb, for the n
@@ -542,7 +540,8 @@ void lde_blocks(NttTables &t, const uint64_t *in, uint64_t *out, uint32_t lg_n, 
     fz.src = in;
     fz.pre = block_twist_table(t, lg_n, false, s) + 4 * (uint64_t)m0 * n;
     fz.src_mask = n - 1;
-    ntt_core(t, out, lg_n, false, false, s, lg_n + lg_blocks(nb), fz);
+    check_blocks(m0, nb);
+    ntt_core(t, out, lg_n, false, false, s, (uint64_t)nb, fz);
 }
 
 __global__ void k_mul_table(uint64_t *d, const uint64_t *T, uint64_t N) {
@@ -557,7 +556,8 @@ void intt_blocks(NttTables &t, uint64_t *d, uint32_t lg_n, int m0, int nb, hipSt
     const uint64_t n = 1ULL << lg_n;
     PassFuse fz;
     fz.post = block_twist_table(t, lg_n, true, s) + 4 * (uint64_t)m0 * n;
-    ntt_core(t, d, lg_n, true, true, s, lg_n + lg_blocks(nb), fz);
+    check_blocks(m0, nb);
+    ntt_core(t, d, lg_n, true, true, s, (uint64_t)nb, fz);
 }
 
 // Coefficients of the 8n-point coset interpolant from the 8 twisted block
@@ -624,6 +624,86 @@ void t_combine(NttTables &t, const uint64_t *Y, uint64_t len, uint64_t q0, uint6
                        w[1], w[2], w[3], inv8n, t.coset_inv_hi.u64(), t.coset_inv_lo.u64(), gn[0], gn[1],
                        gn[2], gn[3], gn[4], gn[5], gn[6], gn[7]);
     PNP_HIP(hipGetLastError());
+}
+
+// Coefficients of t from M < 8 coset blocks m = 0 .. M-1 when deg t < M n
+// (prover.cpp: the quotient of a satisfying circuit has degree < 6n, its
+// pieces t_7, t_8 are zero).  From intt_blocks, Y_m[u] = n g^u
+// sum_(k<M) w_8^(m k) g^(k n) t_(k,u): a Vandermonde system in the nodes w_8^m,
+// solved per u with the host-inverted matrix A[k][m] = g^(-k n) V^-1[k][m] / n:
+//   t_(k,u) = g^-u sum_m A[k][m] Y_m[u]  -> out[k n + u]
+template <int M>
+struct CombineMat {
+    Fr a[M * M];
+};
+template <int M>
+__global__ __launch_bounds__(256) void k_t_combine_mat(const uint64_t *Y, uint64_t n, uint64_t *out,
+                                                       CombineMat<M> A, const uint64_t *chi,
+                                                       const uint64_t *clo) {
+    const uint64_t u = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    if (u >= n) return;
+    Fr y[M];
+#pragma unroll
+    for (int m = 0; m < M; m++) y[m] = load_fr(Y, m * n + u);
+    const Fr s0 = coset_pow(chi, clo, u);  // g^-u
+    for (int k = 0; k < M; k++) {
+        Fr acc = A.a[k * M] * y[0];
+#pragma unroll
+        for (int m = 1; m < M; m++) acc += A.a[k * M + m] * y[m];
+        store_fr(out, k * n + u, acc * s0);
+    }
+}
+
+template <int M>
+static void t_combine_mat(NttTables &t, const uint64_t *Y, uint64_t *out, uint32_t lg_n, hipStream_t s) {
+    const uint64_t n = 1ULL << lg_n;
+    // V[m][k] = w_8^(m k); Gauss-Jordan on [V | I] over Fr
+    const Fr w8 = host_root(3);
+    Fr V[M][2 * M];
+    for (int m = 0; m < M; m++)
+        for (int k = 0; k < M; k++) {
+            V[m][k] = pow_u64(w8, (uint64_t)(m * k));
+            V[m][M + k] = m == k ? Fr::one() : Fr::zero();
+        }
+    for (int c = 0; c < M; c++) {
+        int p = c;
+        while (V[p][c].is_zero()) p++;  // distinct nodes: V is invertible
+        if (p != c)
+            for (int j = 0; j < 2 * M; j++) std::swap(V[p][j], V[c][j]);
+        const Fr inv = pnp::inverse(V[c][c]);
+        for (int j = 0; j < 2 * M; j++) V[c][j] = V[c][j] * inv;
+        for (int r = 0; r < M; r++) {
+            if (r == c || V[r][c].is_zero()) continue;
+            const Fr f = V[r][c];
+            for (int j = 0; j < 2 * M; j++) V[r][j] = V[r][j] - f * V[c][j];
+        }
+    }
+    Fr nf = Fr::zero();
+    nf.v[0] = (uint32_t)n;
+    nf.v[1] = (uint32_t)(n >> 32);
+    const Fr ninv = pnp::inverse(to_mont(nf)), gni = pnp::inverse(pow_u64(host_gen(), n));
+    CombineMat<M> A;
+    Fr gk = ninv;  // g^(-k n) / n
+    for (int k = 0; k < M; k++) {
+        for (int m = 0; m < M; m++) A.a[k * M + m] = gk * V[k][M + m];
+        gk = gk * gni;
+    }
+    ntt_prepare_coset(t, s);
+    hipLaunchKernelGGL(k_t_combine_mat<M>, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, s, Y, n, out, A,
+                       t.coset_inv_hi.u64(), t.coset_inv_lo.u64());
+    PNP_HIP(hipGetLastError());
+}
+
+void t_combine_blocks(NttTables &t, const uint64_t *Y, int nb, uint64_t *out, uint32_t lg_n, hipStream_t s) {
+    switch (nb) {
+        case 5: t_combine_mat<5>(t, Y, out, lg_n, s); break;
+        case 6: t_combine_mat<6>(t, Y, out, lg_n, s); break;
+        case 7: t_combine_mat<7>(t, Y, out, lg_n, s); break;
+        case 8: t_combine(t, Y, 1ULL << lg_n, 0, out, lg_n, s); break;
+        default:
+            set_error("t_combine_blocks: %d blocks", nb);
+            throw Error(PNP_E_ARG);
+    }
 }
 
 // out[b n + brev(j)] = in[8 j + m0 + b], b < nb

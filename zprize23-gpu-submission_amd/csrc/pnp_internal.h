@@ -67,7 +67,7 @@ void ntt_run(NttTables &t, uint64_t *d, uint32_t lg, bool inverse, bool coset, h
 void coset_lde8(NttTables &t, const uint64_t *in, uint64_t *out8, uint32_t lg_n, hipStream_t s);
 
 // block layout of the 8n coset (point i = 8 j + m -> block m, index j):
-// LDE of n coefficients into blocks m0 .. m0+nb-1 (nb a power of two)
+// LDE of n coefficients into blocks m0 .. m0+nb-1 (any nb, m0 + nb <= 8)
 void lde_blocks(NttTables &t, const uint64_t *in, uint64_t *out, uint32_t lg_n, int m0, int nb,
                 hipStream_t s);
 // per block: unscaled inverse size-n DFT then twist by w_8n^(-m u)
@@ -75,6 +75,9 @@ void intt_blocks(NttTables &t, uint64_t *d, uint32_t lg_n, int m0, int nb, hipSt
 // 8-point inverse DFT across blocks + g^-i / (8n): coefficient chunks u in [q0, q0+len)
 void t_combine(NttTables &t, const uint64_t *Y, uint64_t len, uint64_t q0, uint64_t *out,
                uint32_t lg_n, hipStream_t s);
+// coefficient chunks t_1 .. t_nb (out[k n + u]) from blocks 0 .. nb-1 after
+// intt_blocks, for deg t < nb n (nb = 5 .. 8; 8 is t_combine)
+void t_combine_blocks(NttTables &t, const uint64_t *Y, int nb, uint64_t *out, uint32_t lg_n, hipStream_t s);
 void to_blocks(const uint64_t *in, uint64_t *out, uint32_t lg_n, int m0, int nb, hipStream_t s);
 
 // ---- live per-kernel timing with HIP events on the launching stream ----

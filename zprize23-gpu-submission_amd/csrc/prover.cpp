@@ -199,8 +199,24 @@ int prove_impl(pnp_ctx *ctx, const CircuitC *cs, int device_ptrs, ProofC *out, c
     // quotient waits for them (PNP_NO_OVERLAP=1: in round 4, as before).
     static const bool overlap = getenv("PNP_NO_OVERLAP") == nullptr;
     hipStream_t s_lo = overlap ? ctx->side_stream() : s;
+    // Round 4 on one GPU runs on the first 6 coset blocks, not all 8: the
+    // quotient of a satisfying circuit has degree < 6n (the largest term,
+    // q_arith q_hl a^5, has degree < 7n; the reference's t_7, t_8 are zero),
+    // so its values on 6n points of the coset already determine it — 25% fewer
+    // LDE transforms, quotient points and inverse transforms.  Round 5 checks
+    // the quotient identity at the challenge z (lin(z) = -r_0, the verifier's
+    // equation); a circuit the witness does not satisfy fails it and round 4
+    // is redone on all 8 blocks, exactly the reference's computation.
+    // (PNP_QUOT_BLOCKS = 6 .. 8; distributed round 4 keeps its 8 / world
+    // blocks per rank.)
+    static const int quot_blocks = [] {
+        const char *e = getenv("PNP_QUOT_BLOCKS");
+        int v = e ? atoi(e) : 6;
+        return v < 6 ? 6 : v > 8 ? 8 : v;
+    }();
+    int nbq = dist ? nb : quot_blocks;  // blocks this round-4 attempt covers
     auto lde_on = [&](hipStream_t st, const uint64_t *coeffs, uint64_t *dst) {
-        lde_blocks(nt, coeffs, dst, lg, mb0, nb, st);
+        lde_blocks(nt, coeffs, dst, lg, mb0, nbq, st);
     };
     auto fork = [&]() {
         if (!overlap) return;
@@ -406,458 +422,502 @@ int prove_impl(pnp_ctx *ctx, const CircuitC *cs, int device_ptrs, ProofC *out, c
     tm.mark("r3_z2_pi");
 
     // ---------------- round 4: quotient (gen_proof.cuh:209-267, quotient.cu:142-376)
-    Fr alpha = tr.challenge_scalar("alpha");
-    tr.append_scalar("alpha", alpha);
-    Fr range_c = tr.challenge_scalar("range separation challenge");
-    tr.append_scalar("range seperation challenge", range_c);
-    Fr logic_c = tr.challenge_scalar("logic separation challenge");
-    tr.append_scalar("logic seperation challenge", logic_c);
-    Fr fixed_c = tr.challenge_scalar("fixed base separation challenge");
-    tr.append_scalar("fixed base separation challenge", fixed_c);
-    Fr var_c = tr.challenge_scalar("variable base separation challenge");
-    tr.append_scalar("variable base separation challenge", var_c);
-    Fr lsep = tr.challenge_scalar("lookup separation challenge");
-    tr.append_scalar("lookup separation challenge", lsep);
+    // (a satisfying circuit: one pass over nbq blocks; see quot_blocks above)
+    const Transcript tr3 = tr;  // before the round-4 challenges
+    for (;;) {
+        const uint64_t NBq = (uint64_t)nbq * n;
+        Fr alpha = tr.challenge_scalar("alpha");
+        tr.append_scalar("alpha", alpha);
+        Fr range_c = tr.challenge_scalar("range separation challenge");
+        tr.append_scalar("range seperation challenge", range_c);
+        Fr logic_c = tr.challenge_scalar("logic separation challenge");
+        tr.append_scalar("logic seperation challenge", logic_c);
+        Fr fixed_c = tr.challenge_scalar("fixed base separation challenge");
+        tr.append_scalar("fixed base separation challenge", fixed_c);
+        Fr var_c = tr.challenge_scalar("variable base separation challenge");
+        tr.append_scalar("variable base separation challenge", var_c);
+        Fr lsep = tr.challenge_scalar("lookup separation challenge");
+        tr.append_scalar("lookup separation challenge", lsep);
 
-    QuotArgs q;
-    // coset evaluations in block layout, this rank's blocks only
-    auto lde = [&](const uint64_t *coeffs, uint64_t *dst) { lde_on(s, coeffs, dst); };
-    for (int j = 0; j < 4; j++) q.w8[j] = w8buf[j];
-    uint64_t *z28 = ctx->buf("z28", NB);
-    q.z8 = z8;
-    q.pi8 = nullptr;
-    q.l18 = q.l1v = q.pinv = nullptr;
-    if (closed) q.l1v = ctx->blk("l1v");
-    if (pi_closed) {
-        q.pinv = ctx->pk_pinv.u64();
-        q.c_pi = pi_val[0] * pow_u64(root_of_unity(lg), pi_pos[0]) * n_inv;
-    } else if (pi_poly) {
-        uint64_t *pi8 = ctx->buf("pi8", NB);
-        lde(pi_poly, pi8);
-        q.pi8 = pi8;
-    }
-    q.z28 = nullptr;  // z2 = 1: its quotient terms cancel (protocol.h)
-    if (!z2_one) {
-        lde(z2_poly, z28);
-        q.z28 = z28;
-    }
-    q.f8 = q.t8 = nullptr;
-    if (!f_zero) {
-        uint64_t *f8 = ctx->buf("f8", NB);
-        lde(f_poly, f8);
-        q.f8 = f8;
-    }
-    if (!table_zero) {
-        uint64_t *t8 = ctx->buf("t8", NB);
-        lde(table_poly, t8);
-        q.t8 = t8;
-    }
-    q.h18 = q.h28 = nullptr;  // h1 = h2 = 0
-    if (!h_zero) {
-        uint64_t *h18 = ctx->buf("h18", NB), *h28 = ctx->buf("h28", NB);
-        lde(h1_poly, h18);
-        lde(h2_poly, h28);
-        q.h18 = h18;
-        q.h28 = h28;
-    }
-    // compute_first_lagrange_poly_scaled(n, alpha^2) and (n, 1) (quotient.cu:3-8):
-    // one LDE of L1 (coefficients n^-1, no iNTT); alpha^2 is applied in the kernel
-    Fr alpha2 = alpha * alpha;
-    if (!closed) {
-        uint64_t *l1 = ctx->buf("l1", n), *l18 = ctx->buf("l18", NB);
-        k_geometric(l1, n, n_inv, Fr::one(), s);
-        lde(l1, l18);
-        q.l18 = l18;
-    }
-    q.alpha2 = alpha2;
-    // prover-key evaluations: block-layout copies made at key load
-    q.q_m = ctx->blk("q_m");  // nullptr = zero selector
-    q.q_l = ctx->blk("q_l");
-    q.q_r = ctx->blk("q_r");
-    q.q_o = ctx->blk("q_o");
-    q.q_4 = ctx->blk("q_4");
-    q.q_c = ctx->blk("q_c");
-    q.q_hl = ctx->blk("q_hl");
-    q.q_hr = ctx->blk("q_hr");
-    q.q_h4 = ctx->blk("q_h4");
-    q.q_arith = ctx->blk("q_arith");
-    q.q_lookup = ctx->blk("q_lookup");
-    q.sig[0] = ctx->blk("sig0");
-    q.sig[1] = ctx->blk("sig1");
-    q.sig[2] = ctx->blk("sig2");
-    q.sig[3] = ctx->blk("sig3");
-    q.lin = ctx->blk("lin");
-    q.vh_inv = ctx->blk("vh_inv");  // v_h^-1, computed at key load
-    q.n = n;
-    q.lg_n = lg;
-    q.alpha = alpha;
-    q.beta = beta;
-    q.gamma = gamma;
-    q.delta = delta;
-    q.eps = eps;
-    q.zeta = zeta;
-    q.lsep = lsep;
-    // the kernel derives beta k_j from beta for k = 1, 7, 13, 17
-    for (int j = 0; j < 4; j++) q.bk[j] = pa.bk[j];
-    if (!(pa.bk[1] == beta * fr_from_u64(7) && pa.bk[2] == beta * fr_from_u64(13) &&
-          pa.bk[3] == beta * fr_from_u64(17))) {
-        set_error("quotient: unexpected permutation coset constants");
-        return PNP_E_ARG;
-    }
-    q.opd = delta + Fr::one();
-    q.eopd = eps * q.opd;
-    q.sep2 = lsep * lsep;
-    q.sep3 = q.sep2 * lsep;
-    if (overlap) {  // the side-stream LDEs of the wires and z
-        PNP_HIP(hipStreamWaitEvent(s, ctx->ev_w8, 0));
-        PNP_HIP(hipStreamWaitEvent(s, ctx->ev_z8, 0));
-    }
-    tm.mark("r4_lde");
-    uint64_t *t_blk = ctx->buf("t_blk", NB);
-    hipEvent_t qe0 = nullptr;
-    ctx->ktimer.begin("quotient", s, qe0);
-    k_quotient(q, NB, t_blk, s);
-    if (ctx->pk_custom_nz[0] || ctx->pk_custom_nz[1] || ctx->pk_custom_nz[2] || ctx->pk_custom_nz[3]) {
-        WidgetArgs g;
-        for (int j = 0; j < 4; j++) g.w8[j] = q.w8[j];
-        g.q_l = q.q_l;
-        g.q_r = q.q_r;
-        g.q_c = q.q_c;
-        g.vh_inv = q.vh_inv;
-        g.sel[0] = ctx->blk("range");
-        g.sel[1] = ctx->blk("logic");
-        g.sel[2] = ctx->blk("fixed_add");
-        g.sel[3] = ctx->blk("var_add");
-        g.sep[0] = range_c;
-        g.sep[1] = logic_c;
-        g.sep[2] = fixed_c;
-        g.sep[3] = var_c;
-        g.n = n;
-        g.lg_n = lg;
-        k_widgets(g, NB, t_blk, s);
-    }
-    {
-        // algorithmic bytes: every coset array the kernel reads (nullptr = known
-        // zero, not read) plus t, 32 B per point each
-        const uint64_t *arrs[] = {q.w8[0], q.w8[1], q.w8[2], q.w8[3], q.q_m, q.q_l, q.q_r, q.q_o,
-                                  q.q_4, q.q_c, q.q_hl, q.q_hr, q.q_h4, q.q_arith, q.pi8, q.lin,
-                                  q.z8, q.sig[0], q.sig[1], q.sig[2], q.sig[3], q.f8,
-                                  q.t8, q.h18, q.h28, q.q_lookup, q.z28, q.l18, q.vh_inv, q.l1v, q.pinv};
-        int nread = 0;
-        for (const uint64_t *a : arrs) nread += a != nullptr;
-        ctx->ktimer.end("quotient", s, qe0, 32.0 * (double)NB * (nread + 1));
-    }
-    tm.mark("r4_quotient");
-    ctx->ktimer.collect();
-    // Intt_coset of the 8n values: per block an unscaled size-n inverse
-    // transform and a twist, then an 8-point inverse DFT across the blocks
-    // per coefficient index (ntt.hip t_combine) -> the 8 chunks t_1..t_8,
-    // here over this rank's coefficient range [q0, q0 + len): t_poly[k len + u]
-    intt_blocks(nt, t_blk, lg, mb0, nb, s);
-    uint64_t *t_poly = ctx->buf("t_poly", 8 * len);
-    if (!dist) {
-        t_combine(nt, t_blk, n, 0, t_poly, lg, s);
-    } else {
-        // all-to-all: rank r' receives, from every rank, that rank's blocks
-        // restricted to r''s coefficient range; slots arrive block-major
-        const uint64_t slot = (uint64_t)nb * len * 32;
-        if (!ctx->msm.alltoall || ctx->msm.a2a_bytes < 2 * slot * world) {
-            set_error("round-4 all-to-all buffer missing or < %llu B",
-                      (unsigned long long)(2 * slot * world));
+        QuotArgs q;
+        // coset evaluations in block layout, this rank's blocks only
+        auto lde = [&](const uint64_t *coeffs, uint64_t *dst) { lde_on(s, coeffs, dst); };
+        for (int j = 0; j < 4; j++) q.w8[j] = w8buf[j];
+        uint64_t *z28 = ctx->buf("z28", NB);
+        q.z8 = z8;
+        q.pi8 = nullptr;
+        q.l18 = q.l1v = q.pinv = nullptr;
+        if (closed) q.l1v = ctx->blk("l1v");
+        if (pi_closed) {
+            q.pinv = ctx->pk_pinv.u64();
+            q.c_pi = pi_val[0] * pow_u64(root_of_unity(lg), pi_pos[0]) * n_inv;
+        } else if (pi_poly) {
+            uint64_t *pi8 = ctx->buf("pi8", NB);
+            lde(pi_poly, pi8);
+            q.pi8 = pi8;
+        }
+        q.z28 = nullptr;  // z2 = 1: its quotient terms cancel (protocol.h)
+        if (!z2_one) {
+            lde(z2_poly, z28);
+            q.z28 = z28;
+        }
+        q.f8 = q.t8 = nullptr;
+        if (!f_zero) {
+            uint64_t *f8 = ctx->buf("f8", NB);
+            lde(f_poly, f8);
+            q.f8 = f8;
+        }
+        if (!table_zero) {
+            uint64_t *t8 = ctx->buf("t8", NB);
+            lde(table_poly, t8);
+            q.t8 = t8;
+        }
+        q.h18 = q.h28 = nullptr;  // h1 = h2 = 0
+        if (!h_zero) {
+            uint64_t *h18 = ctx->buf("h18", NB), *h28 = ctx->buf("h28", NB);
+            lde(h1_poly, h18);
+            lde(h2_poly, h28);
+            q.h18 = h18;
+            q.h28 = h28;
+        }
+        // compute_first_lagrange_poly_scaled(n, alpha^2) and (n, 1) (quotient.cu:3-8):
+        // one LDE of L1 (coefficients n^-1, no iNTT); alpha^2 is applied in the kernel
+        Fr alpha2 = alpha * alpha;
+        if (!closed) {
+            uint64_t *l1 = ctx->buf("l1", n), *l18 = ctx->buf("l18", NB);
+            k_geometric(l1, n, n_inv, Fr::one(), s);
+            lde(l1, l18);
+            q.l18 = l18;
+        }
+        q.alpha2 = alpha2;
+        // prover-key evaluations: block-layout copies made at key load
+        q.q_m = ctx->blk("q_m");  // nullptr = zero selector
+        q.q_l = ctx->blk("q_l");
+        q.q_r = ctx->blk("q_r");
+        q.q_o = ctx->blk("q_o");
+        q.q_4 = ctx->blk("q_4");
+        q.q_c = ctx->blk("q_c");
+        q.q_hl = ctx->blk("q_hl");
+        q.q_hr = ctx->blk("q_hr");
+        q.q_h4 = ctx->blk("q_h4");
+        q.q_arith = ctx->blk("q_arith");
+        q.q_lookup = ctx->blk("q_lookup");
+        q.sig[0] = ctx->blk("sig0");
+        q.sig[1] = ctx->blk("sig1");
+        q.sig[2] = ctx->blk("sig2");
+        q.sig[3] = ctx->blk("sig3");
+        q.lin = ctx->blk("lin");
+        q.vh_inv = ctx->blk("vh_inv");  // v_h^-1, computed at key load
+        q.n = n;
+        q.lg_n = lg;
+        q.alpha = alpha;
+        q.beta = beta;
+        q.gamma = gamma;
+        q.delta = delta;
+        q.eps = eps;
+        q.zeta = zeta;
+        q.lsep = lsep;
+        // the kernel derives beta k_j from beta for k = 1, 7, 13, 17
+        for (int j = 0; j < 4; j++) q.bk[j] = pa.bk[j];
+        if (!(pa.bk[1] == beta * fr_from_u64(7) && pa.bk[2] == beta * fr_from_u64(13) &&
+              pa.bk[3] == beta * fr_from_u64(17))) {
+            set_error("quotient: unexpected permutation coset constants");
             return PNP_E_ARG;
         }
-        uint64_t *a2a = ctx->msm.a2a;
-        for (int r = 0; r < world; r++) {
-            uint64_t r0, r1;
-            msm_point_range(n, r, world, r0, r1);
-            for (int b = 0; b < nb; b++)
-                PNP_HIP(hipMemcpyAsync(a2a + 4 * ((uint64_t)(r * nb + b) * len), t_blk + 4 * ((uint64_t)b * n + r0),
-                                       32 * len, hipMemcpyDeviceToDevice, s));
+        q.opd = delta + Fr::one();
+        q.eopd = eps * q.opd;
+        q.sep2 = lsep * lsep;
+        q.sep3 = q.sep2 * lsep;
+        if (overlap) {  // the side-stream LDEs of the wires and z
+            PNP_HIP(hipStreamWaitEvent(s, ctx->ev_w8, 0));
+            PNP_HIP(hipStreamWaitEvent(s, ctx->ev_z8, 0));
         }
-        PNP_HIP(hipStreamSynchronize(s));
-        int rc = ctx->msm.alltoall(ctx->msm.a2a_user, slot);
-        if (rc != 0) {
-            set_error("round-4 all-to-all callback failed (%d)", rc);
-            return PNP_E_DEVICE;
+        tm.mark("r4_lde");
+        uint64_t *t_blk = ctx->buf("t_blk", NB);
+        hipEvent_t qe0 = nullptr;
+        ctx->ktimer.begin("quotient", s, qe0);
+        k_quotient(q, NBq, t_blk, s);
+        if (ctx->pk_custom_nz[0] || ctx->pk_custom_nz[1] || ctx->pk_custom_nz[2] || ctx->pk_custom_nz[3]) {
+            WidgetArgs g;
+            for (int j = 0; j < 4; j++) g.w8[j] = q.w8[j];
+            g.q_l = q.q_l;
+            g.q_r = q.q_r;
+            g.q_c = q.q_c;
+            g.vh_inv = q.vh_inv;
+            g.sel[0] = ctx->blk("range");
+            g.sel[1] = ctx->blk("logic");
+            g.sel[2] = ctx->blk("fixed_add");
+            g.sel[3] = ctx->blk("var_add");
+            g.sep[0] = range_c;
+            g.sep[1] = logic_c;
+            g.sep[2] = fixed_c;
+            g.sep[3] = var_c;
+            g.n = n;
+            g.lg_n = lg;
+            k_widgets(g, NBq, t_blk, s);
         }
-        t_combine(nt, a2a + 4 * (uint64_t)nb * len * world, len, q0, t_poly, lg, s);
-    }
-    tm.mark("r4_intt8");
-    CommitmentC *tcm[8] = {&out->t_1_comm, &out->t_2_comm, &out->t_3_comm, &out->t_4_comm,
-                           &out->t_5_comm, &out->t_6_comm, &out->t_7_comm, &out->t_8_comm};
-    {
-        // chunks that are identically zero (t_7, t_8 for a satisfying circuit:
-        // deg t < 6n) commit to the point at infinity without an MSM
-        const uint64_t *sc[9];
-        CommitmentC *oc[9];
-        int nc = 0;
-        uint64_t nz[8];
         {
-            bool b[8];
-            k_any_nonzero_n(t_poly, 4 * len, 4 * len, 8, b, ctx->scratch_b, s);
-            for (int k = 0; k < 8; k++) nz[k] = b[k];
+            // algorithmic bytes: every coset array the kernel reads (nullptr = known
+            // zero, not read) plus t, 32 B per point each
+            const uint64_t *arrs[] = {q.w8[0], q.w8[1], q.w8[2], q.w8[3], q.q_m, q.q_l, q.q_r, q.q_o,
+                                      q.q_4, q.q_c, q.q_hl, q.q_hr, q.q_h4, q.q_arith, q.pi8, q.lin,
+                                      q.z8, q.sig[0], q.sig[1], q.sig[2], q.sig[3], q.f8,
+                                      q.t8, q.h18, q.h28, q.q_lookup, q.z28, q.l18, q.vh_inv, q.l1v, q.pinv};
+            int nread = 0;
+            for (const uint64_t *a : arrs) nread += a != nullptr;
+            ctx->ktimer.end("quotient", s, qe0, 32.0 * (double)NBq * (nread + 1));
         }
-        if (dist) {  // a chunk is zero when it is zero on every rank
-            std::vector<uint64_t> all = shard_allgather(ctx, nz, 8);
-            for (int k = 0; k < 8; k++)
-                for (int r = 0; r < world; r++) nz[k] |= all[8 * r + k];
+        tm.mark("r4_quotient");
+        ctx->ktimer.collect();
+        // Intt_coset of the coset values: per block an unscaled size-n inverse
+        // transform and a twist, then per coefficient index an inverse DFT (8
+        // blocks, ntt.hip t_combine) or Vandermonde solve (6 / 7 blocks,
+        // t_combine_blocks) across the blocks -> the chunks t_1..t_8, here over
+        // this rank's coefficient range [q0, q0 + len): t_poly[k len + u]; with
+        // nbq < 8 blocks the chunks from t_(nbq+1) on are zero
+        intt_blocks(nt, t_blk, lg, mb0, nbq, s);
+        uint64_t *t_poly = ctx->buf("t_poly", 8 * len);
+        const int npieces = dist ? 8 : nbq;
+        if (!dist) {
+            t_combine_blocks(nt, t_blk, nbq, t_poly, lg, s);
+        } else {
+            // all-to-all: rank r' receives, from every rank, that rank's blocks
+            // restricted to r''s coefficient range; slots arrive block-major
+            const uint64_t slot = (uint64_t)nb * len * 32;
+            if (!ctx->msm.alltoall || ctx->msm.a2a_bytes < 2 * slot * world) {
+                set_error("round-4 all-to-all buffer missing or < %llu B",
+                          (unsigned long long)(2 * slot * world));
+                return PNP_E_ARG;
+            }
+            uint64_t *a2a = ctx->msm.a2a;
+            for (int r = 0; r < world; r++) {
+                uint64_t r0, r1;
+                msm_point_range(n, r, world, r0, r1);
+                for (int b = 0; b < nb; b++)
+                    PNP_HIP(hipMemcpyAsync(a2a + 4 * ((uint64_t)(r * nb + b) * len), t_blk + 4 * ((uint64_t)b * n + r0),
+                                           32 * len, hipMemcpyDeviceToDevice, s));
+            }
+            PNP_HIP(hipStreamSynchronize(s));
+            int rc = ctx->msm.alltoall(ctx->msm.a2a_user, slot);
+            if (rc != 0) {
+                set_error("round-4 all-to-all callback failed (%d)", rc);
+                return PNP_E_DEVICE;
+            }
+            t_combine(nt, a2a + 4 * (uint64_t)nb * len * world, len, q0, t_poly, lg, s);
         }
-        for (int k = 0; k < 8; k++) {
-            if (!nz[k]) {
-                set_infinity(tcm[k]);
+        tm.mark("r4_intt8");
+        CommitmentC *tcm[8] = {&out->t_1_comm, &out->t_2_comm, &out->t_3_comm, &out->t_4_comm,
+                               &out->t_5_comm, &out->t_6_comm, &out->t_7_comm, &out->t_8_comm};
+        {
+            // chunks that are identically zero (t_7, t_8 for a satisfying circuit:
+            // deg t < 6n) commit to the point at infinity without an MSM
+            const uint64_t *sc[9];
+            CommitmentC *oc[9];
+            int nc = 0;
+            uint64_t nz[8];
+            {
+                bool b[8] = {false, false, false, false, false, false, false, false};
+                k_any_nonzero_n(t_poly, 4 * len, 4 * len, npieces, b, ctx->scratch_b, s);
+                for (int k = 0; k < 8; k++) nz[k] = b[k];
+            }
+            if (dist) {  // a chunk is zero when it is zero on every rank
+                std::vector<uint64_t> all = shard_allgather(ctx, nz, 8);
+                for (int k = 0; k < 8; k++)
+                    for (int r = 0; r < world; r++) nz[k] |= all[8 * r + k];
+            }
+            for (int k = 0; k < 8; k++) {
+                if (!nz[k]) {
+                    set_infinity(tcm[k]);
+                    continue;
+                }
+                sc[nc] = t_poly + 4 * (uint64_t)k * len;
+                oc[nc++] = tcm[k];
+            }
+            if (z2_one) {
+                // commit([1, 0, ...]) = 1 * powers_of_g[0], already affine
+                uint64_t g0[12];
+                PNP_HIP(hipMemcpyAsync(g0, ctx->ck_dev, sizeof g0, hipMemcpyDeviceToHost, s));
+                PNP_HIP(hipStreamSynchronize(s));
+                memcpy(out->z_2_comm.x, g0, 48);
+                memcpy(out->z_2_comm.y, g0 + 6, 48);
+            } else if (dist) {
+                commit_affine(ctx, z2_poly, n, &out->z_2_comm);
+            } else {
+                sc[nc] = z2_poly;
+                oc[nc++] = &out->z_2_comm;
+            }
+            // distributed: the chunks hold this rank's coefficient range only,
+            // exactly the point range of its MSM share
+            commit_affine_batch(ctx, sc, nc, n, oc, dist);
+        }
+        const char *tl[8] = {"t_1", "t_2", "t_3", "t_4", "t_5", "t_6", "t_7", "t_8"};
+        for (int k = 0; k < 8; k++) append_comm(tr, tl[k], *tcm[k]);
+        tm.mark("r4_commit");
+
+        // ---------------- round 5: linearisation (linearisation.cu:73-306)
+        Fr zc = tr.challenge_scalar("z");
+        tr.append_scalar("z", zc);
+        Fr omega = root_of_unity(lg);
+        Fr zw = zc * omega;
+        Fr vh = pow_u64(zc, n) - Fr::one();
+        Fr zn = vh + Fr::one();
+        Fr l1e = vh * inverse(fr_from_u64(n) * (zc - Fr::one()));
+        ProofEvaluationsC *ev = &out->evaluations;
+        {
+            // evaluations at z
+            const uint64_t *pz[12] = {wpoly[0], wpoly[1], wpoly[2], wpoly[3], pk.left_sigma_coeffs,
+                                      pk.right_sigma_coeffs, pk.out_sigma_coeffs, pk.q_arith_coeffs,
+                                      pk.q_c_coeffs, pk.q_l_coeffs, pk.q_r_coeffs, pk.q_hl_coeffs};
+            Fr rz[12];
+            k_poly_eval_multi(pz, 12, n, zc, ctx->scratch_a, rz, s);
+            const uint64_t *pz2[2] = {pk.q_hr_coeffs, pk.q_h4_coeffs};
+            Fr rz2[2];
+            k_poly_eval_multi(pz2, 2, n, zc, ctx->scratch_a, rz2, s);
+            // evaluations at z * omega
+            const uint64_t *pw[4] = {z_poly, wpoly[0], wpoly[1], wpoly[3]};
+            Fr rw[4];
+            k_poly_eval_multi(pw, 4, n, zw, ctx->scratch_a, rw, s);
+            Fr z2n = Fr::one();
+            if (!z2_one) k_poly_eval(z2_poly, n, zw, ctx->scratch_a, &z2n, s);
+            Fr f_eval = Fr::zero(), t_eval = Fr::zero(), t_next = Fr::zero();
+            Fr ql_eval = Fr::zero(), h1_eval = Fr::zero(), h1_next = Fr::zero(), h2_eval = Fr::zero();
+            if (!ctx->pk_qlookup_zero) k_poly_eval(pk.q_lookup_coeffs, n, zc, ctx->scratch_a, &ql_eval, s);
+            if (!h_zero) {
+                k_poly_eval(h1_poly, n, zc, ctx->scratch_a, &h1_eval, s);
+                k_poly_eval(h1_poly, n, zw, ctx->scratch_a, &h1_next, s);
+                k_poly_eval(h2_poly, n, zc, ctx->scratch_a, &h2_eval, s);
+            }
+            if (!f_zero) k_poly_eval(f_poly, n, zc, ctx->scratch_a, &f_eval, s);
+            if (!table_zero) {
+                k_poly_eval(table_poly, n, zc, ctx->scratch_a, &t_eval, s);
+                k_poly_eval(table_poly, n, zw, ctx->scratch_a, &t_next, s);
+            }
+            store_fr_host(ev->wire_evals.a_eval, rz[0]);
+            store_fr_host(ev->wire_evals.b_eval, rz[1]);
+            store_fr_host(ev->wire_evals.c_eval, rz[2]);
+            store_fr_host(ev->wire_evals.d_eval, rz[3]);
+            store_fr_host(ev->perm_evals.left_sigma_eval, rz[4]);
+            store_fr_host(ev->perm_evals.right_sigma_eval, rz[5]);
+            store_fr_host(ev->perm_evals.out_sigma_eval, rz[6]);
+            store_fr_host(ev->perm_evals.permutation_eval, rw[0]);
+            CustomEvaluationsC *cu = &ev->custom_evals;
+            store_fr_host(cu->q_arith_eval, rz[7]);
+            store_fr_host(cu->q_c_eval, rz[8]);
+            store_fr_host(cu->q_l_eval, rz[9]);
+            store_fr_host(cu->q_r_eval, rz[10]);
+            store_fr_host(cu->q_hl_eval, rz[11]);
+            store_fr_host(cu->q_hr_eval, rz2[0]);
+            store_fr_host(cu->q_h4_eval, rz2[1]);
+            store_fr_host(cu->a_next_eval, rw[1]);
+            store_fr_host(cu->b_next_eval, rw[2]);
+            store_fr_host(cu->d_next_eval, rw[3]);
+            LookupEvaluationsC *lk = &ev->lookup_evals;
+            store_fr_host(lk->q_lookup_eval, ql_eval);
+            store_fr_host(lk->h1_eval, h1_eval);
+            store_fr_host(lk->h1_next_eval, h1_next);
+            store_fr_host(lk->h2_eval, h2_eval);
+            store_fr_host(lk->z2_next_eval, z2n);
+            store_fr_host(lk->f_eval, f_eval);
+            store_fr_host(lk->table_eval, t_eval);
+            store_fr_host(lk->table_next_eval, t_next);
+        }
+        tm.mark("r5_evals");
+        auto ld = [](const uint64_t *p) { return from_u64_limbs<FrP>(p); };
+        const Fr ae = ld(ev->wire_evals.a_eval), be = ld(ev->wire_evals.b_eval),
+                 ce = ld(ev->wire_evals.c_eval), de = ld(ev->wire_evals.d_eval);
+        const Fr qae = ld(ev->custom_evals.q_arith_eval);
+        LinArgs la;
+        la.k = 0;
+        // over this rank's coefficient range (replicated polynomials offset by q0)
+        auto push_local = [&](const uint64_t *p, const Fr &sc) {
+            la.p[la.k] = p;
+            la.s[la.k] = sc;
+            la.k++;
+        };
+        auto push = [&](const uint64_t *p, const Fr &sc) { push_local(p + 4 * q0, sc); };
+        auto p5 = [](const Fr &x) { Fr x2 = x * x; return x2 * x2 * x; };
+        // arithmetic (widget/arithmetic.rs:82-100)
+        if (!ctx->pk_qm_zero) push(pk.q_m_coeffs, ae * be * qae);
+        push(pk.q_l_coeffs, ae * qae);
+        push(pk.q_r_coeffs, be * qae);
+        push(pk.q_o_coeffs, ce * qae);
+        push(pk.q_4_coeffs, de * qae);
+        push(pk.q_hl_coeffs, p5(ae) * qae);
+        push(pk.q_hr_coeffs, p5(be) * qae);
+        push(pk.q_h4_coeffs, p5(de) * qae);
+        push(pk.q_c_coeffs, qae);
+        // custom gates (linearisation_poly.rs:396-430): selector * constraints(evals)
+        {
+            const CustomEvaluationsC *ce_ = &ev->custom_evals;
+            WidgetVals wv;
+            wv.a = ae;
+            wv.b = be;
+            wv.c = ce;
+            wv.d = de;
+            wv.a_next = ld(ce_->a_next_eval);
+            wv.b_next = ld(ce_->b_next_eval);
+            wv.d_next = ld(ce_->d_next_eval);
+            wv.q_l = ld(ce_->q_l_eval);
+            wv.q_r = ld(ce_->q_r_eval);
+            wv.q_c = ld(ce_->q_c_eval);
+            if (ctx->pk_custom_nz[0]) push(pk.range_selector_coeffs, w_range(range_c, wv));
+            if (ctx->pk_custom_nz[1]) push(pk.logic_selector_coeffs, w_logic(logic_c, wv));
+            if (ctx->pk_custom_nz[2]) push(pk.fixed_group_add_selector_coeffs, w_fbsm(fixed_c, wv));
+            if (ctx->pk_custom_nz[3]) push(pk.variable_group_add_selector_coeffs, w_cadd(var_c, wv));
+        }
+        // compute_linearisation_permutation (proof_system/permutation.cu:231-265)
+        {
+            Fr bz = beta * zc;
+            Fr a = (ae + bz + gamma) * (be + fr_from_u64(7) * bz + gamma) *
+                   (ce + fr_from_u64(13) * bz + gamma) * (de + fr_from_u64(17) * bz + gamma) * alpha;
+            push(z_poly, a + l1e * alpha2);
+            const Fr s1 = ld(ev->perm_evals.left_sigma_eval), s2 = ld(ev->perm_evals.right_sigma_eval),
+                     s3 = ld(ev->perm_evals.out_sigma_eval), pe = ld(ev->perm_evals.permutation_eval);
+            Fr b = (ae + beta * s1 + gamma) * (be + beta * s2 + gamma) * (ce + beta * s3 + gamma) *
+                   (beta * pe) * alpha;
+            push(pk.fourth_sigma_coeffs, neg(b));
+        }
+        // lookup (widget/lookup.rs:137-182)
+        {
+            const LookupEvaluationsC *lk = &ev->lookup_evals;
+            Fr sep2 = lsep * lsep, sep3 = sep2 * lsep, opd = delta + Fr::one(), eopd = eps * opd;
+            if (!ctx->pk_qlookup_zero) {
+                Fr ct = ((de * zeta + ce) * zeta + be) * zeta + ae;
+                push(pk.q_lookup_coeffs, (ct - ld(lk->f_eval)) * lsep);
+            }
+            Fr b0 = eps + ld(lk->f_eval);
+            Fr b1 = eopd + ld(lk->table_eval) + delta * ld(lk->table_next_eval);
+            push(z2_poly, opd * b0 * b1 * sep2 + l1e * sep3);
+            if (!h_zero)
+                push(h1_poly, neg(ld(lk->z2_next_eval)) * sep2 * (eopd + ld(lk->h2_eval) + delta * ld(lk->h1_next_eval)));
+        }
+        // - Z_H(z) * sum_k z^(kn) t_(k+1)  (linearisation.cu:250-292)
+        {
+            Fr p = neg(vh);
+            for (int k = 0; k < npieces; k++) {
+                push_local(t_poly + 4 * (uint64_t)k * len, p);  // t_poly is range-local
+                p = p * zn;
+            }
+        }
+        uint64_t *lin = ctx->buf("lin", len);
+        k_lincomb(la, len, lin, s);
+        if (!dist && nbq < 8) {
+            // the verifier's equation (proof.rs:433-494, oracle/verifier.c): for the
+            // true quotient lin(z) = -r_0; otherwise the witness does not satisfy
+            // the circuit, t has degree >= nbq n and round 4 runs again on all 8
+            // blocks (a false pass needs z to be a root of a nonzero polynomial of
+            // degree < 8n: probability < 2^-228 over the transcript hash)
+            Fr lin_z;
+            k_poly_eval(lin, len, zc, ctx->scratch_a, &lin_z, s);
+            const LookupEvaluationsC *lk = &ev->lookup_evals;
+            Fr pie = Fr::zero();
+            const Fr w_inv = inverse(omega);
+            for (size_t k = 0; k < pi_pos.size(); k++)
+                pie += pi_val[k] * inverse(pow_u64(w_inv, pi_pos[k]) * zc - Fr::one());
+            pie = pie * vh * n_inv;
+            const Fr *wv[3] = {&ae, &be, &ce};
+            const Fr sv[3] = {ld(ev->perm_evals.left_sigma_eval), ld(ev->perm_evals.right_sigma_eval),
+                              ld(ev->perm_evals.out_sigma_eval)};
+            Fr b = Fr::one();
+            for (int j = 0; j < 3; j++) b = b * (*wv[j] + beta * sv[j] + gamma);
+            b = b * (de + gamma) * ld(ev->perm_evals.permutation_eval) * alpha;
+            const Fr opd = delta + Fr::one(), eopd = eps * opd, sep2 = lsep * lsep, sep3 = sep2 * lsep;
+            const Fr h2e = ld(lk->h2_eval);
+            const Fr d = sep2 * ld(lk->z2_next_eval) * (eopd + delta * h2e) *
+                         (eopd + h2e + delta * ld(lk->h1_next_eval));
+            const Fr r0 = pie - b - l1e * alpha2 - d - sep3 * l1e;
+            if (!(lin_z + r0).is_zero()) {
+                ctx->ktimer.credit("quotient_all_blocks", 1);
+                const uint64_t off = 4 * (uint64_t)nbq * n;  // blocks nbq .. 7
+                for (int j = 0; j < 4; j++) lde_blocks(nt, wpoly[j], w8buf[j] + off, lg, nbq, 8 - nbq, s);
+                lde_blocks(nt, z_poly, z8 + off, lg, nbq, 8 - nbq, s);
+                nbq = 8;
+                tr = tr3;
                 continue;
             }
-            sc[nc] = t_poly + 4 * (uint64_t)k * len;
-            oc[nc++] = tcm[k];
         }
-        if (z2_one) {
-            // commit([1, 0, ...]) = 1 * powers_of_g[0], already affine
-            uint64_t g0[12];
-            PNP_HIP(hipMemcpyAsync(g0, ctx->ck_dev, sizeof g0, hipMemcpyDeviceToHost, s));
-            PNP_HIP(hipStreamSynchronize(s));
-            memcpy(out->z_2_comm.x, g0, 48);
-            memcpy(out->z_2_comm.y, g0 + 6, 48);
-        } else if (dist) {
-            commit_affine(ctx, z2_poly, n, &out->z_2_comm);
-        } else {
-            sc[nc] = z2_poly;
-            oc[nc++] = &out->z_2_comm;
-        }
-        // distributed: the chunks hold this rank's coefficient range only,
-        // exactly the point range of its MSM share
-        commit_affine_batch(ctx, sc, nc, n, oc, dist);
-    }
-    const char *tl[8] = {"t_1", "t_2", "t_3", "t_4", "t_5", "t_6", "t_7", "t_8"};
-    for (int k = 0; k < 8; k++) append_comm(tr, tl[k], *tcm[k]);
-    tm.mark("r4_commit");
+        tm.mark("r5_lin");
 
-    // ---------------- round 5: linearisation (linearisation.cu:73-306)
-    Fr zc = tr.challenge_scalar("z");
-    tr.append_scalar("z", zc);
-    Fr omega = root_of_unity(lg);
-    Fr zw = zc * omega;
-    Fr vh = pow_u64(zc, n) - Fr::one();
-    Fr zn = vh + Fr::one();
-    Fr l1e = vh * inverse(fr_from_u64(n) * (zc - Fr::one()));
-    ProofEvaluationsC *ev = &out->evaluations;
-    {
-        // evaluations at z
-        const uint64_t *pz[12] = {wpoly[0], wpoly[1], wpoly[2], wpoly[3], pk.left_sigma_coeffs,
-                                  pk.right_sigma_coeffs, pk.out_sigma_coeffs, pk.q_arith_coeffs,
-                                  pk.q_c_coeffs, pk.q_l_coeffs, pk.q_r_coeffs, pk.q_hl_coeffs};
-        Fr rz[12];
-        k_poly_eval_multi(pz, 12, n, zc, ctx->scratch_a, rz, s);
-        const uint64_t *pz2[2] = {pk.q_hr_coeffs, pk.q_h4_coeffs};
-        Fr rz2[2];
-        k_poly_eval_multi(pz2, 2, n, zc, ctx->scratch_a, rz2, s);
-        // evaluations at z * omega
-        const uint64_t *pw[4] = {z_poly, wpoly[0], wpoly[1], wpoly[3]};
-        Fr rw[4];
-        k_poly_eval_multi(pw, 4, n, zw, ctx->scratch_a, rw, s);
-        Fr z2n = Fr::one();
-        if (!z2_one) k_poly_eval(z2_poly, n, zw, ctx->scratch_a, &z2n, s);
-        Fr f_eval = Fr::zero(), t_eval = Fr::zero(), t_next = Fr::zero();
-        Fr ql_eval = Fr::zero(), h1_eval = Fr::zero(), h1_next = Fr::zero(), h2_eval = Fr::zero();
-        if (!ctx->pk_qlookup_zero) k_poly_eval(pk.q_lookup_coeffs, n, zc, ctx->scratch_a, &ql_eval, s);
-        if (!h_zero) {
-            k_poly_eval(h1_poly, n, zc, ctx->scratch_a, &h1_eval, s);
-            k_poly_eval(h1_poly, n, zw, ctx->scratch_a, &h1_next, s);
-            k_poly_eval(h2_poly, n, zc, ctx->scratch_a, &h2_eval, s);
-        }
-        if (!f_zero) k_poly_eval(f_poly, n, zc, ctx->scratch_a, &f_eval, s);
-        if (!table_zero) {
-            k_poly_eval(table_poly, n, zc, ctx->scratch_a, &t_eval, s);
-            k_poly_eval(table_poly, n, zw, ctx->scratch_a, &t_next, s);
-        }
-        store_fr_host(ev->wire_evals.a_eval, rz[0]);
-        store_fr_host(ev->wire_evals.b_eval, rz[1]);
-        store_fr_host(ev->wire_evals.c_eval, rz[2]);
-        store_fr_host(ev->wire_evals.d_eval, rz[3]);
-        store_fr_host(ev->perm_evals.left_sigma_eval, rz[4]);
-        store_fr_host(ev->perm_evals.right_sigma_eval, rz[5]);
-        store_fr_host(ev->perm_evals.out_sigma_eval, rz[6]);
-        store_fr_host(ev->perm_evals.permutation_eval, rw[0]);
-        CustomEvaluationsC *cu = &ev->custom_evals;
-        store_fr_host(cu->q_arith_eval, rz[7]);
-        store_fr_host(cu->q_c_eval, rz[8]);
-        store_fr_host(cu->q_l_eval, rz[9]);
-        store_fr_host(cu->q_r_eval, rz[10]);
-        store_fr_host(cu->q_hl_eval, rz[11]);
-        store_fr_host(cu->q_hr_eval, rz2[0]);
-        store_fr_host(cu->q_h4_eval, rz2[1]);
-        store_fr_host(cu->a_next_eval, rw[1]);
-        store_fr_host(cu->b_next_eval, rw[2]);
-        store_fr_host(cu->d_next_eval, rw[3]);
-        LookupEvaluationsC *lk = &ev->lookup_evals;
-        store_fr_host(lk->q_lookup_eval, ql_eval);
-        store_fr_host(lk->h1_eval, h1_eval);
-        store_fr_host(lk->h1_next_eval, h1_next);
-        store_fr_host(lk->h2_eval, h2_eval);
-        store_fr_host(lk->z2_next_eval, z2n);
-        store_fr_host(lk->f_eval, f_eval);
-        store_fr_host(lk->table_eval, t_eval);
-        store_fr_host(lk->table_next_eval, t_next);
-    }
-    tm.mark("r5_evals");
-    auto ld = [](const uint64_t *p) { return from_u64_limbs<FrP>(p); };
-    const Fr ae = ld(ev->wire_evals.a_eval), be = ld(ev->wire_evals.b_eval),
-             ce = ld(ev->wire_evals.c_eval), de = ld(ev->wire_evals.d_eval);
-    const Fr qae = ld(ev->custom_evals.q_arith_eval);
-    LinArgs la;
-    la.k = 0;
-    // over this rank's coefficient range (replicated polynomials offset by q0)
-    auto push_local = [&](const uint64_t *p, const Fr &sc) {
-        la.p[la.k] = p;
-        la.s[la.k] = sc;
-        la.k++;
-    };
-    auto push = [&](const uint64_t *p, const Fr &sc) { push_local(p + 4 * q0, sc); };
-    auto p5 = [](const Fr &x) { Fr x2 = x * x; return x2 * x2 * x; };
-    // arithmetic (widget/arithmetic.rs:82-100)
-    if (!ctx->pk_qm_zero) push(pk.q_m_coeffs, ae * be * qae);
-    push(pk.q_l_coeffs, ae * qae);
-    push(pk.q_r_coeffs, be * qae);
-    push(pk.q_o_coeffs, ce * qae);
-    push(pk.q_4_coeffs, de * qae);
-    push(pk.q_hl_coeffs, p5(ae) * qae);
-    push(pk.q_hr_coeffs, p5(be) * qae);
-    push(pk.q_h4_coeffs, p5(de) * qae);
-    push(pk.q_c_coeffs, qae);
-    // custom gates (linearisation_poly.rs:396-430): selector * constraints(evals)
-    {
-        const CustomEvaluationsC *ce_ = &ev->custom_evals;
-        WidgetVals wv;
-        wv.a = ae;
-        wv.b = be;
-        wv.c = ce;
-        wv.d = de;
-        wv.a_next = ld(ce_->a_next_eval);
-        wv.b_next = ld(ce_->b_next_eval);
-        wv.d_next = ld(ce_->d_next_eval);
-        wv.q_l = ld(ce_->q_l_eval);
-        wv.q_r = ld(ce_->q_r_eval);
-        wv.q_c = ld(ce_->q_c_eval);
-        if (ctx->pk_custom_nz[0]) push(pk.range_selector_coeffs, w_range(range_c, wv));
-        if (ctx->pk_custom_nz[1]) push(pk.logic_selector_coeffs, w_logic(logic_c, wv));
-        if (ctx->pk_custom_nz[2]) push(pk.fixed_group_add_selector_coeffs, w_fbsm(fixed_c, wv));
-        if (ctx->pk_custom_nz[3]) push(pk.variable_group_add_selector_coeffs, w_cadd(var_c, wv));
-    }
-    // compute_linearisation_permutation (proof_system/permutation.cu:231-265)
-    {
-        Fr bz = beta * zc;
-        Fr a = (ae + bz + gamma) * (be + fr_from_u64(7) * bz + gamma) *
-               (ce + fr_from_u64(13) * bz + gamma) * (de + fr_from_u64(17) * bz + gamma) * alpha;
-        push(z_poly, a + l1e * alpha2);
-        const Fr s1 = ld(ev->perm_evals.left_sigma_eval), s2 = ld(ev->perm_evals.right_sigma_eval),
-                 s3 = ld(ev->perm_evals.out_sigma_eval), pe = ld(ev->perm_evals.permutation_eval);
-        Fr b = (ae + beta * s1 + gamma) * (be + beta * s2 + gamma) * (ce + beta * s3 + gamma) *
-               (beta * pe) * alpha;
-        push(pk.fourth_sigma_coeffs, neg(b));
-    }
-    // lookup (widget/lookup.rs:137-182)
-    {
+        // transcript appends (gen_proof.cuh:373-403)
+        tr.append_scalar("a_eval", ae);
+        tr.append_scalar("b_eval", be);
+        tr.append_scalar("c_eval", ce);
+        tr.append_scalar("d_eval", de);
+        tr.append_scalar("left_sig_eval", ld(ev->perm_evals.left_sigma_eval));
+        tr.append_scalar("right_sig_eval", ld(ev->perm_evals.right_sigma_eval));
+        tr.append_scalar("out_sig_eval", ld(ev->perm_evals.out_sigma_eval));
+        tr.append_scalar("perm_eval", ld(ev->perm_evals.permutation_eval));
         const LookupEvaluationsC *lk = &ev->lookup_evals;
-        Fr sep2 = lsep * lsep, sep3 = sep2 * lsep, opd = delta + Fr::one(), eopd = eps * opd;
-        if (!ctx->pk_qlookup_zero) {
-            Fr ct = ((de * zeta + ce) * zeta + be) * zeta + ae;
-            push(pk.q_lookup_coeffs, (ct - ld(lk->f_eval)) * lsep);
-        }
-        Fr b0 = eps + ld(lk->f_eval);
-        Fr b1 = eopd + ld(lk->table_eval) + delta * ld(lk->table_next_eval);
-        push(z2_poly, opd * b0 * b1 * sep2 + l1e * sep3);
-        if (!h_zero)
-            push(h1_poly, neg(ld(lk->z2_next_eval)) * sep2 * (eopd + ld(lk->h2_eval) + delta * ld(lk->h1_next_eval)));
-    }
-    // - Z_H(z) * sum_k z^(kn) t_(k+1)  (linearisation.cu:250-292)
-    {
-        Fr p = neg(vh);
-        for (int k = 0; k < 8; k++) {
-            push_local(t_poly + 4 * (uint64_t)k * len, p);  // t_poly is range-local
-            p = p * zn;
-        }
-    }
-    uint64_t *lin = ctx->buf("lin", len);
-    k_lincomb(la, len, lin, s);
-    tm.mark("r5_lin");
+        tr.append_scalar("f_eval", ld(lk->f_eval));
+        tr.append_scalar("q_lookup_eval", ld(lk->q_lookup_eval));
+        tr.append_scalar("lookup_perm_eval", ld(lk->z2_next_eval));
+        tr.append_scalar("h_1_eval", ld(lk->h1_eval));
+        tr.append_scalar("h_1_next_eval", ld(lk->h1_next_eval));
+        tr.append_scalar("h_2_eval", ld(lk->h2_eval));
+        const CustomEvaluationsC *cu = &ev->custom_evals;
+        tr.append_scalar("q_arith_eval", ld(cu->q_arith_eval));
+        tr.append_scalar("q_c_eval", ld(cu->q_c_eval));
+        tr.append_scalar("q_l_eval", ld(cu->q_l_eval));
+        tr.append_scalar("q_r_eval", ld(cu->q_r_eval));
+        tr.append_scalar("q_hl_eval", ld(cu->q_hl_eval));
+        tr.append_scalar("q_hr_eval", ld(cu->q_hr_eval));
+        tr.append_scalar("q_h4_eval", ld(cu->q_h4_eval));
+        tr.append_scalar("a_next_eval", ld(cu->a_next_eval));
+        tr.append_scalar("b_next_eval", ld(cu->b_next_eval));
+        tr.append_scalar("d_next_eval", ld(cu->d_next_eval));
 
-    // transcript appends (gen_proof.cuh:373-403)
-    tr.append_scalar("a_eval", ae);
-    tr.append_scalar("b_eval", be);
-    tr.append_scalar("c_eval", ce);
-    tr.append_scalar("d_eval", de);
-    tr.append_scalar("left_sig_eval", ld(ev->perm_evals.left_sigma_eval));
-    tr.append_scalar("right_sig_eval", ld(ev->perm_evals.right_sigma_eval));
-    tr.append_scalar("out_sig_eval", ld(ev->perm_evals.out_sigma_eval));
-    tr.append_scalar("perm_eval", ld(ev->perm_evals.permutation_eval));
-    const LookupEvaluationsC *lk = &ev->lookup_evals;
-    tr.append_scalar("f_eval", ld(lk->f_eval));
-    tr.append_scalar("q_lookup_eval", ld(lk->q_lookup_eval));
-    tr.append_scalar("lookup_perm_eval", ld(lk->z2_next_eval));
-    tr.append_scalar("h_1_eval", ld(lk->h1_eval));
-    tr.append_scalar("h_1_next_eval", ld(lk->h1_next_eval));
-    tr.append_scalar("h_2_eval", ld(lk->h2_eval));
-    const CustomEvaluationsC *cu = &ev->custom_evals;
-    tr.append_scalar("q_arith_eval", ld(cu->q_arith_eval));
-    tr.append_scalar("q_c_eval", ld(cu->q_c_eval));
-    tr.append_scalar("q_l_eval", ld(cu->q_l_eval));
-    tr.append_scalar("q_r_eval", ld(cu->q_r_eval));
-    tr.append_scalar("q_hl_eval", ld(cu->q_hl_eval));
-    tr.append_scalar("q_hr_eval", ld(cu->q_hr_eval));
-    tr.append_scalar("q_h4_eval", ld(cu->q_h4_eval));
-    tr.append_scalar("a_next_eval", ld(cu->a_next_eval));
-    tr.append_scalar("b_next_eval", ld(cu->b_next_eval));
-    tr.append_scalar("d_next_eval", ld(cu->d_next_eval));
-
-    // ---------------- round 6: openings (gen_proof.cuh:405-463, kzg10.cu:116-145)
-    // Both "aggregate_witness" challenges are squeezed back to back in the
-    // reference (nothing is appended in between), so both witness
-    // polynomials are built first and committed in one batched MSM.
-    uint64_t *comb = ctx->buf("comb", len), *comb2 = ctx->buf("comb2", len);
-    Fr aw = tr.challenge_scalar("aggregate_witness");
-    Fr saw = tr.challenge_scalar("aggregate_witness");
-    {
-        const uint64_t *awp[11] = {lin, pk.left_sigma_coeffs, pk.right_sigma_coeffs,
-                                   pk.out_sigma_coeffs, f_poly, h2_poly, table_poly,
-                                   wpoly[0], wpoly[1], wpoly[2], wpoly[3]};
-        LinArgs oa;
-        oa.k = 0;
-        Fr p = Fr::one();
-        for (int k = 0; k < 11; k++) {
-            bool skip = (k == 4 && f_zero) || (k == 5 && h_zero) || (k == 6 && table_zero);
-            if (!skip) {
-                oa.p[oa.k] = k == 0 ? awp[k] : awp[k] + 4 * q0;  // lin is range-local
-                oa.s[oa.k] = p;
-                oa.k++;
+        // ---------------- round 6: openings (gen_proof.cuh:405-463, kzg10.cu:116-145)
+        // Both "aggregate_witness" challenges are squeezed back to back in the
+        // reference (nothing is appended in between), so both witness
+        // polynomials are built first and committed in one batched MSM.
+        uint64_t *comb = ctx->buf("comb", len), *comb2 = ctx->buf("comb2", len);
+        Fr aw = tr.challenge_scalar("aggregate_witness");
+        Fr saw = tr.challenge_scalar("aggregate_witness");
+        {
+            const uint64_t *awp[11] = {lin, pk.left_sigma_coeffs, pk.right_sigma_coeffs,
+                                       pk.out_sigma_coeffs, f_poly, h2_poly, table_poly,
+                                       wpoly[0], wpoly[1], wpoly[2], wpoly[3]};
+            LinArgs oa;
+            oa.k = 0;
+            Fr p = Fr::one();
+            for (int k = 0; k < 11; k++) {
+                bool skip = (k == 4 && f_zero) || (k == 5 && h_zero) || (k == 6 && table_zero);
+                if (!skip) {
+                    oa.p[oa.k] = k == 0 ? awp[k] : awp[k] + 4 * q0;  // lin is range-local
+                    oa.s[oa.k] = p;
+                    oa.k++;
+                }
+                p = p * aw;
             }
-            p = p * aw;
+            k_lincomb(oa, len, comb, s);
+            div_linear_range(ctx, comb, len, zc, dist);
         }
-        k_lincomb(oa, len, comb, s);
-        div_linear_range(ctx, comb, len, zc, dist);
-    }
-    {
-        const uint64_t *sawp[7] = {z_poly, wpoly[0], wpoly[1], wpoly[3], h1_poly, z2_poly, table_poly};
-        LinArgs oa;
-        oa.k = 0;
-        Fr p = Fr::one();
-        for (int k = 0; k < 7; k++) {
-            bool skip = (k == 4 && h_zero) || (k == 6 && table_zero);
-            if (!skip) {
-                oa.p[oa.k] = sawp[k] + 4 * q0;
-                oa.s[oa.k] = p;
-                oa.k++;
+        {
+            const uint64_t *sawp[7] = {z_poly, wpoly[0], wpoly[1], wpoly[3], h1_poly, z2_poly, table_poly};
+            LinArgs oa;
+            oa.k = 0;
+            Fr p = Fr::one();
+            for (int k = 0; k < 7; k++) {
+                bool skip = (k == 4 && h_zero) || (k == 6 && table_zero);
+                if (!skip) {
+                    oa.p[oa.k] = sawp[k] + 4 * q0;
+                    oa.s[oa.k] = p;
+                    oa.k++;
+                }
+                p = p * saw;
             }
-            p = p * saw;
+            k_lincomb(oa, len, comb2, s);
+            div_linear_range(ctx, comb2, len, zw, dist);
         }
-        k_lincomb(oa, len, comb2, s);
-        div_linear_range(ctx, comb2, len, zw, dist);
+        tm.mark("r6_witness");
+        {
+            const uint64_t *sc[2] = {comb, comb2};
+            CommitmentC *oc[2] = {&out->aw_opening, &out->saw_opening};
+            commit_affine_batch(ctx, sc, 2, n, oc, dist);
+        }
+        tm.mark("r6_commit");
+        break;
     }
-    tm.mark("r6_witness");
-    {
-        const uint64_t *sc[2] = {comb, comb2};
-        CommitmentC *oc[2] = {&out->aw_opening, &out->saw_opening};
-        commit_affine_batch(ctx, sc, 2, n, oc, dist);
-    }
-    tm.mark("r6_commit");
     return PNP_OK;
 }
 
