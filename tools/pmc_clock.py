@@ -45,7 +45,7 @@ def main(root):
             print(f"  pass {p}: {disp[k][p]} dispatches, {ns[k][p] / 1e6:.3f} ms")
         for c in sorted(v):
             print(f"  {c:28s} {v[c]:.6g}")
-        if v.get("SQ_INSTS_VALU"):
+        if v.get("SQ_INSTS_VALU") and "SQ_WAVE_CYCLES" in v:
             print(f"  wave_cycles / VALU inst       {v['SQ_WAVE_CYCLES'] / v['SQ_INSTS_VALU']:.3f}")
             for c in ("SQ_ACTIVE_INST_VALU", "SQ_WAIT_INST_ANY", "SQ_WAIT_ANY"):
                 if c in v:

@@ -564,14 +564,31 @@ void intt_blocks(NttTables &t, uint64_t *d, uint32_t lg_n, int m0, int nb, hipSt
 // transforms Y_m (block-major, `len` entries each, covering u in [q0, q0+len)):
 //   c_(u + n m1) = g^-(u + n m1) / (8n) sum_m w_8^(-m m1) Y_m[u]
 // -> out[m1 len + (u - q0)]: radix-2 8-point inverse DFT per u.
-__global__ __launch_bounds__(256) void k_t_combine(const uint64_t *Y, uint64_t len, uint64_t q0, uint64_t *out, Fr w1, Fr w2,
-                            Fr w3, Fr inv8n, const uint64_t *chi, const uint64_t *clo, Fr gn0, Fr gn1,
-                            Fr gn2, Fr gn3, Fr gn4, Fr gn5, Fr gn6, Fr gn7) {
+// M < 8 blocks (deg t < M n, prover.cpp): the chunks m1 >= M are zero, i.e.
+// sum_m w_8^(-m m1) Y_m = 0 for m1 = M .. 7 — 8 - M linear equations that give
+// the missing Y_M .. Y_7 from Y_0 .. Y_(M-1) (ext, solved on the host); then
+// the same inverse DFT, and only the chunks m1 < M are stored.
+template <int M>
+struct TcombExt {
+    Fr c[M < 8 ? (8 - M) * M : 1];
+};
+template <int M>
+__global__ __launch_bounds__(256) void k_t_combine(const uint64_t *Y, uint64_t len, uint64_t q0, uint64_t *out,
+                                                   TcombExt<M> ext, Fr w1, Fr w2, Fr w3, Fr inv8n,
+                                                   const uint64_t *chi, const uint64_t *clo, Fr gn0, Fr gn1,
+                                                   Fr gn2, Fr gn3, Fr gn4, Fr gn5, Fr gn6, Fr gn7) {
     uint64_t u = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
     if (u >= len) return;
     Fr y[8];
 #pragma unroll
-    for (int m = 0; m < 8; m++) y[m] = load_fr(Y, m * len + u);
+    for (int m = 0; m < M; m++) y[m] = load_fr(Y, m * len + u);
+#pragma unroll
+    for (int e = 0; e < 8 - M; e++) {
+        Fr acc = ext.c[e * M] * y[0];
+#pragma unroll
+        for (int m = 1; m < M; m++) acc += ext.c[e * M + m] * y[m];
+        y[M + e] = acc;
+    }
     // DIF stage h = 4 (twiddles w^k), h = 2 (w^2k), h = 1; output bit-reversed
     const Fr wk[4] = {Fr::one(), w1, w2, w3};
 #pragma unroll
@@ -602,12 +619,13 @@ __global__ __launch_bounds__(256) void k_t_combine(const uint64_t *Y, uint64_t l
 #pragma unroll
     for (int p = 0; p < 8; p++) {
         const int m1 = rev[p];
-        store_fr(out, m1 * len + u, y[p] * (s0 * gn[m1]));
+        if (m1 < M) store_fr(out, m1 * len + u, y[p] * (s0 * gn[m1]));
     }
 }
 
-void t_combine(NttTables &t, const uint64_t *Y, uint64_t len, uint64_t q0, uint64_t *out,
-               uint32_t lg_n, hipStream_t s) {
+template <int M>
+static void t_combine_m(NttTables &t, const uint64_t *Y, uint64_t len, uint64_t q0, uint64_t *out,
+                        uint32_t lg_n, hipStream_t s) {
     ntt_prepare_coset(t, s);
     const uint64_t n = 1ULL << lg_n;
     const Fr w8i = pnp::inverse(host_root(3));
@@ -620,86 +638,53 @@ void t_combine(NttTables &t, const uint64_t *Y, uint64_t len, uint64_t q0, uint6
     Fr gn[8];
     gn[0] = Fr::one();
     for (int k = 1; k < 8; k++) gn[k] = gn[k - 1] * gni;
-    hipLaunchKernelGGL(k_t_combine, dim3((uint32_t)((len + 255) / 256)), dim3(256), 0, s, Y, len, q0, out,
-                       w[1], w[2], w[3], inv8n, t.coset_inv_hi.u64(), t.coset_inv_lo.u64(), gn[0], gn[1],
-                       gn[2], gn[3], gn[4], gn[5], gn[6], gn[7]);
+    TcombExt<M> ext;
+    if (M < 8) {
+        // rows m1 = M .. 7 of sum_m w_8^(-m m1) Y_m = 0: A [Y_M..Y_7] = -B [Y_0..Y_(M-1)],
+        // Gauss-Jordan on [A | -B] (A is a Vandermonde block: invertible)
+        constexpr int E = 8 - M;
+        Fr G[E][8];
+        for (int e = 0; e < E; e++) {
+            const int m1 = M + e;
+            for (int m = 0; m < 8; m++) {
+                const Fr v = pow_u64(w8i, (uint64_t)((m * m1) % 8));
+                if (m >= M) G[e][m - M] = v;
+                else G[e][E + m] = Fr::zero() - v;
+            }
+        }
+        for (int c = 0; c < E; c++) {
+            int p = c;
+            while (G[p][c].is_zero()) p++;
+            if (p != c)
+                for (int j = 0; j < 8; j++) std::swap(G[p][j], G[c][j]);
+            const Fr inv = pnp::inverse(G[c][c]);
+            for (int j = 0; j < 8; j++) G[c][j] = G[c][j] * inv;
+            for (int r = 0; r < E; r++) {
+                if (r == c || G[r][c].is_zero()) continue;
+                const Fr f = G[r][c];
+                for (int j = 0; j < 8; j++) G[r][j] = G[r][j] - f * G[c][j];
+            }
+        }
+        for (int e = 0; e < E; e++)
+            for (int m = 0; m < M; m++) ext.c[e * M + m] = G[e][E + m];
+    }
+    hipLaunchKernelGGL(k_t_combine<M>, dim3((uint32_t)((len + 255) / 256)), dim3(256), 0, s, Y, len, q0, out,
+                       ext, w[1], w[2], w[3], inv8n, t.coset_inv_hi.u64(), t.coset_inv_lo.u64(), gn[0],
+                       gn[1], gn[2], gn[3], gn[4], gn[5], gn[6], gn[7]);
     PNP_HIP(hipGetLastError());
 }
 
-// Coefficients of t from M < 8 coset blocks m = 0 .. M-1 when deg t < M n
-// (prover.cpp: the quotient of a satisfying circuit has degree < 6n, its
-// pieces t_7, t_8 are zero).  From intt_blocks, Y_m[u] = n g^u
-// sum_(k<M) w_8^(m k) g^(k n) t_(k,u): a Vandermonde system in the nodes w_8^m,
-// solved per u with the host-inverted matrix A[k][m] = g^(-k n) V^-1[k][m] / n:
-//   t_(k,u) = g^-u sum_m A[k][m] Y_m[u]  -> out[k n + u]
-template <int M>
-struct CombineMat {
-    Fr a[M * M];
-};
-template <int M>
-__global__ __launch_bounds__(256) void k_t_combine_mat(const uint64_t *Y, uint64_t n, uint64_t *out,
-                                                       CombineMat<M> A, const uint64_t *chi,
-                                                       const uint64_t *clo) {
-    const uint64_t u = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
-    if (u >= n) return;
-    Fr y[M];
-#pragma unroll
-    for (int m = 0; m < M; m++) y[m] = load_fr(Y, m * n + u);
-    const Fr s0 = coset_pow(chi, clo, u);  // g^-u
-    for (int k = 0; k < M; k++) {
-        Fr acc = A.a[k * M] * y[0];
-#pragma unroll
-        for (int m = 1; m < M; m++) acc += A.a[k * M + m] * y[m];
-        store_fr(out, k * n + u, acc * s0);
-    }
-}
-
-template <int M>
-static void t_combine_mat(NttTables &t, const uint64_t *Y, uint64_t *out, uint32_t lg_n, hipStream_t s) {
-    const uint64_t n = 1ULL << lg_n;
-    // V[m][k] = w_8^(m k); Gauss-Jordan on [V | I] over Fr
-    const Fr w8 = host_root(3);
-    Fr V[M][2 * M];
-    for (int m = 0; m < M; m++)
-        for (int k = 0; k < M; k++) {
-            V[m][k] = pow_u64(w8, (uint64_t)(m * k));
-            V[m][M + k] = m == k ? Fr::one() : Fr::zero();
-        }
-    for (int c = 0; c < M; c++) {
-        int p = c;
-        while (V[p][c].is_zero()) p++;  // distinct nodes: V is invertible
-        if (p != c)
-            for (int j = 0; j < 2 * M; j++) std::swap(V[p][j], V[c][j]);
-        const Fr inv = pnp::inverse(V[c][c]);
-        for (int j = 0; j < 2 * M; j++) V[c][j] = V[c][j] * inv;
-        for (int r = 0; r < M; r++) {
-            if (r == c || V[r][c].is_zero()) continue;
-            const Fr f = V[r][c];
-            for (int j = 0; j < 2 * M; j++) V[r][j] = V[r][j] - f * V[c][j];
-        }
-    }
-    Fr nf = Fr::zero();
-    nf.v[0] = (uint32_t)n;
-    nf.v[1] = (uint32_t)(n >> 32);
-    const Fr ninv = pnp::inverse(to_mont(nf)), gni = pnp::inverse(pow_u64(host_gen(), n));
-    CombineMat<M> A;
-    Fr gk = ninv;  // g^(-k n) / n
-    for (int k = 0; k < M; k++) {
-        for (int m = 0; m < M; m++) A.a[k * M + m] = gk * V[k][M + m];
-        gk = gk * gni;
-    }
-    ntt_prepare_coset(t, s);
-    hipLaunchKernelGGL(k_t_combine_mat<M>, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, s, Y, n, out, A,
-                       t.coset_inv_hi.u64(), t.coset_inv_lo.u64());
-    PNP_HIP(hipGetLastError());
+void t_combine(NttTables &t, const uint64_t *Y, uint64_t len, uint64_t q0, uint64_t *out,
+               uint32_t lg_n, hipStream_t s) {
+    t_combine_m<8>(t, Y, len, q0, out, lg_n, s);
 }
 
 void t_combine_blocks(NttTables &t, const uint64_t *Y, int nb, uint64_t *out, uint32_t lg_n, hipStream_t s) {
+    const uint64_t n = 1ULL << lg_n;
     switch (nb) {
-        case 5: t_combine_mat<5>(t, Y, out, lg_n, s); break;
-        case 6: t_combine_mat<6>(t, Y, out, lg_n, s); break;
-        case 7: t_combine_mat<7>(t, Y, out, lg_n, s); break;
-        case 8: t_combine(t, Y, 1ULL << lg_n, 0, out, lg_n, s); break;
+        case 6: t_combine_m<6>(t, Y, n, 0, out, lg_n, s); break;
+        case 7: t_combine_m<7>(t, Y, n, 0, out, lg_n, s); break;
+        case 8: t_combine_m<8>(t, Y, n, 0, out, lg_n, s); break;
         default:
             set_error("t_combine_blocks: %d blocks", nb);
             throw Error(PNP_E_ARG);
