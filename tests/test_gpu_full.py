@@ -71,6 +71,20 @@ def test_msm_2e22_random_vs_oracle(big):
     _check(ctx, srs.data_ptr(), pts, h)
 
 
+@pytest.mark.parametrize("lg", [18, 19])
+def test_msm_rank_range_vs_oracle(big, lg):
+    """The folded MSM at one rank's point range of a 16 / 8-GPU proof at 2^22
+    (2^18 / 2^19 points: the window is c = lg bits, msm_cfg) vs the oracle."""
+    ctx, srs, pts = big
+    m = 1 << lg
+    sc = empty_dev(m)
+    ctx.random_fr(sc.data_ptr(), m, 1000 + lg)
+    ctx.sync()
+    h = from_dev(sc).copy()
+    h[::5] = 0
+    _check(ctx, srs.data_ptr(), np.ascontiguousarray(pts[:m]), h)
+
+
 def test_msm_2e22_degenerate_vs_oracle(big):
     """Repeated bases with equal scalars (equal points inside a bucket piece:
     the exact redo path), r-1, zeros, and ~10^5-entry buckets from a handful

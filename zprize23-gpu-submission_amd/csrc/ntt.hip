@@ -18,6 +18,7 @@
 //     tile pairs swapped through LDS) restores natural order and fuses the
 //     N^-1 and g^-i scalings of the inverse / coset-inverse transforms.
 #include "pnp_internal.h"
+#include "fr29.cuh"
 
 namespace pnp {
 
@@ -77,6 +78,38 @@ const uint64_t *ntt_twiddles(NttTables &t, uint32_t lg, bool inverse, hipStream_
     const uint64_t *p = buf.u64();
     m.emplace(lg, std::move(buf));
     return p;
+}
+
+// a 2^256-form table (32-bit Montgomery Fr) -> its 2^261 form in radix 2^29
+__global__ void k_table_to_r29(const uint64_t *tab, uint64_t count, uint32_t *out) {
+    const uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    if (i >= count) return;
+    const uint32_t *w = reinterpret_cast<const uint32_t *>(tab + 4 * i);
+    R29 c;
+#pragma unroll
+    for (int k = 0; k < 9; k++) c.l[k] = R29_C266[k];
+    const R29 x = r29_canon(r29_mul(r29_from_words(w), c));
+    uint32_t *o = out + 9 * i;
+#pragma unroll
+    for (int k = 0; k < 9; k++) o[k] = x.l[k];
+}
+
+static const uint32_t *to_r29_table(std::map<uint32_t, DevBuf> &m, uint32_t key, const uint64_t *tab,
+                                    uint64_t count, hipStream_t s) {
+    auto it = m.find(key);
+    if (it != m.end()) return static_cast<const uint32_t *>(it->second.p);
+    DevBuf buf(count * 36);
+    hipLaunchKernelGGL(k_table_to_r29, dim3((uint32_t)((count + 255) / 256)), dim3(256), 0, s, tab, count,
+                       static_cast<uint32_t *>(buf.p));
+    PNP_HIP(hipGetLastError());
+    const uint32_t *p = static_cast<const uint32_t *>(buf.p);
+    m.emplace(key, std::move(buf));
+    return p;
+}
+
+static const uint32_t *ntt_twiddles29(NttTables &t, uint32_t lg, bool inverse, hipStream_t s) {
+    const uint64_t half = lg ? (1ULL << (lg - 1)) : 1;
+    return to_r29_table(inverse ? t.inv29 : t.fwd29, lg, ntt_twiddles(t, lg, inverse, s), half, s);
 }
 
 void ntt_prepare_coset(NttTables &t, hipStream_t s) {
@@ -184,6 +217,94 @@ __global__ __launch_bounds__(NTT_THREADS) void k_ntt_pass(uint64_t *data, const 
             dst[0] = lds_lo[e];
             dst[1] = lds_hi[e];
         }
+    }
+}
+
+// The same pass in radix-2^29 arithmetic (fr29.cuh): canonical 2^256-form Fr
+// in and out (the HBM layout is unchanged), nine-limb values in LDS (two
+// 16-byte planes + one 4-byte plane, 36 KiB per tile), twiddles / twists from
+// the 2^261-form tables.  Bounds (tests/test_fr29.py): a DIF level l of the
+// pass doubles the inputs (< 2^l 1.04 r), its difference adds 2^(l+1) r; a DIT
+// level adds a product output (< 4 r) and 4 r; outputs < 2^264 -> r29_canon.
+template <int K, bool DIT>
+__global__ __launch_bounds__(NTT_THREADS) void k_ntt_pass29(uint64_t *data, const uint32_t *tw,
+                                                             uint32_t lg_n, uint32_t lg_hlo,
+                                                             const uint64_t *src, const uint32_t *pre,
+                                                             uint64_t src_mask, const uint32_t *post) {
+    constexpr int G = TILE >> K;
+    __shared__ uint4 l_lo[TILE];
+    __shared__ uint4 l_mid[TILE];
+    __shared__ uint32_t l_top[TILE];
+    auto put = [&](int e, const R29 &x) {
+        l_lo[e] = make_uint4(x.l[0], x.l[1], x.l[2], x.l[3]);
+        l_mid[e] = make_uint4(x.l[4], x.l[5], x.l[6], x.l[7]);
+        l_top[e] = x.l[8];
+    };
+    auto get = [&](int e) {
+        const uint4 a = l_lo[e], b = l_mid[e];
+        R29 x;
+        x.l[0] = a.x; x.l[1] = a.y; x.l[2] = a.z; x.l[3] = a.w;
+        x.l[4] = b.x; x.l[5] = b.y; x.l[6] = b.z; x.l[7] = b.w;
+        x.l[8] = l_top[e];
+        return x;
+    };
+    const uint64_t hlo = 1ULL << lg_hlo;
+    const uint64_t gid0 = (uint64_t)blockIdx.x * G;
+    for (int e = threadIdx.x; e < TILE; e += NTT_THREADS) {
+        const int g = e % G, m = e / G;
+        const uint64_t gid = gid0 + g;
+        const uint64_t j = gid & (hlo - 1), b = gid >> lg_hlo;
+        const uint64_t idx = (b << (lg_hlo + K)) + j + ((uint64_t)m << lg_hlo);
+        const uint4 *p = reinterpret_cast<const uint4 *>((src ? src + 4 * (idx & src_mask) : data + 4 * idx));
+        const uint4 q0 = p[0], q1 = p[1];
+        const uint32_t w[8] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w};
+        R29 x = r29_from_words(w);
+        if (src) x = r29_mul(x, r29_load(pre, idx));
+        put(e, x);
+    }
+    __syncthreads();
+#pragma unroll 1
+    for (int step = 0; step < K; step++) {
+        const int l = DIT ? step : K - 1 - step;
+        const uint32_t sh = lg_n - 1 - lg_hlo - l;
+        const bool unit = lg_hlo == 0 && l == 0;  // half size 1: twiddle 1, no product
+        const uint32_t *kd = R29_KDIF[step];
+        for (int bf = threadIdx.x; bf < TILE / 2; bf += NTT_THREADS) {
+            const int g = bf % G, q = bf / G;
+            const int mlow = q & ((1 << l) - 1);
+            const int m = ((q >> l) << (l + 1)) | mlow;
+            const int e0 = m * G + g, e1 = (m + (1 << l)) * G + g;
+            const uint64_t j = (gid0 + g) & (hlo - 1);
+            const uint64_t r = j + ((uint64_t)mlow << lg_hlo);
+            const R29 a = get(e0), b = get(e1);
+            R29 s, d;
+            if (DIT) {
+                const R29 t = unit ? b : r29_mul(b, r29_load(tw, r << sh));
+                s = r29_add(a, t);
+                d = r29_sub(a, t, R29_KDIT);
+            } else {
+                s = r29_add(a, b);
+                d = r29_sub(a, b, kd);
+                if (!unit) d = r29_mul(d, r29_load(tw, r << sh));
+            }
+            put(e0, s);
+            put(e1, d);
+        }
+        __syncthreads();
+    }
+    for (int e = threadIdx.x; e < TILE; e += NTT_THREADS) {
+        const int g = e % G, m = e / G;
+        const uint64_t gid = gid0 + g;
+        const uint64_t j = gid & (hlo - 1), b = gid >> lg_hlo;
+        const uint64_t idx = (b << (lg_hlo + K)) + j + ((uint64_t)m << lg_hlo);
+        R29 x = get(e);
+        if (post) x = r29_mul(x, r29_load(post, idx));
+        x = r29_canon(x);
+        uint32_t w[8];
+        r29_to_words(x, w);
+        uint4 *dst = reinterpret_cast<uint4 *>(data + 4 * idx);
+        dst[0] = make_uint4(w[0], w[1], w[2], w[3]);
+        dst[1] = make_uint4(w[4], w[5], w[6], w[7]);
     }
 }
 
@@ -342,7 +463,22 @@ __global__ void k_pad_coset(const uint64_t *in, uint64_t *out, uint64_t n, uint6
 struct PassFuse {
     const uint64_t *src = nullptr, *pre = nullptr, *post = nullptr;
     uint64_t src_mask = 0;
+    const uint32_t *pre29 = nullptr, *post29 = nullptr;  // the 2^261 forms of pre / post
 };
+
+// PNP_NTT29=1: the radix-2^29 passes (k_ntt_pass29).  Measured SLOWER than the
+// 32-bit-limb passes on MI355X (same-box, n = 2^22: 12.9 vs 11.6 ms for the
+// <7, DIF> passes of a proof): the v_addc_co_u32 of the 32-bit product issues
+// at the full VALU rate inside the multiply-add chain, so the 29-bit product
+// saves fewer cycles than its 36-byte LDS planes (4 instead of 5 workgroups
+// per CU), extra LDS instructions and per-pass canonicalisation cost.
+static bool ntt29_enabled() {
+    static const bool on = [] {
+        const char *e = getenv("PNP_NTT29");
+        return e && atoi(e) != 0;
+    }();
+    return on;
+}
 __global__ void k_mul_table(uint64_t *d, const uint64_t *T, uint64_t N);
 __global__ void k_lde_twist(const uint64_t *in, const uint64_t *T, uint64_t *out, uint64_t n, uint64_t N);
 
@@ -383,12 +519,34 @@ static void ntt_core(NttTables &t, uint64_t *d, uint32_t lg, bool inverse, bool 
         rem -= ks[p];
     }
     uint32_t lo = dit ? 0 : lg;  // DIF: current top exponent; DIT: current bottom
+    const bool r29 = ntt29_enabled() && (!fz.src || fz.pre29) && (!fz.post || fz.post29);
+    const uint32_t *tw29 = r29 ? ntt_twiddles29(t, lg, inverse, s) : nullptr;
     for (int p = 0; p < npass; p++) {
         const int k = ks[p];
         const uint32_t lg_hlo = dit ? lo : lo - k;
         const uint32_t blocks = (uint32_t)((N >> k) / (TILE >> k));
         const uint64_t *src = p == 0 ? fz.src : nullptr, *pre = p == 0 ? fz.pre : nullptr;
         const uint64_t *post = p == npass - 1 ? fz.post : nullptr;
+        if (r29 && k <= 8) {
+            const uint32_t *pre29 = p == 0 ? fz.pre29 : nullptr, *post29 = p == npass - 1 ? fz.post29 : nullptr;
+            switch (k) {
+#define PNP_CASE29(KK)                                                                              \
+    case KK:                                                                                        \
+        if (dit)                                                                                    \
+            hipLaunchKernelGGL((k_ntt_pass29<KK, true>), dim3(blocks), dim3(NTT_THREADS), 0, s, d, tw29, \
+                               lg, lg_hlo, src, pre29, fz.src_mask, post29);                       \
+        else                                                                                        \
+            hipLaunchKernelGGL((k_ntt_pass29<KK, false>), dim3(blocks), dim3(NTT_THREADS), 0, s, d, tw29, \
+                               lg, lg_hlo, src, pre29, fz.src_mask, post29);                       \
+        break;
+                PNP_CASE29(1) PNP_CASE29(2) PNP_CASE29(3) PNP_CASE29(4)
+                PNP_CASE29(5) PNP_CASE29(6) PNP_CASE29(7) PNP_CASE29(8)
+#undef PNP_CASE29
+            }
+            PNP_HIP(hipGetLastError());
+            lo = dit ? lo + k : lo - k;
+            continue;
+        }
         switch (k) {
 #define PNP_CASE(KK)                                                                               \
     case KK:                                                                                       \
@@ -533,12 +691,18 @@ static void check_blocks(int m0, int nb) {
 // coefficients `in`: the twist is fused into the first DIF pass and the DIF's
 // bit-reversed output is kept ("block-bitrev layout", no reversal pass); the
 // quotient's arrays share the layout and intt_blocks undoes it with a DIT.
+static const uint32_t *block_twist_table29(NttTables &t, uint32_t lg_n, bool inverse, hipStream_t s) {
+    return to_r29_table(inverse ? t.blk_twist_inv29 : t.blk_twist29, lg_n, block_twist_table(t, lg_n, inverse, s),
+                        8ULL << lg_n, s);
+}
+
 void lde_blocks(NttTables &t, const uint64_t *in, uint64_t *out, uint32_t lg_n, int m0, int nb,
                 hipStream_t s) {
     const uint64_t n = 1ULL << lg_n;
     PassFuse fz;
     fz.src = in;
     fz.pre = block_twist_table(t, lg_n, false, s) + 4 * (uint64_t)m0 * n;
+    if (ntt29_enabled()) fz.pre29 = block_twist_table29(t, lg_n, false, s) + 9 * (uint64_t)m0 * n;
     fz.src_mask = n - 1;
     check_blocks(m0, nb);
     ntt_core(t, out, lg_n, false, false, s, (uint64_t)nb, fz);
@@ -556,6 +720,7 @@ void intt_blocks(NttTables &t, uint64_t *d, uint32_t lg_n, int m0, int nb, hipSt
     const uint64_t n = 1ULL << lg_n;
     PassFuse fz;
     fz.post = block_twist_table(t, lg_n, true, s) + 4 * (uint64_t)m0 * n;
+    if (ntt29_enabled()) fz.post29 = block_twist_table29(t, lg_n, true, s) + 9 * (uint64_t)m0 * n;
     check_blocks(m0, nb);
     ntt_core(t, d, lg_n, true, true, s, (uint64_t)nb, fz);
 }

@@ -58,6 +58,9 @@ struct NttTables {
     std::map<uint32_t, DevBuf> lde_twist;
     // block layout twists per lg_n: (g w_8n^m)^j and w_8n^(-m j), block m
     std::map<uint32_t, DevBuf> blk_twist, blk_twist_inv;
+    // the same twiddles / twists times 2^261 in radix 2^29 (9 u32 per entry)
+    // for the radix-2^29 passes (fr29.cuh)
+    std::map<uint32_t, DevBuf> fwd29, inv29, blk_twist29, blk_twist_inv29;
 };
 const uint64_t *ntt_twiddles(NttTables &t, uint32_t lg, bool inverse, hipStream_t s);
 void ntt_prepare_coset(NttTables &t, hipStream_t s);
