@@ -608,8 +608,8 @@ __global__ __launch_bounds__(64) void k_accumulate_redo(const uint32_t *pts29, c
                                                         uint32_t *buckets, uint32_t *head,
                                                         uint32_t *tail, const uint32_t *redo,
                                                         const uint32_t *nredo) {
-    uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
-    if (r >= *nredo) return;
+    // grid-stride over the flagged lanes (none for random inputs: a small grid
+    // that exits at once instead of one lane per accumulation lane)
     auto ld = [pts29](uint32_t i, Fq &x, Fq &y) {
         x = to_fq32(load29(pts29 + PT29 * i));
         y = to_fq32(load29(pts29 + PT29 * i + 14));
@@ -621,7 +621,9 @@ __global__ __launch_bounds__(64) void k_accumulate_redo(const uint32_t *pts29, c
         store_f29(d + 28, from_fq32(p.zz));
         store_f29(d + 42, from_fq32(p.zzz));
     };
-    segment32(redo[r], ld, st, sorted, offs, 1, U, S);
+    const uint32_t cnt = *nredo;
+    for (uint32_t r = blockIdx.x * blockDim.x + threadIdx.x; r < cnt; r += gridDim.x * blockDim.x)
+        segment32(redo[r], ld, st, sorted, offs, 1, U, S);
 }
 
 // ---------------------------------------------------------------- folded table
@@ -819,7 +821,7 @@ static void accumulate_group(MsmWork &wk, MsmGroup &gb, const GroupPlan &gp, con
         PNP_HIP(hipGetLastError());
         // equal / opposite points or infinity inside a piece: exact recomputation
         // of the flagged lanes (the count stays on the device: no host sync)
-        hipLaunchKernelGGL(k_accumulate_redo, dim3((uint32_t)((nthr + 63) / 64)), dim3(64), 0, s, t29,
+        hipLaunchKernelGGL(k_accumulate_redo, dim3((uint32_t)std::min<uint64_t>((nthr + 63) / 64, 1024)), dim3(64), 0, s, t29,
                            sorted, bstart, WB, S, bk29, head, tail, redo, nredo);
         PNP_HIP(hipGetLastError());
         // every bucket into bk29 (in place, F29), reduced by msm_reduce29

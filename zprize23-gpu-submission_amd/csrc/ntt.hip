@@ -737,13 +737,19 @@ template <int M>
 struct TcombExt {
     Fr c[M < 8 ? (8 - M) * M : 1];
 };
+// nz: bit m1 set when chunk m1 has a non-zero coefficient in this range (the
+// chunks that are zero commit to infinity without an MSM)
 template <int M>
 __global__ __launch_bounds__(256) void k_t_combine(const uint64_t *Y, uint64_t len, uint64_t q0, uint64_t *out,
                                                    TcombExt<M> ext, Fr w1, Fr w2, Fr w3, Fr inv8n,
                                                    const uint64_t *chi, const uint64_t *clo, Fr gn0, Fr gn1,
-                                                   Fr gn2, Fr gn3, Fr gn4, Fr gn5, Fr gn6, Fr gn7) {
-    uint64_t u = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
-    if (u >= len) return;
+                                                   Fr gn2, Fr gn3, Fr gn4, Fr gn5, Fr gn6, Fr gn7,
+                                                   unsigned *nz) {
+    __shared__ unsigned bm;
+    if (threadIdx.x == 0) bm = 0;
+    __syncthreads();
+    const uint64_t u = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    if (u < len) {
     Fr y[8];
 #pragma unroll
     for (int m = 0; m < M; m++) y[m] = load_fr(Y, m * len + u);
@@ -781,16 +787,25 @@ __global__ __launch_bounds__(256) void k_t_combine(const uint64_t *Y, uint64_t l
     const Fr s0 = coset_pow(chi, clo, q0 + u) * inv8n;  // g^-u / (8n)
     const Fr gn[8] = {gn0, gn1, gn2, gn3, gn4, gn5, gn6, gn7};
     const int rev[8] = {0, 4, 2, 6, 1, 5, 3, 7};
+    unsigned mask = 0;
 #pragma unroll
     for (int p = 0; p < 8; p++) {
         const int m1 = rev[p];
-        if (m1 < M) store_fr(out, m1 * len + u, y[p] * (s0 * gn[m1]));
+        if (m1 < M) {
+            const Fr v = y[p] * (s0 * gn[m1]);
+            store_fr(out, m1 * len + u, v);
+            if (!v.is_zero()) mask |= 1u << m1;
+        }
     }
+    if (mask) atomicOr(&bm, mask);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0 && bm) atomicOr(nz, bm);
 }
 
 template <int M>
 static void t_combine_m(NttTables &t, const uint64_t *Y, uint64_t len, uint64_t q0, uint64_t *out,
-                        uint32_t lg_n, hipStream_t s) {
+                        uint32_t lg_n, unsigned *nz, hipStream_t s) {
     ntt_prepare_coset(t, s);
     const uint64_t n = 1ULL << lg_n;
     const Fr w8i = pnp::inverse(host_root(3));
@@ -835,21 +850,22 @@ static void t_combine_m(NttTables &t, const uint64_t *Y, uint64_t len, uint64_t 
     }
     hipLaunchKernelGGL(k_t_combine<M>, dim3((uint32_t)((len + 255) / 256)), dim3(256), 0, s, Y, len, q0, out,
                        ext, w[1], w[2], w[3], inv8n, t.coset_inv_hi.u64(), t.coset_inv_lo.u64(), gn[0],
-                       gn[1], gn[2], gn[3], gn[4], gn[5], gn[6], gn[7]);
+                       gn[1], gn[2], gn[3], gn[4], gn[5], gn[6], gn[7], nz);
     PNP_HIP(hipGetLastError());
 }
 
 void t_combine(NttTables &t, const uint64_t *Y, uint64_t len, uint64_t q0, uint64_t *out,
-               uint32_t lg_n, hipStream_t s) {
-    t_combine_m<8>(t, Y, len, q0, out, lg_n, s);
+               uint32_t lg_n, unsigned *nz, hipStream_t s) {
+    t_combine_m<8>(t, Y, len, q0, out, lg_n, nz, s);
 }
 
-void t_combine_blocks(NttTables &t, const uint64_t *Y, int nb, uint64_t *out, uint32_t lg_n, hipStream_t s) {
+void t_combine_blocks(NttTables &t, const uint64_t *Y, int nb, uint64_t *out, uint32_t lg_n, unsigned *nz,
+                      hipStream_t s) {
     const uint64_t n = 1ULL << lg_n;
     switch (nb) {
-        case 6: t_combine_m<6>(t, Y, n, 0, out, lg_n, s); break;
-        case 7: t_combine_m<7>(t, Y, n, 0, out, lg_n, s); break;
-        case 8: t_combine_m<8>(t, Y, n, 0, out, lg_n, s); break;
+        case 6: t_combine_m<6>(t, Y, n, 0, out, lg_n, nz, s); break;
+        case 7: t_combine_m<7>(t, Y, n, 0, out, lg_n, nz, s); break;
+        case 8: t_combine_m<8>(t, Y, n, 0, out, lg_n, nz, s); break;
         default:
             set_error("t_combine_blocks: %d blocks", nb);
             throw Error(PNP_E_ARG);

@@ -77,10 +77,12 @@ void lde_blocks(NttTables &t, const uint64_t *in, uint64_t *out, uint32_t lg_n, 
 void intt_blocks(NttTables &t, uint64_t *d, uint32_t lg_n, int m0, int nb, hipStream_t s);
 // 8-point inverse DFT across blocks + g^-i / (8n): coefficient chunks u in [q0, q0+len)
 void t_combine(NttTables &t, const uint64_t *Y, uint64_t len, uint64_t q0, uint64_t *out,
-               uint32_t lg_n, hipStream_t s);
+               uint32_t lg_n, unsigned *nz, hipStream_t s);
 // coefficient chunks t_1 .. t_nb (out[k n + u]) from blocks 0 .. nb-1 after
-// intt_blocks, for deg t < nb n (nb = 6 .. 8; 8 is t_combine)
-void t_combine_blocks(NttTables &t, const uint64_t *Y, int nb, uint64_t *out, uint32_t lg_n, hipStream_t s);
+// intt_blocks, for deg t < nb n (nb = 6 .. 8; 8 is t_combine).  Both OR into
+// the device word *nz bit k when chunk k has a non-zero coefficient.
+void t_combine_blocks(NttTables &t, const uint64_t *Y, int nb, uint64_t *out, uint32_t lg_n, unsigned *nz,
+                      hipStream_t s);
 void to_blocks(const uint64_t *in, uint64_t *out, uint32_t lg_n, int m0, int nb, hipStream_t s);
 
 // ---- live per-kernel timing with HIP events on the launching stream ----

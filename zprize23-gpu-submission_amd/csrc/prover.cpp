@@ -578,8 +578,10 @@ int prove_impl(pnp_ctx *ctx, const CircuitC *cs, int device_ptrs, ProofC *out, c
         intt_blocks(nt, t_blk, lg, mb0, nbq, s);
         uint64_t *t_poly = ctx->buf("t_poly", 8 * len);
         const int npieces = dist ? 8 : nbq;
+        unsigned *t_nz = reinterpret_cast<unsigned *>(ctx->buf("t_nz", 1));  // bit k: chunk k != 0
+        PNP_HIP(hipMemsetAsync(t_nz, 0, 4, s));
         if (!dist) {
-            t_combine_blocks(nt, t_blk, nbq, t_poly, lg, s);
+            t_combine_blocks(nt, t_blk, nbq, t_poly, lg, t_nz, s);
         } else {
             // all-to-all: rank r' receives, from every rank, that rank's blocks
             // restricted to r''s coefficient range; slots arrive block-major
@@ -603,7 +605,7 @@ int prove_impl(pnp_ctx *ctx, const CircuitC *cs, int device_ptrs, ProofC *out, c
                 set_error("round-4 all-to-all callback failed (%d)", rc);
                 return PNP_E_DEVICE;
             }
-            t_combine(nt, a2a + 4 * (uint64_t)nb * len * world, len, q0, t_poly, lg, s);
+            t_combine(nt, a2a + 4 * (uint64_t)nb * len * world, len, q0, t_poly, lg, t_nz, s);
         }
         tm.mark("r4_intt8");
         CommitmentC *tcm[8] = {&out->t_1_comm, &out->t_2_comm, &out->t_3_comm, &out->t_4_comm,
@@ -616,9 +618,10 @@ int prove_impl(pnp_ctx *ctx, const CircuitC *cs, int device_ptrs, ProofC *out, c
             int nc = 0;
             uint64_t nz[8];
             {
-                bool b[8] = {false, false, false, false, false, false, false, false};
-                k_any_nonzero_n(t_poly, 4 * len, 4 * len, npieces, b, ctx->scratch_b, s);
-                for (int k = 0; k < 8; k++) nz[k] = b[k];
+                unsigned bits = 0;  // flagged by the combine kernel as it wrote the chunks
+                PNP_HIP(hipMemcpyAsync(&bits, t_nz, 4, hipMemcpyDeviceToHost, s));
+                PNP_HIP(hipStreamSynchronize(s));
+                for (int k = 0; k < 8; k++) nz[k] = k < npieces && ((bits >> k) & 1);
             }
             if (dist) {  // a chunk is zero when it is zero on every rank
                 std::vector<uint64_t> all = shard_allgather(ctx, nz, 8);
