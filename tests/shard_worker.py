@@ -2,12 +2,14 @@
 
     RANK=r WORLD_SIZE=N MASTER_ADDR=127.0.0.1 MASTER_PORT=p \
         python shard_worker.py {cpu|gpu} OUT_PREFIX [lg seed]
+        python shard_worker.py full OUT_PREFIX lg gates seed
 
 cpu: exercises pnp.shard.WindowExchange over gloo with host tensors.
 gpu: every rank proves the same seeded instance on cuda:0 with point-range
      sharded MSMs and, when world divides 8, the distributed round 4 (gloo
      exchanges through host memory, since the ranks share one GPU) and writes
-     its ProofC bytes to OUT_PREFIX.<rank>."""
+     its ProofC bytes to OUT_PREFIX.<rank>.
+full: the same over bench.Synthetic at full size (keys GPU-resident)."""
 import os
 import sys
 
@@ -46,6 +48,26 @@ def main():
         assert cb(None, 1 << 20) == 1 and ex.error is not None  # oversize slot -> error code
         with open(f"{out}.{rank}", "w") as f:
             f.write("ok")
+    elif mode == "full":
+        # bench.Synthetic (the HEIGHT=15 instance, GPU-generated) at full size
+        lg, gates, seed = int(sys.argv[3]), int(sys.argv[4]), int(sys.argv[5])
+        sys.path.insert(0, os.path.dirname(HERE))
+        import pnp
+        from pnp import abi
+        from bench import Synthetic
+        from pnp.shard import a2a_bytes_for
+        ctx = pnp.Context(0)
+        ex = WindowExchange(rank, world, device="cuda", a2a_bytes=a2a_bytes_for(lg, world))
+        ctx.set_msm_shard(ex)
+        syn = Synthetic(ctx, lg, gates, seed=seed)
+        ctx.load_prover_key(syn.pk, syn.n, device_ptrs=True)
+        ctx.load_commit_key(syn.ck, syn.n, device_ptrs=True)
+        proof = ctx.prove(syn.cs, device_ptrs=True)
+        assert ex.calls > 0
+        assert (ex.a2a_calls > 0) == (8 % world == 0)
+        with open(f"{out}.{rank}", "wb") as f:
+            f.write(abi.proof_to_bytes(proof))
+        ctx.close()
     else:
         lg, seed = int(sys.argv[3]), int(sys.argv[4])
         import pnp

@@ -63,3 +63,23 @@ def test_sharded_gen_proof_parity(tmp_path, world):
     _launch(world, ["gpu", prefix, str(lg), str(seed)], tmp_path, 600)
     for r in range(world):
         assert open(f"{prefix}.{r}", "rb").read() == exp, f"rank {r}"
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_sharded_full_size_matches_golden(tmp_path, world):
+    """The HEIGHT=15 instance (n = 2^22, bench.Synthetic seed 1) proved by
+    `world` ranks sharing the GPU — point-range MSMs (c = 20, or c = 19 for the
+    2^19-point ranks of world 8), distributed round 4 over 8/world blocks and
+    the all-to-all — equals the golden ProofC the CPU restatement produced
+    (tests/golden/full_2e22_seed1.json) on every rank."""
+    import json
+    path = os.path.join(HERE, "golden", "full_2e22_seed1.json")
+    if not os.path.exists(path):
+        pytest.skip("golden 2^22 proof not generated")
+    with open(path) as f:
+        g = json.load(f)
+    prefix = str(tmp_path / "full")
+    _launch(world, ["full", prefix, str(g["lg"]), str(g["gates"]), str(g["seed"])], tmp_path, 900)
+    for r in range(world):
+        assert open(f"{prefix}.{r}", "rb").read().hex() == g["proof_hex"], f"rank {r}"

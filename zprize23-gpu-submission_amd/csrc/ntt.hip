@@ -153,7 +153,8 @@ __global__ __launch_bounds__(NTT_THREADS) void k_ntt_pass(uint64_t *data, const 
         uint64_t j = gid & (hlo - 1), b = gid >> lg_hlo;
         uint64_t idx = (b << (lg_hlo + K)) + j + ((uint64_t)m << lg_hlo);
         if (src) {
-            Fr x = load_fr(src, idx & src_mask) * load_fr(pre, idx);
+            Fr x = load_fr(src, idx & src_mask);
+            if (pre) x = x * load_fr(pre, idx);
             lds_lo[e] = make_uint4(x.v[0], x.v[1], x.v[2], x.v[3]);
             lds_hi[e] = make_uint4(x.v[4], x.v[5], x.v[6], x.v[7]);
         } else {
@@ -492,10 +493,12 @@ static void ntt_core(NttTables &t, uint64_t *d, uint32_t lg, bool inverse, bool 
     // LDS-tile passes need whole tiles (a tile holds TILE >> lg transforms when
     // lg < LGTILE); otherwise one single-workgroup transform per block
     if (N % TILE != 0 || (lg <= (uint32_t)LGTILE && count == 1)) {
-        if (fz.src) {
+        if (fz.src && fz.pre) {
             hipLaunchKernelGGL(k_lde_twist, dim3((uint32_t)((N + 255) / 256)), dim3(256), 0, s, fz.src,
                                fz.pre, d, fz.src_mask + 1, N);
             PNP_HIP(hipGetLastError());
+        } else if (fz.src) {  // out of place, no twist (src_mask covers N)
+            PNP_HIP(hipMemcpyAsync(d, fz.src, 32 * N, hipMemcpyDeviceToDevice, s));
         }
         for (uint64_t b = 0; b < count; b++) {
             if (dit)
@@ -519,7 +522,7 @@ static void ntt_core(NttTables &t, uint64_t *d, uint32_t lg, bool inverse, bool 
         rem -= ks[p];
     }
     uint32_t lo = dit ? 0 : lg;  // DIF: current top exponent; DIT: current bottom
-    const bool r29 = ntt29_enabled() && (!fz.src || fz.pre29) && (!fz.post || fz.post29);
+    const bool r29 = ntt29_enabled() && !(fz.src && !fz.pre) && (!fz.pre || fz.pre29) && (!fz.post || fz.post29);
     const uint32_t *tw29 = r29 ? ntt_twiddles29(t, lg, inverse, s) : nullptr;
     for (int p = 0; p < npass; p++) {
         const int k = ks[p];
@@ -585,16 +588,28 @@ static void bitrev(uint64_t *d, uint32_t lg, const Scale &sc, hipStream_t s, uin
     PNP_HIP(hipGetLastError());
 }
 
-void ntt_run(NttTables &t, uint64_t *d, uint32_t lg, bool inverse, bool coset, hipStream_t s) {
-    if (lg == 0) return;
+void ntt_run(NttTables &t, uint64_t *d, uint32_t lg, bool inverse, bool coset, hipStream_t s,
+             const uint64_t *src) {
     uint64_t n = 1ULL << lg;
+    if (src && src != d && (lg == 0 || (!inverse && coset))) {
+        PNP_HIP(hipMemcpyAsync(d, src, 32 * n, hipMemcpyDeviceToDevice, s));
+        src = nullptr;
+    }
+    if (lg == 0) return;
     if (coset) ntt_prepare_coset(t, s);
     if (!inverse && coset) {
         hipLaunchKernelGGL(k_coset_scale, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, s, d, n,
                            t.coset_hi.u64(), t.coset_lo.u64());
         PNP_HIP(hipGetLastError());
     }
-    dif(t, d, lg, inverse, s);
+    if (src && src != d) {  // the first pass reads src: no separate copy
+        PassFuse fz;
+        fz.src = src;
+        fz.src_mask = n - 1;
+        ntt_core(t, d, lg, inverse, false, s, 1, fz);
+    } else {
+        dif(t, d, lg, inverse, s);
+    }
     Scale sc{0, Fr::one(), nullptr, nullptr};
     if (inverse) {
         Fr nf = Fr::zero();

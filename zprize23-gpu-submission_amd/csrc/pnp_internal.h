@@ -64,8 +64,10 @@ struct NttTables {
 };
 const uint64_t *ntt_twiddles(NttTables &t, uint32_t lg, bool inverse, hipStream_t s);
 void ntt_prepare_coset(NttTables &t, hipStream_t s);
-// in place natural-order NTT of 2^lg elements
-void ntt_run(NttTables &t, uint64_t *d, uint32_t lg, bool inverse, bool coset, hipStream_t s);
+// natural-order NTT of 2^lg elements in place, or from `src` into d (the first
+// pass reads src: no separate copy)
+void ntt_run(NttTables &t, uint64_t *d, uint32_t lg, bool inverse, bool coset, hipStream_t s,
+             const uint64_t *src = nullptr);
 // out8[i] = i < n ? in[i] * g^i : 0, then forward NTT of size 8n (Ntt_coset::forward)
 void coset_lde8(NttTables &t, const uint64_t *in, uint64_t *out8, uint32_t lg_n, hipStream_t s);
 

@@ -248,10 +248,7 @@ int prove_impl(pnp_ctx *ctx, const CircuitC *cs, int device_ptrs, ProofC *out, c
     }
 
     // ---------------- round 1: witness polynomials (gen_proof.cuh:25-50)
-    for (int j = 0; j < 4; j++) {
-        PNP_HIP(hipMemcpyAsync(wpoly[j], wsc[j], 32 * n, hipMemcpyDeviceToDevice, s));
-        ntt_run(nt, wpoly[j], lg, true, false, s);
-    }
+    for (int j = 0; j < 4; j++) ntt_run(nt, wpoly[j], lg, true, false, s, wsc[j]);
     tm.mark("r1_intt");
     uint64_t *w8buf[4];
     for (int j = 0; j < 4; j++) w8buf[j] = ctx->buf("w8_" + std::to_string(j), NB);
@@ -279,10 +276,9 @@ int prove_impl(pnp_ctx *ctx, const CircuitC *cs, int device_ptrs, ProofC *out, c
     const uint64_t *wconst[4] = {wsc[0], wsc[1], wsc[2], wsc[3]};
     k_query_f(fc, qlk, ng, wconst, tc, zeta, n, s);
     const bool f_zero = !k_any_nonzero(fc, 4 * n, ctx->scratch_b, s);
-    PNP_HIP(hipMemcpyAsync(table_poly, tc, 32 * n, hipMemcpyDeviceToDevice, s));
-    PNP_HIP(hipMemcpyAsync(f_poly, fc, 32 * n, hipMemcpyDeviceToDevice, s));
-    if (!table_zero) ntt_run(nt, table_poly, lg, true, false, s);
-    if (!f_zero) ntt_run(nt, f_poly, lg, true, false, s);
+    // (zero f / table: their polynomials are never read)
+    if (!table_zero) ntt_run(nt, table_poly, lg, true, false, s, tc);
+    if (!f_zero) ntt_run(nt, f_poly, lg, true, false, s, fc);
     // s = sorted concatenation of f and t, halves h1 / h2 (prover.rs:304-329).
     // f = t = 0 (the Merkle circuit): h1 = h2 = 0, commitments at infinity.
     // The f, h1, h2 MSMs are independent of the transcript in between, so
@@ -310,10 +306,8 @@ int prove_impl(pnp_ctx *ctx, const CircuitC *cs, int device_ptrs, ProofC *out, c
                 set_error("lookup: a query value is not in the lookup table (Error::ElementNotIndexed)");
                 return PNP_E_ARG;
             }
-            PNP_HIP(hipMemcpyAsync(h1_poly, h1, 32 * n, hipMemcpyDeviceToDevice, s));
-            PNP_HIP(hipMemcpyAsync(h2_poly, h2, 32 * n, hipMemcpyDeviceToDevice, s));
-            ntt_run(nt, h1_poly, lg, true, false, s);
-            ntt_run(nt, h2_poly, lg, true, false, s);
+            ntt_run(nt, h1_poly, lg, true, false, s, h1);
+            ntt_run(nt, h2_poly, lg, true, false, s, h2);
             sc[nc] = h1_poly;
             oc[nc++] = &out->h_1_comm;
             sc[nc] = h2_poly;
@@ -359,8 +353,7 @@ int prove_impl(pnp_ctx *ctx, const CircuitC *cs, int device_ptrs, ProofC *out, c
     k_batch_inverse(den, n, ctx->scratch_a, s);
     k_mul_inplace(num, den, n, s);
     k_prefix_product(num, n, ctx->scratch_a, s);
-    PNP_HIP(hipMemcpyAsync(z_poly, num, 32 * n, hipMemcpyDeviceToDevice, s));
-    ntt_run(nt, z_poly, lg, true, false, s);
+    ntt_run(nt, z_poly, lg, true, false, s, num);
     tm.mark("r3_z");
     uint64_t *z8 = ctx->buf("z8", NB);
     fork();
@@ -384,8 +377,7 @@ int prove_impl(pnp_ctx *ctx, const CircuitC *cs, int device_ptrs, ProofC *out, c
         k_batch_inverse(den, n, ctx->scratch_a, s);
         k_mul_inplace(num, den, n, s);
         k_prefix_product(num, n, ctx->scratch_a, s);
-        PNP_HIP(hipMemcpyAsync(z2_poly, num, 32 * n, hipMemcpyDeviceToDevice, s));
-        ntt_run(nt, z2_poly, lg, true, false, s);
+        ntt_run(nt, z2_poly, lg, true, false, s, num);
     }
     // z_2_comm is not appended to the transcript (gen_proof.cuh:200-205): its
     // MSM is batched with the quotient chunks in round 4
