@@ -2,10 +2,15 @@
 import numpy as np
 
 
+# torch fills / copies on its own stream; the library works on another one, so
+# every helper waits for torch before handing the buffer over (without this a
+# late zero-fill can overwrite what the library already wrote)
 def to_dev(arr: np.ndarray):
     import torch
     a = np.ascontiguousarray(arr).view(np.int64)
-    return torch.from_numpy(a.copy()).to("cuda")
+    t = torch.from_numpy(a.copy()).to("cuda")
+    torch.cuda.synchronize()
+    return t
 
 
 def from_dev(t, shape_last=4) -> np.ndarray:
@@ -16,4 +21,6 @@ def from_dev(t, shape_last=4) -> np.ndarray:
 
 def empty_dev(n_elems: int, limbs: int = 4):
     import torch
-    return torch.zeros((n_elems, limbs), dtype=torch.int64, device="cuda")
+    t = torch.zeros((n_elems, limbs), dtype=torch.int64, device="cuda")
+    torch.cuda.synchronize()
+    return t
