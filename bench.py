@@ -139,6 +139,7 @@ FQ_PRODUCTS_PER_MADD = 10
 MADS_PER_FQ_PRODUCT = 288
 MADD_ISSUE_CYCLES = 19761
 SIMDS, CLOCK_HZ = 256 * 4, 2.4e9
+HELD_CLOCK_GHZ = 2.10  # k_accumulate29 under load (DVFS), PMC clock pass, profiles/r02_pmc_clock.txt
 UBENCH_FILE = os.path.join(REPO, "profiles", "r02_ubench_ops.txt")
 
 
@@ -345,6 +346,7 @@ def main():
     entries = ctx.kernel_bytes("msm_entries")
     q_ms, q_n = ctx.kernel_stats("quotient")
     q_bytes = ctx.kernel_bytes("quotient")
+    redo_lanes = ctx.kernel_bytes("msm_redo_lanes")
     ctx.kernel_timing(False)
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
@@ -403,7 +405,13 @@ def main():
                          "issue_model": {"peak_gmadd_s": round(valu_peak / 1e9, 3),
                                          "frac": round(madds_per_s / valu_peak, 4),
                                          "basis": "tools/isa_model.py: 19,761 SIMD cycles per 64 "
-                                                  "mixed additions of the compiled kernel"},
+                                                  "mixed additions of the compiled kernel",
+                                         "held_clock_ghz": HELD_CLOCK_GHZ,
+                                         "frac_at_held_clock": round(
+                                             madds_per_s / (valu_peak * HELD_CLOCK_GHZ * 1e9 / CLOCK_HZ), 4),
+                                         "held_clock_basis": "GRBM_GUI_ACTIVE / 8 XCDs / kernel time "
+                                                             "(profiles/r02_pmc_clock.txt)"},
+                         "redo_lanes_per_proof": round(redo_lanes / args.steps, 2),
                          "hbm": {"achieved_gbs": round(achieved, 1), "peak_gbs": HBM_PEAK_GBS,
                                  "frac": round(achieved / HBM_PEAK_GBS, 5),
                                  "basis": "algorithmic bytes n*(96+32) per window sweep"},

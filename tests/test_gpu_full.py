@@ -74,7 +74,7 @@ def test_msm_2e22_random_vs_oracle(big):
 @pytest.mark.parametrize("lg", [18, 19])
 def test_msm_rank_range_vs_oracle(big, lg):
     """The folded MSM at one rank's point range of a 16 / 8-GPU proof at 2^22
-    (2^18 / 2^19 points: the window is c = lg bits, msm_cfg) vs the oracle."""
+    (2^18 / 2^19 points: c = 15 / 20, msm_cfg) vs the oracle."""
     ctx, srs, pts = big
     m = 1 << lg
     sc = empty_dev(m)

@@ -46,10 +46,11 @@ def main():
             ctx.commit_ck(sc.data_ptr(), n)
             acc_ms, _ = ctx.kernel_stats("msm_accumulate")
             fb = ctx.kernel_bytes("msm_exact_fallback")
+            redo = ctx.kernel_bytes("msm_redo_lanes")
             ctx.kernel_timing(False)
             print(json.dumps({"lg": lg, "c": c, "ms_min": round(1e3 * min(ts), 3),
                               "ms_med": round(1e3 * sorted(ts)[2], 3), "accumulate_ms": round(acc_ms, 3),
-                              "exact_fallbacks": fb}), flush=True)
+                              "exact_fallbacks": fb, "redo_lanes": redo}), flush=True)
             ctx.close()
             del srs, sc, tau
             torch.cuda.empty_cache()

@@ -958,13 +958,18 @@ static void msm_local_batch(MsmWork &wk, const uint64_t *d_points, const uint64_
         PNP_HIP(hipStreamWaitEvent(s, evR0, 0));
     }
     std::vector<uint64_t> win[2];
-    uint32_t exc[2] = {0, 0};
+    uint32_t exc[2] = {0, 0}, nredo[2] = {0, 0};
     for (int k = 0; k < ng; k++) {
         win[k].resize((size_t)gp[k].nv * 24);
         PNP_HIP(hipMemcpyAsync(win[k].data(), res[k], win[k].size() * 8, hipMemcpyDeviceToHost, s));
-        if (folded) PNP_HIP(hipMemcpyAsync(&exc[k], wk.grp[k].exc.p, 4, hipMemcpyDeviceToHost, s));
+        if (folded) {
+            PNP_HIP(hipMemcpyAsync(&exc[k], wk.grp[k].exc.p, 4, hipMemcpyDeviceToHost, s));
+            PNP_HIP(hipMemcpyAsync(&nredo[k], wk.grp[k].redo.p, 4, hipMemcpyDeviceToHost, s));
+        }
     }
     PNP_HIP(hipStreamSynchronize(s));
+    // accumulation lanes recomputed exactly (a degenerate step in a piece)
+    if (wk.timer) wk.timer->credit("msm_redo_lanes", (double)nredo[0] + nredo[1]);
     for (int k = 0; k < ng; k++) {
         if (!exc[k]) continue;
         if (wk.timer) wk.timer->credit("msm_exact_fallback", 1);

@@ -19,12 +19,11 @@ inline MsmCfg msm_cfg(uint64_t n, int c = 0, bool folded = false) {
     MsmCfg g;
     int lg = 0;
     while ((1ULL << lg) < n) lg++;
-    // folded: W n entries + ~2.6 NB addition-equivalents of bucket reduction is
-    // least at c = 20 for 2^20+ points and at c = lg for 2^18 / 2^19 points (one
-    // rank's point range of an 8-GPU proof at n = 2^22 is 2^19: 14 windows of
-    // 2^18 buckets instead of 16 of 2^15)
+    // folded: c = 20 from 2^19 points (one rank's range of an 8-GPU proof at
+    // n = 2^22): measured per MSM at 2^19 / 2^20 / 2^21 points, c = 20 beats
+    // 16..19 (tools/msm_c_sweep.sh, profiles/r02_msm_c_sweep.jsonl)
     if (folded)
-        g.c = lg >= 20 ? 20 : lg >= 18 ? lg : (lg - 3 < 4 ? 4 : lg - 3);
+        g.c = lg >= 19 ? 20 : (lg - 3 < 4 ? 4 : lg - 3);
     else
         g.c = lg >= 20 ? 16 : (lg - 3 < 4 ? 4 : lg - 3);
     if (c > 0) g.c = c;
