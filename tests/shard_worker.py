@@ -62,7 +62,18 @@ def main():
         syn = Synthetic(ctx, lg, gates, seed=seed)
         ctx.load_prover_key(syn.pk, syn.n, device_ptrs=True)
         ctx.load_commit_key(syn.ck, syn.n, device_ptrs=True)
-        proof = ctx.prove(syn.cs, device_ptrs=True)
+        # the context keeps block-layout copies of this rank's 8n evaluations
+        # and never reads the caller's 8n arrays again: free them, so that 8
+        # ranks fit one GPU's HBM
+        for k in [k for k, t in syn.keep.items() if t.shape[0] == 8 * syn.n]:
+            del syn.keep[k]
+        torch.cuda.synchronize()
+        torch.cuda.empty_cache()
+        try:
+            proof = ctx.prove(syn.cs, device_ptrs=True)
+        except Exception:
+            print(f"rank {rank}: exchange error: {ex.error!r}", flush=True)
+            raise
         assert ex.calls > 0
         assert (ex.a2a_calls > 0) == (8 % world == 0)
         with open(f"{out}.{rank}", "wb") as f:

@@ -830,7 +830,9 @@ static void accumulate_group(MsmWork &wk, MsmGroup &gb, const GroupPlan &gp, con
         gb.S = S;
         gb.pieces = (uint32_t)(nent / WB / S + 1);
         gb.nthr = nthr;
-        msm_merge_pieces29(bstart, WB, S, gb.pieces, bk29, head, tail, static_cast<uint32_t *>(gb.exc.p), s);
+        need(gb.heavy, (WB + 1) * 4);
+        msm_merge_pieces29(bstart, WB, S, gb.pieces, bk29, head, tail, static_cast<uint32_t *>(gb.exc.p),
+                           static_cast<uint32_t *>(gb.heavy.p), s);
     } else {
         need(gb.seg, nthr * 2 * 24 * 8);
         uint64_t *head = gb.seg.u64(), *tail = head + nthr * 24;

@@ -43,8 +43,10 @@ void msm_merge_pieces(const uint32_t *offs, int nch, uint64_t U, uint32_t S, uin
 // bk29 holds the buckets inside one lane's segment on entry and EVERY bucket
 // (F29, infinity = zero limbs) on exit
 // (an equal / opposite pair of operands sets *exc: see msm_reduce29)
+// `heavy`: U + 1 u32 of scratch (count, then the queued buckets of > 64 pieces)
 void msm_merge_pieces29(const uint32_t *offs, uint64_t U, uint32_t S, uint32_t pieces, uint32_t *bk29,
-                        const uint32_t *head, const uint32_t *tail, uint32_t *exc, hipStream_t s);
+                        const uint32_t *head, const uint32_t *tail, uint32_t *exc, uint32_t *heavy,
+                        hipStream_t s);
 // exact fallback: the same pieces summed in 32-bit Fq into bk (R384)
 void msm_merge_pieces29_exact(const uint32_t *offs, uint64_t U, uint32_t S, uint32_t pieces,
                               const uint32_t *bk29, const uint32_t *head, const uint32_t *tail, uint64_t *bk,

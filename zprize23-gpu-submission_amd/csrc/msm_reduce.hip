@@ -131,10 +131,14 @@ void msm_merge_pieces(const uint32_t *offs, int nch, uint64_t U, uint32_t S, uin
 // the 32-bit Fq products, no per-piece conversion).  A bucket inside one
 // lane's segment is already bk29[u]; else tail29[t0] + head29[t0+1] + ... +
 // head29[t1] is written to bk29[u] (in place); empty buckets become infinity
-// (zero limbs).
+// (zero limbs).  A bucket of more than HEAVY pieces (clustered or repeated
+// scalars, a short top window) is not summed here, where G <= 8 lanes would
+// add its pieces one after another, but queued for k_merge_heavy29.
+constexpr uint32_t MERGE_HEAVY = 64;
 __global__ __launch_bounds__(256) void k_merge_pieces29(const uint32_t *offs, uint64_t U, uint32_t S,
                                                         int G, uint32_t *bk29, const uint32_t *head,
-                                                        const uint32_t *tail, uint32_t *exc) {
+                                                        const uint32_t *tail, uint32_t *exc,
+                                                        uint32_t *heavy, uint32_t *nheavy) {
     __shared__ uint32_t lds[256 * 56];
     const uint64_t g = (blockIdx.x * (uint64_t)blockDim.x + threadIdx.x) / G;
     const int j = threadIdx.x % G;
@@ -146,7 +150,9 @@ __global__ __launch_bounds__(256) void k_merge_pieces29(const uint32_t *offs, ui
             if (j == 0) store_xyzz29(bk29 + 56 * g, inf29());
         } else {
             const uint32_t t0 = s0 / S, t1 = (e0 - 1) / S;
-            if (t0 != t1) {
+            if (t1 - t0 >= MERGE_HEAVY) {
+                if (j == 0) heavy[atomicAdd(nheavy, 1u)] = (uint32_t)g;
+            } else if (t0 != t1) {
                 live = true;
 #pragma unroll 1
                 for (uint32_t k = j; k <= t1 - t0; k += G)
@@ -164,13 +170,46 @@ __global__ __launch_bounds__(256) void k_merge_pieces29(const uint32_t *offs, ui
     if (live && j == 0) store_xyzz29(bk29 + 56 * g, acc);
 }
 
+// the queued heavy buckets, one workgroup each (grid-stride over the queue):
+// 256 lanes sum every 256th piece, then an 8-level LDS tree
+__global__ __launch_bounds__(256) void k_merge_heavy29(const uint32_t *offs, uint32_t S, uint32_t *bk29,
+                                                       const uint32_t *head, const uint32_t *tail, uint32_t *exc,
+                                                       const uint32_t *heavy, const uint32_t *nheavy) {
+    __shared__ uint32_t lds[256 * 56];
+    const uint32_t cnt = *nheavy;
+    uint32_t *mine = lds + 56 * threadIdx.x;
+    for (uint32_t q = blockIdx.x; q < cnt; q += gridDim.x) {
+        const uint32_t g = heavy[q];
+        const uint32_t t0 = offs[g] / S, t1 = (offs[g + 1] - 1) / S;
+        Xyzz29 acc = inf29();
+#pragma unroll 1
+        for (uint32_t k = threadIdx.x; k <= t1 - t0; k += blockDim.x)
+            acc = xadd29_inf(acc, load_xyzz29(k == 0 ? tail + 56ULL * t0 : head + 56ULL * (t0 + k)), exc);
+        for (uint32_t h = blockDim.x / 2; h >= 1; h /= 2) {
+            store_xyzz29(mine, acc);
+            __syncthreads();
+            if (threadIdx.x < h) acc = xadd29_inf(acc, load_xyzz29(mine + 56 * h), exc);
+            __syncthreads();
+        }
+        if (threadIdx.x == 0) store_xyzz29(bk29 + 56ULL * g, acc);
+        __syncthreads();
+    }
+}
+
 void msm_merge_pieces29(const uint32_t *offs, uint64_t U, uint32_t S, uint32_t pieces, uint32_t *bk29,
-                        const uint32_t *head, const uint32_t *tail, uint32_t *exc, hipStream_t s) {
+                        const uint32_t *head, const uint32_t *tail, uint32_t *exc, uint32_t *heavy,
+                        hipStream_t s) {
     int G = 1;
     while (G < 8 && (uint32_t)G * 8 <= pieces) G *= 2;
     const uint64_t blocks = (U * G + 255) / 256;
+    uint32_t *nheavy = heavy, *list = heavy + 1;
+    PNP_HIP(hipMemsetAsync(nheavy, 0, 4, s));
     hipLaunchKernelGGL(k_merge_pieces29, dim3((uint32_t)blocks), dim3(256), 0, s, offs, U, S, G, bk29, head,
-                       tail, exc);
+                       tail, exc, list, nheavy);
+    PNP_HIP(hipGetLastError());
+    // a small grid: it exits at once when nothing was queued
+    hipLaunchKernelGGL(k_merge_heavy29, dim3(256), dim3(256), 0, s, offs, S, bk29, head, tail, exc, list,
+                       nheavy);
     PNP_HIP(hipGetLastError());
 }
 

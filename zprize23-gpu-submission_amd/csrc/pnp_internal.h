@@ -122,6 +122,7 @@ struct KernelTimer {
 struct MsmGroup {
     DevBuf counts, offsets, scan_tmp, ent, fkey, sorted, buckets, seg, redo;
     DevBuf exc;  // folded: an F29 merge / tree addition met equal or opposite operands
+    DevBuf heavy;  // folded: the merge's queue of buckets with many pieces
     uint32_t S = 0, pieces = 0;  // folded: accumulate segment length, pieces per bucket
     uint64_t nthr = 0;           // folded: accumulate lanes (head / tail slots)
 };
