@@ -221,6 +221,145 @@ __global__ __launch_bounds__(NTT_THREADS) void k_ntt_pass(uint64_t *data, const 
     }
 }
 
+// The same pass with two levels per LDS round trip (radix-4 groups): each of
+// 256 lanes reads 4 elements, does the 4 butterflies of two consecutive
+// levels in registers (3 twiddles) and writes 4 elements back, so the tile
+// makes half the LDS round trips and barriers of k_ntt_pass; an odd K ends
+// (DIF) or ends (DIT) with one radix-2 level.  Same indexing and twiddles as
+// k_ntt_pass (level l, group element m: pair distance 2^l in m).
+constexpr int NTT4_THREADS = 256;
+__device__ __forceinline__ Fr lds_get(const uint4 *lo, const uint4 *hi, int e) {
+    const uint4 a = lo[e], b = hi[e];
+    Fr x;
+    x.v[0] = a.x; x.v[1] = a.y; x.v[2] = a.z; x.v[3] = a.w;
+    x.v[4] = b.x; x.v[5] = b.y; x.v[6] = b.z; x.v[7] = b.w;
+    return x;
+}
+__device__ __forceinline__ void lds_put(uint4 *lo, uint4 *hi, int e, const Fr &x) {
+    lo[e] = make_uint4(x.v[0], x.v[1], x.v[2], x.v[3]);
+    hi[e] = make_uint4(x.v[4], x.v[5], x.v[6], x.v[7]);
+}
+template <int K, bool DIT>
+__global__ __launch_bounds__(NTT4_THREADS) void k_ntt_pass4(uint64_t *data, const uint64_t *tw,
+                                                            uint32_t lg_n, uint32_t lg_hlo,
+                                                            const uint64_t *src, const uint64_t *pre,
+                                                            uint64_t src_mask, const uint64_t *post) {
+    constexpr int G = TILE >> K;
+    __shared__ uint4 lds_lo[TILE];
+    __shared__ uint4 lds_hi[TILE];
+    const uint64_t hlo = 1ULL << lg_hlo;
+    const uint64_t gid0 = (uint64_t)blockIdx.x * G;
+    for (int e = threadIdx.x; e < TILE; e += NTT4_THREADS) {
+        const int g = e % G, m = e / G;
+        const uint64_t gid = gid0 + g;
+        const uint64_t j = gid & (hlo - 1), b = gid >> lg_hlo;
+        const uint64_t idx = (b << (lg_hlo + K)) + j + ((uint64_t)m << lg_hlo);
+        if (src) {
+            Fr x = load_fr(src, idx & src_mask);
+            if (pre) x = x * load_fr(pre, idx);
+            lds_put(lds_lo, lds_hi, e, x);
+        } else {
+            const uint4 *p = reinterpret_cast<const uint4 *>(data + 4 * idx);
+            lds_lo[e] = p[0];
+            lds_hi[e] = p[1];
+        }
+    }
+    __syncthreads();
+    // twiddle of a level-l butterfly whose lower element has low bits mlow
+    auto twl = [&](uint64_t j, int l, uint32_t mlow) {
+        return load_fr(tw, (j + ((uint64_t)mlow << lg_hlo)) << (lg_n - 1 - lg_hlo - l));
+    };
+    constexpr int NPAIR = K / 2;
+#pragma unroll 1
+    for (int pr = 0; pr < NPAIR; pr++) {
+        // DIF: levels (hi, hi - 1) from K - 1 down; DIT: (lo, lo + 1) from 0 up
+        const int l = DIT ? 2 * pr : K - 1 - 2 * pr;  // the first level of the pair
+        const int lb = DIT ? l : l - 1;                // the lower of the two
+        for (int q = threadIdx.x; q < TILE / 4; q += NTT4_THREADS) {
+            const int g = q % G, q4 = q / G;
+            const uint32_t ml = q4 & ((1 << lb) - 1);
+            const int m = ((q4 >> lb) << (lb + 2)) | (int)ml;
+            const int e0 = m * G + g, e1 = (m + (1 << lb)) * G + g, e2 = (m + (2 << lb)) * G + g,
+                      e3 = (m + (3 << lb)) * G + g;
+            const uint64_t j = (gid0 + g) & (hlo - 1);
+            Fr x0 = lds_get(lds_lo, lds_hi, e0), x1 = lds_get(lds_lo, lds_hi, e1);
+            Fr x2 = lds_get(lds_lo, lds_hi, e2), x3 = lds_get(lds_lo, lds_hi, e3);
+            const bool unit = lg_hlo == 0 && lb == 0;  // level lb has half size 1
+            if (DIT) {
+                // level lb: (x0, x1), (x2, x3), one twiddle
+                if (unit) {
+                    Fr t = x1; x1 = x0 - t; x0 = x0 + t;
+                    t = x3; x3 = x2 - t; x2 = x2 + t;
+                } else {
+                    const Fr w = twl(j, lb, ml);
+                    Fr t = x1 * w; x1 = x0 - t; x0 = x0 + t;
+                    t = x3 * w; x3 = x2 - t; x2 = x2 + t;
+                }
+                // level lb + 1: (x0, x2) with low bits ml, (x1, x3) with ml + 2^lb
+                Fr t = x2 * twl(j, lb + 1, ml); x2 = x0 - t; x0 = x0 + t;
+                t = x3 * twl(j, lb + 1, ml + (1u << lb)); x3 = x1 - t; x1 = x1 + t;
+            } else {
+                // level lb + 1: (x0, x2) with low bits ml, (x1, x3) with ml + 2^lb
+                Fr d = (x0 - x2) * twl(j, lb + 1, ml); x0 = x0 + x2; x2 = d;
+                d = (x1 - x3) * twl(j, lb + 1, ml + (1u << lb)); x1 = x1 + x3; x3 = d;
+                // level lb: (x0, x1), (x2, x3)
+                if (unit) {
+                    d = x0 - x1; x0 = x0 + x1; x1 = d;
+                    d = x2 - x3; x2 = x2 + x3; x3 = d;
+                } else {
+                    const Fr w = twl(j, lb, ml);
+                    d = (x0 - x1) * w; x0 = x0 + x1; x1 = d;
+                    d = (x2 - x3) * w; x2 = x2 + x3; x3 = d;
+                }
+            }
+            lds_put(lds_lo, lds_hi, e0, x0);
+            lds_put(lds_lo, lds_hi, e1, x1);
+            lds_put(lds_lo, lds_hi, e2, x2);
+            lds_put(lds_lo, lds_hi, e3, x3);
+        }
+        __syncthreads();
+    }
+    if (K & 1) {  // the remaining level: DIF level 0, DIT level K - 1
+        const int l = DIT ? K - 1 : 0;
+        const bool unit = lg_hlo == 0 && l == 0;
+        for (int bf = threadIdx.x; bf < TILE / 2; bf += NTT4_THREADS) {
+            const int g = bf % G, q = bf / G;
+            const int mlow = q & ((1 << l) - 1);
+            const int m = ((q >> l) << (l + 1)) | mlow;
+            const int e0 = m * G + g, e1 = (m + (1 << l)) * G + g;
+            const uint64_t j = (gid0 + g) & (hlo - 1);
+            Fr a = lds_get(lds_lo, lds_hi, e0), b = lds_get(lds_lo, lds_hi, e1), s2, d;
+            if (unit) {
+                s2 = a + b;
+                d = a - b;
+            } else if (DIT) {
+                const Fr t = b * twl(j, l, (uint32_t)mlow);
+                s2 = a + t;
+                d = a - t;
+            } else {
+                s2 = a + b;
+                d = (a - b) * twl(j, l, (uint32_t)mlow);
+            }
+            lds_put(lds_lo, lds_hi, e0, s2);
+            lds_put(lds_lo, lds_hi, e1, d);
+        }
+        __syncthreads();
+    }
+    for (int e = threadIdx.x; e < TILE; e += NTT4_THREADS) {
+        const int g = e % G, m = e / G;
+        const uint64_t gid = gid0 + g;
+        const uint64_t j = gid & (hlo - 1), b = gid >> lg_hlo;
+        const uint64_t idx = (b << (lg_hlo + K)) + j + ((uint64_t)m << lg_hlo);
+        if (post) {
+            store_fr(data, idx, lds_get(lds_lo, lds_hi, e) * load_fr(post, idx));
+        } else {
+            uint4 *dst = reinterpret_cast<uint4 *>(data + 4 * idx);
+            dst[0] = lds_lo[e];
+            dst[1] = lds_hi[e];
+        }
+    }
+}
+
 // The same pass in radix-2^29 arithmetic (fr29.cuh): canonical 2^256-form Fr
 // in and out (the HBM layout is unchanged), nine-limb values in LDS (two
 // 16-byte planes + one 4-byte plane, 36 KiB per tile), twiddles / twists from
@@ -467,6 +606,15 @@ struct PassFuse {
     const uint32_t *pre29 = nullptr, *post29 = nullptr;  // the 2^261 forms of pre / post
 };
 
+// PNP_NTT_R4=0: the radix-2 passes (k_ntt_pass) instead of k_ntt_pass4
+static bool ntt4_enabled() {
+    static const bool on = [] {
+        const char *e = getenv("PNP_NTT_R4");
+        return !(e && atoi(e) == 0);
+    }();
+    return on;
+}
+
 // PNP_NTT29=1: the radix-2^29 passes (k_ntt_pass29).  Measured SLOWER than the
 // 32-bit-limb passes on MI355X (same-box, n = 2^22: 12.9 vs 11.6 ms for the
 // <7, DIF> passes of a proof): the v_addc_co_u32 of the 32-bit product issues
@@ -545,6 +693,28 @@ static void ntt_core(NttTables &t, uint64_t *d, uint32_t lg, bool inverse, bool 
                 PNP_CASE29(1) PNP_CASE29(2) PNP_CASE29(3) PNP_CASE29(4)
                 PNP_CASE29(5) PNP_CASE29(6) PNP_CASE29(7) PNP_CASE29(8)
 #undef PNP_CASE29
+            }
+            PNP_HIP(hipGetLastError());
+            lo = dit ? lo + k : lo - k;
+            continue;
+        }
+        if (ntt4_enabled() && k >= 2) {
+            switch (k) {
+#define PNP_CASE4(KK)                                                                               \
+    case KK:                                                                                        \
+        if (dit)                                                                                    \
+            hipLaunchKernelGGL((k_ntt_pass4<KK, true>), dim3(blocks), dim3(NTT4_THREADS), 0, s, d, tw, \
+                               lg, lg_hlo, src, pre, fz.src_mask, post);                           \
+        else                                                                                        \
+            hipLaunchKernelGGL((k_ntt_pass4<KK, false>), dim3(blocks), dim3(NTT4_THREADS), 0, s, d, tw, \
+                               lg, lg_hlo, src, pre, fz.src_mask, post);                           \
+        break;
+                PNP_CASE4(2) PNP_CASE4(3) PNP_CASE4(4) PNP_CASE4(5) PNP_CASE4(6)
+                PNP_CASE4(7) PNP_CASE4(8) PNP_CASE4(9) PNP_CASE4(10)
+#undef PNP_CASE4
+                default:
+                    set_error("bad NTT pass size %d", k);
+                    throw Error(PNP_E_ARG);
             }
             PNP_HIP(hipGetLastError());
             lo = dit ? lo + k : lo - k;
