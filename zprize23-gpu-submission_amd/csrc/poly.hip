@@ -213,26 +213,35 @@ void k_poly_div_linear(uint64_t *d, uint64_t n, const Fr &z, DevBuf &scratch, hi
 }
 
 // ---------------------------------------------------------------- evaluation
-// partial[b] = sum over block b's chunks of sum_i c_i x^i, for each of np polys
+// partial[p][b] = sum over block b's 256 * EV_K coefficients of c_i x^i for
+// each of NP polys.  Lane t of block b takes the coefficients
+// base + t + 256 k (k < EV_K, coalesced loads), Horner in X = x^256, then one
+// product by x^(base + t) = (x^(256 EV_K))^b x^t: a 9- and an 8-bit power per
+// lane instead of the full x^lo power per 32-coefficient chunk of the
+// previous layout (which cost more products than the Horner steps).
+static constexpr int EV_K = 32;
 template <int NP>
-__global__ __launch_bounds__(256) void k_eval_partial(const uint64_t *const *polys, uint64_t n,
-                                                      Fr x, uint64_t *partial) {
+__global__ __launch_bounds__(256) void k_eval_partial(const uint64_t *const *polys, uint64_t n, Fr x,
+                                                      Fr x256, Fr xblk, uint64_t *partial) {
     __shared__ uint4 red_lo[256], red_hi[256];
-    uint64_t c = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
-    uint64_t lo = c * CHUNK;
+    const uint64_t base = (uint64_t)blockIdx.x * 256 * EV_K + threadIdx.x;
     Fr h[NP];
 #pragma unroll
     for (int p = 0; p < NP; p++) h[p] = Fr::zero();
-    if (lo < n) {
-        uint64_t hi = lo + CHUNK < n ? lo + CHUNK : n;
-        for (uint64_t i = hi; i-- > lo;) {
+#pragma unroll 1
+    for (int k = EV_K - 1; k >= 0; k--) {
+        const uint64_t i = base + 256ull * k;
+        if (i < n) {
 #pragma unroll
-            for (int p = 0; p < NP; p++) h[p] = h[p] * x + load_fr(polys[p], i);
+            for (int p = 0; p < NP; p++) h[p] = h[p] * x256 + load_fr(polys[p], i);
+        } else {
+#pragma unroll
+            for (int p = 0; p < NP; p++) h[p] = h[p] * x256;
         }
-        Fr xs = pow_u64(x, lo);
-#pragma unroll
-        for (int p = 0; p < NP; p++) h[p] = h[p] * xs;
     }
+    const Fr sc = pow_u64(xblk, blockIdx.x) * pow_u64(x, threadIdx.x);  // x^(base)
+#pragma unroll
+    for (int p = 0; p < NP; p++) h[p] = h[p] * sc;
 #pragma unroll
     for (int p = 0; p < NP; p++) {
         red_lo[threadIdx.x] = make_uint4(h[p].v[0], h[p].v[1], h[p].v[2], h[p].v[3]);
@@ -287,8 +296,8 @@ __global__ __launch_bounds__(256) void k_sum_partials(const uint64_t *partial, u
 void k_poly_eval_multi(const uint64_t *const *polys, int npolys, uint64_t n, const Fr &x,
                        DevBuf &scratch, Fr *out, hipStream_t s) {
     if (npolys <= 0) return;
-    uint64_t nc = (n + CHUNK - 1) / CHUNK;
-    uint32_t nb = nblk(nc);
+    const uint32_t nb = (uint32_t)std::max<uint64_t>(1, (n + 256 * EV_K - 1) / (256 * EV_K));
+    const Fr x256 = pow_u64(x, 256), xblk = pow_u64(x, 256ull * EV_K);
     // layout: [8 poly pointers][partials np*nb][results np]
     size_t need = 64 * 8 + (size_t)npolys * nb * 32 + (size_t)npolys * 32 + 64;
     if (scratch.bytes < need) scratch.alloc(need);
@@ -304,7 +313,7 @@ void k_poly_eval_multi(const uint64_t *const *polys, int npolys, uint64_t n, con
         switch (np) {
 #define PNP_EV(K)                                                                                 \
     case K:                                                                                       \
-        hipLaunchKernelGGL(k_eval_partial<K>, dim3(nb), dim3(256), 0, s, dptrs, n, x, pt);      \
+        hipLaunchKernelGGL(k_eval_partial<K>, dim3(nb), dim3(256), 0, s, dptrs, n, x, x256, xblk, pt); \
         break;
             PNP_EV(1) PNP_EV(2) PNP_EV(3) PNP_EV(4) PNP_EV(5) PNP_EV(6) PNP_EV(7) PNP_EV(8)
 #undef PNP_EV
