@@ -1,15 +1,16 @@
 """gen_proof benchmark on MI355X (BASELINE.json metric).
 
-One step = one gen_proof of the HEIGHT=15 Poseidon-Merkle circuit shape
-(3,161,924 gates -> domain n = 2^22, quotient on the 8n = 2^25 coset) with the
-prover key, SRS and witness already resident in HBM (v2 API, pnp_prove with
-device pointers).  Inputs are synthetic (seeded, generated on the GPU by
-pnp_synth_circuit): a SATISFYING random arithmetic circuit of the same size
-(random a, d and selectors, copy cycles b_i = a_pi(i), c solved per gate), so
-the quotient has degree < 6n and t_7 = t_8 = 0 as in the real Merkle circuit;
-zero custom-gate selectors / lookup tables / q_lookup (the Merkle circuit's
-structure); prover-key evaluations = coset LDE of the coefficients; real coset
-points and Z_H values; SRS = [tau^i] G.
+One step = one gen_proof of the HEIGHT=15 Poseidon-Merkle circuit (3,161,924
+gates -> domain n = 2^22, quotient on the 8n = 2^25 coset) with the prover
+key, SRS and witness already resident in HBM (v2 API, pnp_prove with device
+pointers).  Inputs are generated on the GPU (seeded): by default
+(--circuit merkle, pnp_synth_merkle) the reference's own circuit — width-3
+Poseidon with the plonk-hashing constants, the merkle-tree constraint layout
+row for row (checked against tests/merkle_circuit.py), random leaves and
+blinding values; --circuit arith (pnp_synth_circuit) is the round-1 stand-in,
+a satisfying random arithmetic circuit of the same size.  Prover-key
+evaluations = coset LDE of the coefficients; real coset points and Z_H
+values; SRS = [tau^i] G.
 
     python bench.py [--gpus N --steps K --warmup W]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
@@ -38,6 +39,7 @@ sys.path.insert(0, os.path.join(REPO, "zprize23-gpu-submission_amd"))
 HEIGHT15_GATES = 3_161_924
 REF_SECONDS = (9.543495451 + 9.337866544 + 9.287114947 + 9.309883876) / 4  # TOP-README:16-19
 HBM_PEAK_GBS = 8000.0                      # MI355X_MICROARCH.md, spec
+R_MOD = 0x73eda753299d7d483339d80809a1d80553bda402fffe5bfeffffffff00000001
 METRIC = "gen_proof wall-clock (s), HEIGHT=15 Poseidon tree, 1/2/4/8 MI355X + HBM GB/s"
 
 
@@ -51,11 +53,11 @@ class Synthetic:
     POLYS = ("q_l", "q_r", "q_o", "q_4", "q_c", "q_hl", "q_hr", "q_h4", "q_arith",
              "left_sigma", "right_sigma", "out_sigma", "fourth_sigma")
 
-    def __init__(self, ctx, lg_n: int, gates: int, seed: int):
+    def __init__(self, ctx, lg_n: int, gates: int, seed: int, circuit: str = "arith"):
         import torch
         from pnp import abi
         n, N8 = 1 << lg_n, 8 << lg_n
-        self.n, self.lg_n, self.gates = n, lg_n, gates
+        self.n, self.lg_n = n, lg_n
         dev = "cuda"
         keep = self.keep = {}
 
@@ -66,21 +68,50 @@ class Synthetic:
             return t.data_ptr()
 
         s = seed * 1000
-        # satisfying random arithmetic circuit (pnp_synth_circuit): random a, d
-        # and selectors, b_i = a_pi(i) copy cycles, c solved from each gate
-        w = {name: alloc(name, gates) for name in ("w_l", "w_r", "w_o", "w_4")}
-        ctx.random_fr(w["w_l"], gates, s + 1)
-        ctx.random_fr(w["w_4"], gates, s + 4)
-        qlk = alloc("q_lookup", gates)
-        self.pi = (C.c_uint64 * 4)(123456789 + seed, 0, 0, 0)
-        ev = {p: alloc(p + "_nevals", n) for p in self.POLYS}
         sel_in = ("q_l", "q_r", "q_o", "q_4", "q_c", "q_hl", "q_hr", "q_h4")
-        for i, p in enumerate(sel_in):
-            ctx.random_fr(ev[p], n, s + 100 + i)
-        ctx.synth_circuit([w["w_l"], w["w_r"], w["w_o"], w["w_4"]],
-                          [ev[p] for p in sel_in] + [ev["q_arith"]],
-                          [ev[p] for p in ("left_sigma", "right_sigma", "out_sigma", "fourth_sigma")],
-                          n, gates, 7, list(self.pi))
+        ev = {p: alloc(p + "_nevals", n) for p in self.POLYS}
+        if circuit == "merkle":
+            # the reference's own circuit (pnp_synth_merkle, checked row for row
+            # against tests/merkle_circuit.py): HEIGHT = lg - 7 (15 at 2^22),
+            # random leaves and blinding values, PI = -root at the last gate
+            sys.path.insert(0, os.path.join(REPO, "tests"))
+            from poseidon import PoseidonConstants, flat_constants
+            height = lg_n - 7
+            gates = 193 * ((1 << (height - 1)) - 1) + 5
+            w = {name: alloc(name, gates) for name in ("w_l", "w_r", "w_o", "w_4")}
+            leaves = alloc("leaves", 1 << (height - 1))
+            blind = alloc("blind", 8)
+            nodes = alloc("nodes", (1 << (height - 1)) - 1)
+            ctx.random_fr(leaves, 1 << (height - 1), s + 1)
+            ctx.random_fr(blind, 8, s + 2)
+            root = ctx.synth_merkle(height, flat_constants(PoseidonConstants()), leaves, blind, nodes,
+                                    [w["w_l"], w["w_r"], w["w_o"], w["w_4"]],
+                                    [ev[p] for p in sel_in] + [ev["q_arith"]],
+                                    [ev[p] for p in ("left_sigma", "right_sigma", "out_sigma", "fourth_sigma")],
+                                    n)
+            ctx.sync()
+            neg = (-root) % R_MOD
+            self.pi = (C.c_uint64 * 4)(*[(neg >> (64 * k)) & (2**64 - 1) for k in range(4)])
+            pi_pos = gates - 1
+            for name in ("leaves", "blind", "nodes"):
+                del keep[name]
+            self.height = height
+        else:
+            # satisfying random arithmetic circuit (pnp_synth_circuit): random a, d
+            # and selectors, b_i = a_pi(i) copy cycles, c solved from each gate
+            w = {name: alloc(name, gates) for name in ("w_l", "w_r", "w_o", "w_4")}
+            ctx.random_fr(w["w_l"], gates, s + 1)
+            ctx.random_fr(w["w_4"], gates, s + 4)
+            self.pi = (C.c_uint64 * 4)(123456789 + seed, 0, 0, 0)
+            pi_pos = 7
+            for i, p in enumerate(sel_in):
+                ctx.random_fr(ev[p], n, s + 100 + i)
+            ctx.synth_circuit([w["w_l"], w["w_r"], w["w_o"], w["w_4"]],
+                              [ev[p] for p in sel_in] + [ev["q_arith"]],
+                              [ev[p] for p in ("left_sigma", "right_sigma", "out_sigma", "fourth_sigma")],
+                              n, gates, pi_pos, list(self.pi))
+        self.gates, self.circuit = gates, circuit
+        qlk = alloc("q_lookup", gates)
         pk = abi.ProverKeyC()
         for p in self.POLYS:
             c = alloc(p + "_coeffs", n)
@@ -122,7 +153,7 @@ class Synthetic:
         ctx.sync()
         self.pk = pk
         self.ck = abi.CommitKeyC(powers_of_g=abi.ptr(srs), powers_of_gamma_g=abi.ptr(empty))
-        self.cs = abi.CircuitC(n=gates, lookup_len=0, intended_pi_pos=7, q_lookup=abi.ptr(qlk),
+        self.cs = abi.CircuitC(n=gates, lookup_len=0, intended_pi_pos=pi_pos, q_lookup=abi.ptr(qlk),
                                pi=C.cast(self.pi, abi.U64P), w_l=abi.ptr(w["w_l"]),
                                w_r=abi.ptr(w["w_r"]), w_o=abi.ptr(w["w_o"]), w_4=abi.ptr(w["w_4"]))
 
@@ -290,6 +321,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--lg", type=int, default=22, help="log2 domain (22 = HEIGHT 15)")
     ap.add_argument("--gates", type=int, default=HEIGHT15_GATES)
+    ap.add_argument("--circuit", default="merkle", choices=("merkle", "arith"),
+                    help="merkle: the reference's Poseidon Merkle circuit (HEIGHT = lg - 7); "
+                         "arith: a random satisfying arithmetic circuit of --gates gates")
     ap.add_argument("--cpu-lg", type=int, default=17, help="CPU baseline sample size; 0 = skip")
     ap.add_argument("--stages", action="store_true", help="print per-stage ms to stderr")
     ap.add_argument("--drop-in", default="v1", choices=("", "v2", "v1"),
@@ -318,7 +352,8 @@ def main():
         from pnp.shard import WindowExchange, a2a_bytes_for
         ctx.set_msm_shard(WindowExchange(rank, world, device=torch.device("cuda", local),
                                          a2a_bytes=a2a_bytes_for(args.lg, world)))
-    syn = Synthetic(ctx, args.lg, gates, seed=1)  # same instance on every rank
+    syn = Synthetic(ctx, args.lg, gates, seed=1, circuit=args.circuit)  # same instance on every rank
+    gates = syn.gates
     ctx.load_prover_key(syn.pk, syn.n, device_ptrs=True)
     ctx.load_commit_key(syn.ck, syn.n, device_ptrs=True)
     log(f"[rank {rank}] synthetic inputs + key load: {time.perf_counter() - t0:.1f}s")
@@ -383,9 +418,12 @@ def main():
             "vs_baseline": round(per_proof / REF_SECONDS, 4) if args.lg == 22 else None,
             "dtype": "u64",
             "data": "synthetic",
-            "config": {"workload": f"HEIGHT=15 gen_proof: {gates} gates, domain 2^{args.lg}, "
+            "config": {"workload": (f"HEIGHT={syn.height} Poseidon Merkle-tree circuit (the reference's "
+                                    f"merkle-tree layout, random leaves)" if args.circuit == "merkle" else
+                                    f"random satisfying arithmetic circuit of the HEIGHT=15 size")
+                                   + f" gen_proof: {gates} gates, domain 2^{args.lg}, "
                                    f"quotient on 2^{args.lg + 3} coset, pk+SRS+witness HBM-resident",
-                       "domain_log2": args.lg, "gates": gates,
+                       "circuit": args.circuit, "domain_log2": args.lg, "gates": gates,
                        "parallelism": (f"msm-point-range-shard + round4-block-shard x{world}"
                                        if world > 1 else "single")},
             "roofline": {"bound": "valu", "kernel": "k_accumulate29 (MSM bucket accumulation)",

@@ -343,6 +343,20 @@ int pnp_synth_srs(pnp_ctx *ctx, uint64_t *d_out, uint64_t n, const uint64_t tau[
 int pnp_synth_circuit(pnp_ctx *ctx, uint64_t *const w[4], uint64_t *const sel[9],
                       uint64_t *const sigma[4], uint64_t n, uint64_t n_gates, uint64_t pi_pos,
                       const uint64_t pi_canon[4]);
+/* The reference's own Poseidon Merkle-tree circuit of height `height`
+ * (merkle-tree/src/constraints.rs:20-107 laid out like the reference composer;
+ * 193 (2^(height-1) - 1) + 5 gates, mirrors tests/merkle_circuit.py):
+ * in:  consts = 199 canonical Fr (4 limbs each): the 189 Poseidon round
+ *      constants, the 3x3 MDS matrix row-major, the domain tag;
+ *      d_leaves = 2^(height-1) Montgomery Fr, d_blind = 8 Montgomery Fr (the
+ *      two blinding rows of StandardComposer::new);
+ * out: d_nodes = the 2^(height-1) - 1 tree nodes (level order, root first),
+ *      w[0..3] wire values of the gates, sel[0..8] = q_l q_r q_o q_4 q_c q_hl
+ *      q_hr q_h4 q_arith and sigma[0..3] evaluations on the n-domain,
+ *      root_canon = the root (PI = -root at row gates - 1). */
+int pnp_synth_merkle(pnp_ctx *ctx, uint32_t height, const uint64_t *consts, const uint64_t *d_leaves,
+                     const uint64_t *d_blind, uint64_t *d_nodes, uint64_t *const w[4], uint64_t *const sel[9],
+                     uint64_t *const sigma[4], uint64_t n, uint64_t root_canon[4]);
 /* d_out[i] = (g * w_8n^i)^n - 1 (v_h on the 8n coset) and the coset points. */
 int pnp_synth_coset_consts(pnp_ctx *ctx, uint64_t *d_vh, uint64_t *d_x, uint32_t lg_n);
 

@@ -220,6 +220,7 @@ class GeneralInputs:
         polys = {name: [r[0].get(name, 0) % R_MOD for r in cp.rows] + [0] * (n - ng) for name in SEL}
         for j, name in enumerate(("left_sigma", "right_sigma", "out_sigma", "fourth_sigma")):
             polys[name] = sig[j]
+        self._sig = sig
         self.nonzero = set()
         for name, vals in polys.items():
             c = ints_to_arr([fr_mont(v) for v in vals])
@@ -264,6 +265,11 @@ class GeneralInputs:
         a["pi"] = np.array(to_limbs(self.pis[0][1], 4), dtype=np.uint64)
         self.pi_pos = self.pis[0][0]
         self._build_structs()
+
+    @property
+    def sigma_evals(self):
+        """The 4 sigma polynomials on the n-domain (Montgomery arrays)."""
+        return [ints_to_arr([fr_mont(v) for v in col]) for col in self._sig]
 
     def _build_structs(self):
         a = self.arrays

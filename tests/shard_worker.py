@@ -51,6 +51,7 @@ def main():
     elif mode == "full":
         # bench.Synthetic (the HEIGHT=15 instance, GPU-generated) at full size
         lg, gates, seed = int(sys.argv[3]), int(sys.argv[4]), int(sys.argv[5])
+        circuit = sys.argv[6] if len(sys.argv) > 6 else "arith"
         sys.path.insert(0, os.path.dirname(HERE))
         import pnp
         from pnp import abi
@@ -59,7 +60,7 @@ def main():
         ctx = pnp.Context(0)
         ex = WindowExchange(rank, world, device="cuda", a2a_bytes=a2a_bytes_for(lg, world))
         ctx.set_msm_shard(ex)
-        syn = Synthetic(ctx, lg, gates, seed=seed)
+        syn = Synthetic(ctx, lg, gates, seed=seed, circuit=circuit)
         ctx.load_prover_key(syn.pk, syn.n, device_ptrs=True)
         ctx.load_commit_key(syn.ck, syn.n, device_ptrs=True)
         # the context keeps block-layout copies of this rank's 8n evaluations

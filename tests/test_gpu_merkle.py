@@ -71,3 +71,43 @@ def test_merkle_wrong_node_all_blocks(pc):
     assert abi.proof_to_bytes(got) == abi.proof_to_bytes(exp)
     assert fallback == 1
     assert not verify(inp.vk(), got, pis_of(inp), inp.tau_mont[0])
+
+
+@pytest.mark.parametrize("height", [4, 8])
+def test_synth_merkle_matches_builder(pc, height):
+    """pnp_synth_merkle (bench's HEIGHT=15 generator) == tests/merkle_circuit.py
+    row for row: wires of every gate, the 9 selectors and 4 sigmas on the whole
+    domain, the root."""
+    import numpy as np
+    import pnp
+    from pnp_testlib import fr_mont, ints_to_arr
+    from gpu_util import to_dev, empty_dev, from_dev
+    import merkle_circuit as mcm
+    cp, nodes = mc.merkle_circuit(height, seed=height, pc=pc)
+    inp = cp.build()
+    n, ng = inp.n, len(cp.rows)
+    ctx = pnp.Context(0)
+    try:
+        leaves = to_dev(ints_to_arr([fr_mont(v) for v in cp.leaves]))
+        blind = to_dev(ints_to_arr([fr_mont(v) for v in cp.blind]))
+        dnodes = empty_dev(len(nodes))
+        w = [empty_dev(ng) for _ in range(4)]
+        sel = [empty_dev(n) for _ in range(9)]
+        sig = [empty_dev(n) for _ in range(4)]
+        root = ctx.synth_merkle(height, mcm.flat_constants(pc), leaves.data_ptr(), blind.data_ptr(),
+                                dnodes.data_ptr(), [t.data_ptr() for t in w], [t.data_ptr() for t in sel],
+                                [t.data_ptr() for t in sig], n)
+        ctx.sync()
+        assert root == nodes[0]
+        for j, name in enumerate(("w_l", "w_r", "w_o", "w_4")):
+            assert np.array_equal(from_dev(w[j]), inp.arrays[name]), name
+        exp_nodes = ints_to_arr([fr_mont(v) for v in nodes])
+        assert np.array_equal(from_dev(dnodes), exp_nodes)
+        names = ("q_l", "q_r", "q_o", "q_4", "q_c", "q_hl", "q_hr", "q_h4", "q_arith")
+        for j, name in enumerate(names):
+            exp = ints_to_arr([fr_mont(r[0].get(name, 0) % mc.R_MOD) for r in cp.rows] + [0] * (n - ng))
+            assert np.array_equal(from_dev(sel[j]), exp), name
+        for j, name in enumerate(("left_sigma", "right_sigma", "out_sigma", "fourth_sigma")):
+            assert np.array_equal(from_dev(sig[j]), inp.sigma_evals[j]), name
+    finally:
+        ctx.close()

@@ -143,18 +143,24 @@ def test_gen_proof_parity_2e14():
     assert _diff(got, exp) == []
 
 
-def test_full_size_height15_properties():
+@pytest.mark.parametrize("circuit", ["arith", "merkle"])
+def test_full_size_height15_properties(circuit):
     """BASELINE config 4 size (3,161,924 gates, n = 2^22): properties that hold
     for any correct prover on a satisfying circuit: deg t < 6n so t_7 = t_8 =
     infinity while t_1..t_6 are not; h1 = h2 = f = infinity; z2 commits to
-    [1, 0, ...] = G; proving is deterministic."""
+    [1, 0, ...] = G; proving is deterministic.  circuit = "merkle" is the
+    reference's own HEIGHT=15 Poseidon Merkle circuit (pnp_synth_merkle): the
+    round-5 check lin(z) = -r_0 (the verifier's equation) passing on the
+    6-block quotient shows the generated witness satisfies every gate and copy
+    constraint."""
     import os
     import sys
     import pnp
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     from bench import Synthetic, HEIGHT15_GATES
     ctx = pnp.Context(0)
-    syn = Synthetic(ctx, 22, HEIGHT15_GATES, seed=5)
+    syn = Synthetic(ctx, 22, HEIGHT15_GATES, seed=5, circuit=circuit)
+    assert syn.gates == HEIGHT15_GATES
     ctx.load_prover_key(syn.pk, syn.n, device_ptrs=True)
     ctx.load_commit_key(syn.ck, syn.n, device_ptrs=True)
     ctx.kernel_timing(True)

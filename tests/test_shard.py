@@ -69,7 +69,7 @@ def test_sharded_gen_proof_parity(tmp_path, world):
 @pytest.mark.parametrize("world", [2, 4, 8])
 def test_sharded_full_size_matches_golden(tmp_path, world):
     """The HEIGHT=15 instance (n = 2^22, bench.Synthetic seed 1) proved by
-    `world` ranks sharing the GPU — point-range MSMs (c = 20, or c = 19 for the
+    `world` ranks sharing the GPU — point-range MSMs (c = 20 down to the
     2^19-point ranks of world 8), distributed round 4 over 8/world blocks and
     the all-to-all — equals the golden ProofC the CPU restatement produced
     (tests/golden/full_2e22_seed1.json) on every rank."""
@@ -89,3 +89,33 @@ def test_sharded_full_size_matches_golden(tmp_path, world):
     _launch(world, ["full", prefix, str(g["lg"]), str(g["gates"]), str(g["seed"])], tmp_path, 900)
     for r in range(world):
         assert open(f"{prefix}.{r}", "rb").read().hex() == g["proof_hex"], f"rank {r}"
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 8])
+def test_sharded_merkle_circuit(tmp_path, world):
+    """The reference's Poseidon Merkle circuit (bench.Synthetic(circuit=
+    "merkle"), HEIGHT = 8 at 2^15: PI at the last gate, the real selector and
+    copy-cycle pattern) proved by `world` ranks equals the single-GPU proof of
+    the same instance (which tests/test_gpu_merkle.py pins to the oracle)."""
+    import torch
+    import pnp
+    from pnp import abi
+    sys.path.insert(0, os.path.dirname(HERE))
+    from bench import Synthetic
+    lg, seed = 15, 4
+    ctx = pnp.Context(0)
+    try:
+        syn = Synthetic(ctx, lg, 0, seed=seed, circuit="merkle")
+        ctx.load_prover_key(syn.pk, syn.n, device_ptrs=True)
+        ctx.load_commit_key(syn.ck, syn.n, device_ptrs=True)
+        exp = abi.proof_to_bytes(ctx.prove(syn.cs, device_ptrs=True))
+    finally:
+        ctx.close()
+    del syn
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    prefix = str(tmp_path / "mk")
+    _launch(world, ["full", prefix, str(lg), "0", str(seed), "merkle"], tmp_path, 600)
+    for r in range(world):
+        assert open(f"{prefix}.{r}", "rb").read() == exp, f"rank {r}"

@@ -310,6 +310,24 @@ int pnp_synth_circuit(pnp_ctx *ctx, uint64_t *const w[4], uint64_t *const sel[9]
                             ctx->stream));
 }
 
+int pnp_synth_merkle(pnp_ctx *ctx, uint32_t height, const uint64_t *consts, const uint64_t *d_leaves,
+                     const uint64_t *d_blind, uint64_t *d_nodes, uint64_t *const w[4], uint64_t *const sel[9],
+                     uint64_t *const sigma[4], uint64_t n, uint64_t root_canon[4]) {
+    if (!ctx || !consts || !d_leaves || !d_blind || !d_nodes || !w || !sel || !sigma || !root_canon)
+        return PNP_E_ARG;
+    try {
+        std::vector<uint64_t> pc(199 * 4);
+        for (int k = 0; k < 199; k++) to_u64_limbs(to_mont(from_u64_limbs<FrP>(consts + 4 * k)), &pc[4 * k]);
+        k_synth_merkle((int)height, pc.data(), d_leaves, d_blind, d_nodes, w, sel, sigma, n, ctx->stream);
+        uint64_t r[4];
+        PNP_HIP(hipMemcpy(r, d_nodes, 32, hipMemcpyDeviceToHost));
+        to_u64_limbs(from_mont(from_u64_limbs<FrP>(r)), root_canon);
+        return PNP_OK;
+    } catch (const Error &e) {
+        return e.code;
+    }
+}
+
 int pnp_synth_coset_consts(pnp_ctx *ctx, uint64_t *d_vh, uint64_t *d_x, uint32_t lg_n) {
     if (!ctx || lg_n > 25) return PNP_E_ARG;
     PNP_TRY(k_coset_consts(d_vh, d_x, lg_n, ctx->stream));

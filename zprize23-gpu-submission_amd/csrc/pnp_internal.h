@@ -182,6 +182,9 @@ void k_random_fr(uint64_t *d, uint64_t n, uint64_t seed, hipStream_t s);
 void k_geometric(uint64_t *d, uint64_t n, const Fr &c0, const Fr &r, hipStream_t s);
 void k_srs(uint64_t *d, uint64_t n, const Fr &tau, hipStream_t s);
 void k_coset_consts(uint64_t *vh, uint64_t *x, uint32_t lg_n, hipStream_t s);
+void k_synth_merkle(int height, const uint64_t *pc_mont_host, const uint64_t *leaves, const uint64_t *blind,
+                    uint64_t *nodes, uint64_t *const w[4], uint64_t *const sel[9], uint64_t *const sigma[4],
+                    uint64_t n, hipStream_t s);
 void k_synth_circuit(uint64_t *const w[4], uint64_t *const sel[9], uint64_t *const sigma[4],
                      uint64_t n, uint64_t n_gates, uint64_t pi_pos, const Fr &pi_mont,
                      hipStream_t s);

@@ -33,7 +33,8 @@ SYMBOLS = ("gen_proof", "pnp_last_error", "pnp_ctx_create", "pnp_ctx_destroy",
            "pnp_set_exchange_a2a",
            "pnp_sync", "pnp_ntt", "pnp_coset_lde8", "pnp_commit", "pnp_commit_ck", "pnp_poly_eval",
            "pnp_poly_div_linear", "pnp_prefix_product", "pnp_batch_inverse",
-           "pnp_synth_random_fr", "pnp_synth_srs", "pnp_synth_coset_consts", "pnp_synth_circuit")
+           "pnp_synth_random_fr", "pnp_synth_srs", "pnp_synth_coset_consts", "pnp_synth_circuit",
+           "pnp_synth_merkle")
 
 
 # int allgather(void *user, uint64_t bytes_per_rank) — pnp_set_msm_shard
@@ -94,6 +95,8 @@ def load(path: str = LIB_PATH):
     lib.pnp_synth_coset_consts.argtypes = [vp, vp, vp, C.c_uint32]
     lib.pnp_synth_circuit.argtypes = [vp, C.c_void_p * 4, C.c_void_p * 9, C.c_void_p * 4, u64, u64,
                                       u64, vp]
+    lib.pnp_synth_merkle.argtypes = [vp, C.c_uint32, vp, vp, vp, vp, C.c_void_p * 4, C.c_void_p * 9,
+                                     C.c_void_p * 4, u64, vp]
     for name in SYMBOLS:
         if name.startswith("pnp_") and name not in ("pnp_last_error", "pnp_ctx_destroy"):
             getattr(lib, name).restype = C.c_int if name != "pnp_last_error" else C.c_char_p
@@ -248,6 +251,18 @@ class Context:
         G = (C.c_void_p * 4)(*sigma)
         p = (C.c_uint64 * 4)(*pi_limbs)
         check(self.lib.pnp_synth_circuit(self.h, W, S, G, n, n_gates, pi_pos, p), "pnp_synth_circuit")
+
+    def synth_merkle(self, height: int, consts, leaves: int, blind: int, nodes: int, w, sel, sigma, n: int):
+        """The reference's Poseidon Merkle circuit (include/pnp_plonk.h):
+        consts = 199 canonical ints (round constants, MDS row-major, tag);
+        leaves / blind / nodes / w / sel / sigma device addresses; returns the
+        root (canonical int)."""
+        cs = (C.c_uint64 * (4 * 199))(*[(v >> (64 * k)) & (2**64 - 1) for v in consts for k in range(4)])
+        root = (C.c_uint64 * 4)()
+        check(self.lib.pnp_synth_merkle(self.h, height, cs, C.c_void_p(leaves), C.c_void_p(blind),
+                                        C.c_void_p(nodes), (C.c_void_p * 4)(*w), (C.c_void_p * 9)(*sel),
+                                        (C.c_void_p * 4)(*sigma), n, root), "pnp_synth_merkle")
+        return sum(int(root[k]) << (64 * k) for k in range(4))
 
     def coset_consts(self, vh: int, x: int, lg_n: int):
         check(self.lib.pnp_synth_coset_consts(self.h, C.c_void_p(vh), C.c_void_p(x), lg_n),
