@@ -229,8 +229,10 @@ def cpu_baseline(lg: int, seconds_budget: float):
     b = cpu_exponent()
     out = {"value": round(dt, 3), "unit": f"s per gen_proof at n=2^{lg}",
            "cores": int(lib.or_num_threads()), "kind": "port",
-           "sample": f"one gen_proof of bench.Synthetic's shape at n=2^{lg} ({gates} gates) with "
-                     f"the C restatement (oracle/, OpenMP), instance generation excluded"}
+           "sample": f"one gen_proof at n=2^{lg} ({gates} gates, bench.Synthetic's --circuit arith "
+                     f"instance: same gate count per domain, selector density and PI handling cost as "
+                     f"the Merkle circuit) with the C restatement (oracle/, OpenMP), instance generation "
+                     f"excluded"}
     if b is not None:
         out["extrapolated_full_s"] = round(dt * (2.0 ** ((22 - lg) * b)), 1)
         out["extrapolation"] = f"t ~ n^{b:.3f} fitted over measured 2^15..2^22 (profiles/r02_cpu_scaling.json)"
