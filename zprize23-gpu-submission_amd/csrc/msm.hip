@@ -524,7 +524,7 @@ __device__ __forceinline__ void unstage_point(const uint4 *st, F29 &x, F29 &y) {
 __global__ __launch_bounds__(256, PNP_ACC_WAVES) void k_accumulate29(const uint32_t *pts29, const uint32_t *sorted,
                                                       const uint32_t *offs, uint64_t U, uint32_t S,
                                                       uint32_t *buckets, uint32_t *head,
-                                                      uint32_t *tail, uint32_t *redo,
+                                                      uint32_t *tail, uint32_t *tailb, uint32_t *redo,
                                                       uint32_t *nredo) {
 #if PNP_ACC_GLDS
     // per wave: the staged point (7 x 64 x 16 B) and the staged next index
@@ -598,7 +598,11 @@ __global__ __launch_bounds__(256, PNP_ACC_WAVES) void k_accumulate29(const uint3
             madd29(acc, x, y);
         }
     }
-    ok &= store29(first ? head + 56 * t : (next > hi ? tail + 56 * t : buckets + 56 * cur), acc);
+    // a bucket continuing past this segment leaves its first piece in tail[t];
+    // tailb[t] names it for the merge (one merge lane per accumulation lane)
+    const bool to_tail = !first && next > hi;
+    ok &= store29(first ? head + 56 * t : (to_tail ? tail + 56 * t : buckets + 56 * cur), acc);
+    tailb[t] = to_tail ? (uint32_t)cur : NO_TAIL;
     if (!ok) redo[atomicAdd(nredo, 1u)] = (uint32_t)t;
 }
 
@@ -808,30 +812,30 @@ static void accumulate_group(MsmWork &wk, MsmGroup &gb, const GroupPlan &gp, con
     const uint64_t nthr = (nent + S - 1) / S;
     if (table) {
         // raw radix-2^29 pieces: buckets inside one segment, then heads, tails
-        need(gb.seg, (WB + 2 * nthr) * 224);
+        need(gb.seg, (WB + 2 * nthr) * 224 + nthr * 4);
         uint32_t *bk29 = static_cast<uint32_t *>(gb.seg.p);
-        uint32_t *head = bk29 + 56 * WB, *tail = head + 56 * nthr;
+        uint32_t *head = bk29 + 56 * WB, *tail = head + 56 * nthr, *tailb = tail + 56 * nthr;
         need(gb.redo, nthr * 4 + 16);
         uint32_t *nredo = static_cast<uint32_t *>(gb.redo.p), *redo = nredo + 4;
         PNP_HIP(hipMemsetAsync(nredo, 0, 4, s));
         const uint32_t *t29 = reinterpret_cast<const uint32_t *>(table);
         const uint32_t blocks = (uint32_t)((nthr + 255) / 256);
         hipLaunchKernelGGL(k_accumulate29, dim3(blocks), dim3(256), 0, s, t29, sorted, bstart, WB, S, bk29,
-                           head, tail, redo, nredo);
+                           head, tail, tailb, redo, nredo);
         PNP_HIP(hipGetLastError());
         // equal / opposite points or infinity inside a piece: exact recomputation
         // of the flagged lanes (the count stays on the device: no host sync)
         hipLaunchKernelGGL(k_accumulate_redo, dim3((uint32_t)std::min<uint64_t>((nthr + 63) / 64, 1024)), dim3(64), 0, s, t29,
                            sorted, bstart, WB, S, bk29, head, tail, redo, nredo);
         PNP_HIP(hipGetLastError());
-        // every bucket into bk29 (in place, F29), reduced by msm_reduce29
+        // split buckets into bk29 (in place, F29; empty ones stay unwritten), reduced by msm_reduce29
         need(gb.exc, 16);
         PNP_HIP(hipMemsetAsync(gb.exc.p, 0, 4, s));
         gb.S = S;
         gb.pieces = (uint32_t)(nent / WB / S + 1);
         gb.nthr = nthr;
         need(gb.heavy, (WB + 1) * 4);
-        msm_merge_pieces29(bstart, WB, S, gb.pieces, bk29, head, tail, static_cast<uint32_t *>(gb.exc.p),
+        msm_merge_pieces29(bstart, WB, S, nthr, tailb, bk29, head, tail, static_cast<uint32_t *>(gb.exc.p),
                            static_cast<uint32_t *>(gb.heavy.p), s);
     } else {
         need(gb.seg, nthr * 2 * 24 * 8);
@@ -854,7 +858,8 @@ static const uint64_t *reduce_group(MsmGroup &gb, const GroupPlan &gp, const Msm
     const uint64_t WB = (uint64_t)gp.nv * g.NB;
     uint64_t *bk = gb.buckets.u64();
     if (folded)  // radix-2^29 buckets in gb.seg, the tree in gb.buckets
-        return msm_reduce29(static_cast<const uint32_t *>(gb.seg.p), (uint64_t)gp.nv, g.NB,
+        return msm_reduce29(static_cast<const uint32_t *>(gb.seg.p), static_cast<const uint32_t *>(gb.offsets.p),
+                            (uint64_t)gp.nv, g.NB,
                             reinterpret_cast<uint32_t *>(bk), static_cast<uint32_t *>(gb.exc.p), s);
     return msm_reduce(bk, (uint64_t)gp.nv, g.NB, bk + WB * 24, s);
 }

@@ -39,14 +39,18 @@ inline MsmCfg msm_cfg(uint64_t n, int c = 0, bool folded = false) {
 void msm_merge_pieces(const uint32_t *offs, int nch, uint64_t U, uint32_t S, uint32_t pieces,
                       const uint64_t *head, const uint64_t *tail, uint64_t *bk, hipStream_t s);
 
-// the same over raw radix-2^29 pieces (folded layout, 56 u32 each, ec29.cuh):
-// bk29 holds the buckets inside one lane's segment on entry and EVERY bucket
-// (F29, infinity = zero limbs) on exit
-// (an equal / opposite pair of operands sets *exc: see msm_reduce29)
-// `heavy`: U + 1 u32 of scratch (count, then the queued buckets of > 64 pieces)
-void msm_merge_pieces29(const uint32_t *offs, uint64_t U, uint32_t S, uint32_t pieces, uint32_t *bk29,
-                        const uint32_t *head, const uint32_t *tail, uint32_t *exc, uint32_t *heavy,
-                        hipStream_t s);
+// the same over raw radix-2^29 pieces (folded layout, 56 u32 each, ec29.cuh),
+// one merge lane per accumulation lane t whose segment ended inside bucket
+// tailb[t] (NO_TAIL otherwise): bk29 holds the buckets inside one lane's
+// segment on entry and every NON-EMPTY bucket (F29) on exit; empty buckets
+// (offs[u] = offs[u + 1]) are left unwritten and read as infinity by
+// msm_reduce29.  (An equal / opposite pair of operands sets *exc: see
+// msm_reduce29.)  `heavy`: U + 1 u32 of scratch (count, then the queued
+// buckets of > 64 pieces).
+constexpr uint32_t NO_TAIL = 0xFFFFFFFFu;
+void msm_merge_pieces29(const uint32_t *offs, uint64_t U, uint32_t S, uint64_t nthr, const uint32_t *tailb,
+                        uint32_t *bk29, const uint32_t *head, const uint32_t *tail, uint32_t *exc,
+                        uint32_t *heavy, hipStream_t s);
 // exact fallback: the same pieces summed in 32-bit Fq into bk (R384)
 void msm_merge_pieces29_exact(const uint32_t *offs, uint64_t U, uint32_t S, uint32_t pieces,
                               const uint32_t *bk29, const uint32_t *head, const uint32_t *tail, uint64_t *bk,
@@ -63,7 +67,9 @@ const uint64_t *msm_reduce(const uint64_t *bk, uint64_t nwin, int NB, uint64_t *
 // an addition met equal or opposite operands (never for random inputs): the
 // results are then wrong and the caller redoes the group with
 // msm_merge_pieces29_exact + msm_reduce (32-bit, exact)
-const uint64_t *msm_reduce29(const uint32_t *bk29, uint64_t nwin, int NB, uint32_t *scratch, uint32_t *exc,
-                             hipStream_t s);
+// `offs`: the nwin*NB + 1 bucket starts (empty buckets are infinity whatever
+// bk29 holds for them)
+const uint64_t *msm_reduce29(const uint32_t *bk29, const uint32_t *offs, uint64_t nwin, int NB,
+                             uint32_t *scratch, uint32_t *exc, hipStream_t s);
 
 }  // namespace pnp

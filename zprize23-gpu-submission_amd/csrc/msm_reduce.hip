@@ -129,45 +129,33 @@ void msm_merge_pieces(const uint32_t *offs, int nch, uint64_t U, uint32_t S, uin
 // Folded layout: the pieces are raw radix-2^29 XYZZ points (56 u32, msm.hip
 // store29) and stay in radix 2^29 (ec29.cuh: shorter dependent chains than
 // the 32-bit Fq products, no per-piece conversion).  A bucket inside one
-// lane's segment is already bk29[u]; else tail29[t0] + head29[t0+1] + ... +
-// head29[t1] is written to bk29[u] (in place); empty buckets become infinity
-// (zero limbs).  A bucket of more than HEAVY pieces (clustered or repeated
-// scalars, a short top window) is not summed here, where G <= 8 lanes would
-// add its pieces one after another, but queued for k_merge_heavy29.
+// lane's segment is already bk29[u].  A bucket u split across lanes t0 < t1 is
+// tail29[t0] + head29[t0+1] + ... + head29[t1]; its merge lane is accumulation
+// lane t0, which recorded u in tailb[t0].  (One lane per BUCKET, the first
+// version, left ~2/3 of every wave idle: with ~3 buckets per accumulation
+// segment only one bucket in three is split.)  Empty buckets are not written
+// (msm_reduce29 reads them as infinity).  A bucket of more than MERGE_HEAVY
+// pieces (clustered or repeated scalars, a short top window) is not summed
+// here, where one lane would add its pieces one after another, but queued
+// for k_merge_heavy29.
 constexpr uint32_t MERGE_HEAVY = 64;
-__global__ __launch_bounds__(256) void k_merge_pieces29(const uint32_t *offs, uint64_t U, uint32_t S,
-                                                        int G, uint32_t *bk29, const uint32_t *head,
-                                                        const uint32_t *tail, uint32_t *exc,
-                                                        uint32_t *heavy, uint32_t *nheavy) {
-    __shared__ uint32_t lds[256 * 56];
-    const uint64_t g = (blockIdx.x * (uint64_t)blockDim.x + threadIdx.x) / G;
-    const int j = threadIdx.x % G;
-    bool live = false;  // a bucket split across lanes: this group sums its pieces
-    Xyzz29 acc = inf29();
-    if (g < U) {
-        const uint32_t s0 = offs[g], e0 = offs[g + 1];
-        if (s0 == e0) {
-            if (j == 0) store_xyzz29(bk29 + 56 * g, inf29());
-        } else {
-            const uint32_t t0 = s0 / S, t1 = (e0 - 1) / S;
-            if (t1 - t0 >= MERGE_HEAVY) {
-                if (j == 0) heavy[atomicAdd(nheavy, 1u)] = (uint32_t)g;
-            } else if (t0 != t1) {
-                live = true;
+__global__ __launch_bounds__(256) void k_merge_tails29(const uint32_t *offs, uint64_t U, uint32_t S, uint64_t nthr,
+                                                       const uint32_t *tailb, uint32_t *bk29, const uint32_t *head,
+                                                       const uint32_t *tail, uint32_t *exc, uint32_t *heavy,
+                                                       uint32_t *nheavy) {
+    const uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    if (t >= nthr || t * S >= offs[U]) return;  // no segment: tailb[t] never written
+    const uint32_t u = tailb[t];
+    if (u == NO_TAIL) return;
+    const uint32_t t1 = (offs[u + 1] - 1) / S;
+    if (t1 - (uint32_t)t >= MERGE_HEAVY) {
+        heavy[atomicAdd(nheavy, 1u)] = u;
+        return;
+    }
+    Xyzz29 acc = load_xyzz29(tail + 56 * t);
 #pragma unroll 1
-                for (uint32_t k = j; k <= t1 - t0; k += G)
-                    acc = xadd29_inf(acc, load_xyzz29(k == 0 ? tail + 56ULL * t0 : head + 56ULL * (t0 + k)), exc);
-            }
-        }
-    }
-    uint32_t *mine = lds + 56 * threadIdx.x;
-    for (int h = G / 2; h >= 1; h /= 2) {
-        store_xyzz29(mine, acc);
-        __syncthreads();
-        if (live && j < h) acc = xadd29_inf(acc, load_xyzz29(mine + 56 * h), exc);
-        __syncthreads();
-    }
-    if (live && j == 0) store_xyzz29(bk29 + 56 * g, acc);
+    for (uint32_t k = (uint32_t)t + 1; k <= t1; k++) acc = xadd29_inf(acc, load_xyzz29(head + 56ULL * k), exc);
+    store_xyzz29(bk29 + 56ULL * u, acc);
 }
 
 // the queued heavy buckets, one workgroup each (grid-stride over the queue):
@@ -196,16 +184,13 @@ __global__ __launch_bounds__(256) void k_merge_heavy29(const uint32_t *offs, uin
     }
 }
 
-void msm_merge_pieces29(const uint32_t *offs, uint64_t U, uint32_t S, uint32_t pieces, uint32_t *bk29,
-                        const uint32_t *head, const uint32_t *tail, uint32_t *exc, uint32_t *heavy,
-                        hipStream_t s) {
-    int G = 1;
-    while (G < 8 && (uint32_t)G * 8 <= pieces) G *= 2;
-    const uint64_t blocks = (U * G + 255) / 256;
+void msm_merge_pieces29(const uint32_t *offs, uint64_t U, uint32_t S, uint64_t nthr, const uint32_t *tailb,
+                        uint32_t *bk29, const uint32_t *head, const uint32_t *tail, uint32_t *exc,
+                        uint32_t *heavy, hipStream_t s) {
     uint32_t *nheavy = heavy, *list = heavy + 1;
     PNP_HIP(hipMemsetAsync(nheavy, 0, 4, s));
-    hipLaunchKernelGGL(k_merge_pieces29, dim3((uint32_t)blocks), dim3(256), 0, s, offs, U, S, G, bk29, head,
-                       tail, exc, list, nheavy);
+    hipLaunchKernelGGL(k_merge_tails29, dim3((uint32_t)((nthr + 255) / 256)), dim3(256), 0, s, offs, U, S, nthr,
+                       tailb, bk29, head, tail, exc, list, nheavy);
     PNP_HIP(hipGetLastError());
     // a small grid: it exits at once when nothing was queued
     hipLaunchKernelGGL(k_merge_heavy29, dim3(256), dim3(256), 0, s, offs, S, bk29, head, tail, exc, list,
@@ -267,16 +252,20 @@ void msm_merge_pieces29_exact(const uint32_t *offs, uint64_t U, uint32_t S, uint
 
 // radix-2^29 tree: the (S, T, D) nodes of k_tree_leafw / k_tree_level, 168
 // u32 per node
+// (bucket u empty, offs[u] = offs[u + 1]: infinity, bk29[u] unwritten)
+__device__ __forceinline__ Xyzz29 bucket29(const uint32_t *bk, const uint32_t *offs, uint64_t u) {
+    return offs[u] == offs[u + 1] ? inf29() : load_xyzz29(bk + 56 * u);
+}
 template <int LW>
-__global__ __launch_bounds__(256) void k_tree_leafw29(const uint32_t *bk, uint64_t nout, uint32_t *out,
-                                                      uint32_t *exc) {
+__global__ __launch_bounds__(256) void k_tree_leafw29(const uint32_t *bk, const uint32_t *offs, uint64_t nout,
+                                                      uint32_t *out, uint32_t *exc) {
     uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
     if (t >= nout) return;
-    const uint32_t *b = bk + 56ULL * LW * t;
-    Xyzz29 S = load_xyzz29(b + 56 * (LW - 1)), T = S;
+    const uint64_t u0 = (uint64_t)LW * t;
+    Xyzz29 S = bucket29(bk, offs, u0 + LW - 1), T = S;
 #pragma unroll 1
     for (int k = LW - 2; k >= 0; k--) {
-        S = xadd29_inf(S, load_xyzz29(b + 56 * k), exc);
+        S = xadd29_inf(S, bucket29(bk, offs, u0 + k), exc);
         T = xadd29_inf(T, S, exc);
     }
     uint32_t *o = out + 168 * t;
@@ -311,8 +300,8 @@ __global__ void k_tree_roots29(const uint32_t *in, uint64_t n, uint64_t *out) {
     if (t < n) store_xyzz(out + 24 * t, to32(load_xyzz29(in + 168 * t + 56)));
 }
 
-const uint64_t *msm_reduce29(const uint32_t *bk29, uint64_t nwin, int NB, uint32_t *scratch, uint32_t *exc,
-                             hipStream_t s) {
+const uint64_t *msm_reduce29(const uint32_t *bk29, const uint32_t *offs, uint64_t nwin, int NB,
+                             uint32_t *scratch, uint32_t *exc, hipStream_t s) {
     // leaves of PNP_LEAF_W buckets (pairs for the small windows of small MSMs)
     const int LW = NB >= 2 * PNP_LEAF_W ? PNP_LEAF_W : 2;
     if (NB < 2 * LW) {
@@ -324,9 +313,9 @@ const uint64_t *msm_reduce29(const uint32_t *bk29, uint64_t nwin, int NB, uint32
     uint64_t *roots = reinterpret_cast<uint64_t *>(scratch + 252 * m);
     const dim3 lgrid((uint32_t)((m + 255) / 256));
     if (LW == 2)
-        hipLaunchKernelGGL(k_tree_leafw29<2>, lgrid, dim3(256), 0, s, bk29, m, a, exc);
+        hipLaunchKernelGGL(k_tree_leafw29<2>, lgrid, dim3(256), 0, s, bk29, offs, m, a, exc);
     else
-        hipLaunchKernelGGL(k_tree_leafw29<PNP_LEAF_W>, lgrid, dim3(256), 0, s, bk29, m, a, exc);
+        hipLaunchKernelGGL(k_tree_leafw29<PNP_LEAF_W>, lgrid, dim3(256), 0, s, bk29, offs, m, a, exc);
     PNP_HIP(hipGetLastError());
     while (m > nwin) {
         m /= 2;
