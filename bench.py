@@ -342,9 +342,18 @@ def main():
         return 2
     import torch
     import torch.distributed as dist
+    # PNP_BENCH_BACKEND=gloo: rehearsal of the multi-rank bench on fewer GPUs
+    # than ranks (ranks share devices round-robin, exchanges through host
+    # memory); the real run is RCCL, one rank per GPU
+    backend = os.environ.get("PNP_BENCH_BACKEND", "nccl")
+    if backend == "gloo":
+        local = local % max(torch.cuda.device_count(), 1)
     torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     import pnp
 
     ctx = pnp.Context(local)
@@ -386,7 +395,7 @@ def main():
     redo_lanes = ctx.kernel_bytes("msm_redo_lanes")
     ctx.kernel_timing(False)
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda" if backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     per_proof = elapsed / args.steps
@@ -462,7 +471,7 @@ def main():
         }
         if args.drop_in and world == 1:
             out["drop_in"] = drop_in(ctx, syn, args.steps, v1=args.drop_in == "v1")
-        if args.cpu_lg:
+        if args.cpu_lg and world == 1:  # the CPU baseline: rank 0 at N = 1 only
             try:
                 out["cpu_baseline"] = cpu_baseline(args.cpu_lg, 30.0)
             except Exception as e:  # the CPU leg must never hide the GPU number
