@@ -61,6 +61,20 @@ K64(k_mad64v, I_MAD64V)
 K64(k_shr64, I_SHR64)
 K64(k_ladd64, I_LADD64)
 
+// FP64 FMA (the 52-bit-limb alternative to radix-2^29 products)
+__global__ void k_fma64(uint64_t *out, uint32_t a) {
+    double r0 = threadIdx.x, r1 = r0 + 1, r2 = r0 + 2, r3 = r0 + 3, r4 = r0 + 4, r5 = r0 + 5, r6 = r0 + 6,
+           r7 = r0 + 7, x = 1.0000001 + a, y = 0.9999999;
+    for (int i = 0; i < ITERS; i++) {
+#define I_FMA64(r) "v_fma_f64 " r ", %8, %9, " r "\n"
+        asm volatile(R8(I_FMA64("%0") I_FMA64("%1") I_FMA64("%2") I_FMA64("%3") I_FMA64("%4") I_FMA64("%5")
+                            I_FMA64("%6") I_FMA64("%7"))
+                     : "+v"(r0), "+v"(r1), "+v"(r2), "+v"(r3), "+v"(r4), "+v"(r5), "+v"(r6), "+v"(r7)
+                     : "v"(x), "v"(y));
+    }
+    out[blockIdx.x * blockDim.x + threadIdx.x] = (uint64_t)(r0 + r1 + r2 + r3 + r4 + r5 + r6 + r7);
+}
+
 // dependent chain latency: one chain per lane, 1 wave per SIMD
 __global__ void k_lat_mad(uint64_t *out, uint32_t a) {
     uint64_t r = threadIdx.x;
@@ -87,7 +101,7 @@ int main() {
         {"v_add3_u32", k_add3, 64}, {"v_and_b32", k_and, 64}, {"v_alignbit_b32", k_align, 64},
         {"v_mul_lo_u32", k_mullo, 64}, {"v_mad_u32_u24", k_mad24, 64}, {"v_cndmask_b32", k_cnd, 64},
         {"v_mad_u64_u32(sdst)", k_mad64, 64}, {"v_mad_u64_u32(vcc)", k_mad64v, 64},
-        {"v_lshrrev_b64", k_shr64, 64}, {"v_lshl_add_u64", k_ladd64, 64}};
+        {"v_lshrrev_b64", k_shr64, 64}, {"v_lshl_add_u64", k_ladd64, 64}, {"v_fma_f64", k_fma64, 64}};
     hipEvent_t e0, e1;
     hipEventCreate(&e0); hipEventCreate(&e1);
     const int blocks = 256 * 8, threads = 256;
