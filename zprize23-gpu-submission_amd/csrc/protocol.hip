@@ -69,28 +69,34 @@ void k_query_f(uint64_t *out, const uint64_t *ql, uint64_t n_gates, const uint64
 
 // num_i = prod_j (w_j + beta k_j w^i + gamma), den_i = prod_j (w_j + beta sigma_j + gamma)
 static constexpr int PCHUNK = 16;
-__global__ void k_perm_numden_(uint64_t *num, uint64_t *den, PermArgs a, uint64_t n) {
-    uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
-    uint64_t lo = t * PCHUNK;
-    if (lo >= n) return;
-    uint64_t hi = lo + PCHUNK < n ? lo + PCHUNK : n;
-    Fr root = pow_u64(a.omega, lo);
-    for (uint64_t i = lo; i < hi; i++) {
+// Grid-stride over the domain (element i = t + k T, T = total lanes): loads
+// coalesced across the wave (one lane per 16 consecutive elements strided
+// every load by 512 B, 1.3 ms at 2^22); x = w^i stepped by w^T; x beta k_j by
+// doublings from x beta (k = 1, 7, 13, 17, as the quotient).
+__global__ void k_perm_numden_(uint64_t *num, uint64_t *den, PermArgs a, Fr step, uint64_t n) {
+    const uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    const uint64_t T = (uint64_t)gridDim.x * blockDim.x;
+    if (t >= n) return;
+    Fr root = pow_u64(a.omega, t);
+    for (uint64_t i = t; i < n; i += T) {
+        const Fr xb = root * a.beta, x2 = xb + xb, x4 = x2 + x2, x8 = x4 + x4;
+        const Fr xk[4] = {xb, x8 - xb, x8 + x4 + xb, x8 + x8 + xb};
         Fr nm = Fr::one(), dn = Fr::one();
 #pragma unroll
         for (int j = 0; j < 4; j++) {
             Fr w = load_fr(a.w[j], i);
-            nm = nm * (w + a.bk[j] * root + a.gamma);
+            nm = nm * (w + xk[j] + a.gamma);
             dn = dn * (w + load_fr(a.sigma[j], i) * a.beta + a.gamma);
         }
         store_fr(num, i, nm);
         store_fr(den, i, dn);
-        root = root * a.omega;
+        root = root * step;
     }
 }
 void k_perm_numden(uint64_t *num, uint64_t *den, const PermArgs &a, uint64_t n, hipStream_t s) {
-    hipLaunchKernelGGL(k_perm_numden_, dim3(nblk((n + PCHUNK - 1) / PCHUNK)), dim3(256), 0, s, num, den,
-                       a, n);
+    const uint64_t blocks = nblk((n + PCHUNK - 1) / PCHUNK);
+    const Fr step = pow_u64(a.omega, blocks * 256);
+    hipLaunchKernelGGL(k_perm_numden_, dim3((uint32_t)blocks), dim3(256), 0, s, num, den, a, step, n);
     PNP_HIP(hipGetLastError());
 }
 
