@@ -28,6 +28,8 @@
 #define I_MULLO(r) "v_mul_lo_u32 " r ", " r ", %8\n"
 #define I_MAD24(r) "v_mad_u32_u24 " r ", " r ", %8, " r "\n"
 #define I_CND(r) "v_cndmask_b32 " r ", " r ", %8, vcc\n"
+#define I_CND64(r) "v_cndmask_b32_e64 " r ", " r ", %8, s[20:21]\n"
+#define I_SUBB(r) "v_subb_co_u32 " r ", vcc, " r ", %8, vcc\n"
 K32(k_add, I_ADD)
 K32(k_addco, I_ADDCO)
 K32(k_addc3, I_ADDC3)
@@ -37,6 +39,19 @@ K32(k_align, I_ALIGN)
 K32(k_mullo, I_MULLO)
 K32(k_mad24, I_MAD24)
 K32(k_cnd, I_CND)
+K32(k_cnd64, I_CND64)
+K32(k_subb, I_SUBB)
+// a cndmask stream as compiled field code uses it: VCC produced by a compare
+// right before (the mask written, then read)
+__global__ void k_cnd_cmp(uint64_t *out, uint32_t a) {
+    uint32_t r0 = threadIdx.x, r1 = r0 + 1, r2 = r0 + 2, r3 = r0 + 3, x = a + threadIdx.x;
+    for (int i = 0; i < ITERS; i++) {
+#define I_CC(r) "v_cmp_gt_u32 vcc, " r ", %4\n v_cndmask_b32 " r ", " r ", %4, vcc\n"
+        asm volatile(R8(I_CC("%0") I_CC("%1") I_CC("%2") I_CC("%3")) : "+v"(r0), "+v"(r1), "+v"(r2), "+v"(r3)
+                     : "v"(x) : "vcc");
+    }
+    out[blockIdx.x * blockDim.x + threadIdx.x] = r0 + r1 + r2 + r3;
+}
 
 #define K64(NAME, INSTR)                                                                    \
     __global__ void NAME(uint64_t *out, uint32_t a) {                                       \
@@ -99,7 +114,8 @@ int main() {
     struct { const char *name; kfn f; double per_iter; } ks[] = {
         {"v_add_u32", k_add, 64}, {"v_add_co_u32(vcc)", k_addco, 64}, {"v_addc_co_u32_e64", k_addc3, 64},
         {"v_add3_u32", k_add3, 64}, {"v_and_b32", k_and, 64}, {"v_alignbit_b32", k_align, 64},
-        {"v_mul_lo_u32", k_mullo, 64}, {"v_mad_u32_u24", k_mad24, 64}, {"v_cndmask_b32", k_cnd, 64},
+        {"v_mul_lo_u32", k_mullo, 64}, {"v_mad_u32_u24", k_mad24, 64}, {"v_cndmask_b32", k_cnd, 64}, {"v_cndmask_b32_e64(sgpr)", k_cnd64, 64},
+        {"v_subb_co_u32(vcc)", k_subb, 64}, {"v_cmp+v_cndmask pair", k_cnd_cmp, 32},
         {"v_mad_u64_u32(sdst)", k_mad64, 64}, {"v_mad_u64_u32(vcc)", k_mad64v, 64},
         {"v_lshrrev_b64", k_shr64, 64}, {"v_lshl_add_u64", k_ladd64, 64}, {"v_fma_f64", k_fma64, 64}};
     hipEvent_t e0, e1;
