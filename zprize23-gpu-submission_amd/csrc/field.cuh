@@ -211,7 +211,9 @@ __device__ __forceinline__ void mac96x2(uint64_t &acc, uint32_t &acc2, uint32_t 
 #define PNP_MONT_VARIANT 0
 #endif
 #include "mont_asm.inc"
-template <class P>
+// REDUCE = false: the result is left in [0, 2P) (no final conditional
+// subtraction); valid for a b < R P, e.g. a < 4P, b < P for Fr (4r < 2^256)
+template <class P, bool REDUCE = true>
 __device__ __forceinline__ Fp<P> mont_mul_dev(const Fp<P> &a, const Fp<P> &b) {
     constexpr int N = P::N;
     Fp<P> r;
@@ -256,7 +258,7 @@ __device__ __forceinline__ Fp<P> mont_mul_dev(const Fp<P> &a, const Fp<P> &b) {
         acc2 = 0;
     }
 #endif
-    reduce_once(r);  // result < 2P < 2^(32N) for both moduli
+    if (REDUCE) reduce_once(r);  // result < 2P < 2^(32N) for both moduli
     return r;
 }
 

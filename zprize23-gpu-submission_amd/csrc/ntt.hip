@@ -239,6 +239,43 @@ __device__ __forceinline__ void lds_put(uint4 *lo, uint4 *hi, int e, const Fr &x
     lo[e] = make_uint4(x.v[0], x.v[1], x.v[2], x.v[3]);
     hi[e] = make_uint4(x.v[4], x.v[5], x.v[6], x.v[7]);
 }
+// Lazy residues inside a radix-4 tile: values stay in [0, 2r) between the
+// levels of a pass and are made canonical when the pass stores them.  The
+// twiddle products skip their final subtraction (a < 2r, w < r: result
+// < r (2r / 2^256 + 1) < 2r); sums and differences stay in [0, 2r) with one
+// conditional step each, as before.  (2r < 2^256 but 4r is not: r = 0.45 *
+// 2^256, so Harvey's unconditional a - b + 2r does not fit 8 limbs.)
+constexpr uint32_t FR_2R[8] = {PNP_LIMB(0xfffffffe00000002), PNP_LIMB(0xa77b4805fffcb7fd),
+                               PNP_LIMB(0x6673b0101343b00a), PNP_LIMB(0xe7db4ea6533afa90)};
+__device__ __forceinline__ Fr lz_add(const Fr &a, const Fr &b) {  // [0, 2r) + [0, 2r) -> [0, 2r)
+    Fr s, t;
+    const uint32_t c = add_n<8>(s.v, a.v, b.v);  // < 4r < 2^257: carry out possible
+    const uint32_t br = sub_n<8>(t.v, s.v, FR_2R);
+    const bool keep = br && !c;                  // s < 2r
+#pragma unroll
+    for (int i = 0; i < 8; i++) s.v[i] = keep ? s.v[i] : t.v[i];
+    return s;
+}
+__device__ __forceinline__ Fr lz_sub(const Fr &a, const Fr &b) {  // [0, 2r) - [0, 2r) -> [0, 2r)
+    Fr d, t;
+    const uint32_t br = sub_n<8>(d.v, a.v, b.v);
+    add_n<8>(t.v, d.v, FR_2R);
+#pragma unroll
+    for (int i = 0; i < 8; i++) d.v[i] = br ? t.v[i] : d.v[i];
+    return d;
+}
+__device__ __forceinline__ Fr lz_mul(const Fr &a, const Fr &w) {  // a < 2r, w < r -> [0, 2r)
+#ifdef __HIP_DEVICE_COMPILE__
+    return mont_mul_dev<FrP, false>(a, w);
+#else
+    return a * w;  // (host pass of the single-source compile; never called)
+#endif
+}
+__device__ __forceinline__ Fr lz_canon(Fr a) {  // [0, 2r) -> [0, r)
+    reduce_once(a);
+    return a;
+}
+
 template <int K, bool DIT>
 __global__ __launch_bounds__(NTT4_THREADS) void k_ntt_pass4(uint64_t *data, const uint64_t *tw,
                                                             uint32_t lg_n, uint32_t lg_hlo,
@@ -285,31 +322,32 @@ __global__ __launch_bounds__(NTT4_THREADS) void k_ntt_pass4(uint64_t *data, cons
             Fr x0 = lds_get(lds_lo, lds_hi, e0), x1 = lds_get(lds_lo, lds_hi, e1);
             Fr x2 = lds_get(lds_lo, lds_hi, e2), x3 = lds_get(lds_lo, lds_hi, e3);
             const bool unit = lg_hlo == 0 && lb == 0;  // level lb has half size 1
+            // (lazy residues in [0, 2r), see lz_add)
             if (DIT) {
                 // level lb: (x0, x1), (x2, x3), one twiddle
                 if (unit) {
-                    Fr t = x1; x1 = x0 - t; x0 = x0 + t;
-                    t = x3; x3 = x2 - t; x2 = x2 + t;
+                    Fr t = x1; x1 = lz_sub(x0, t); x0 = lz_add(x0, t);
+                    t = x3; x3 = lz_sub(x2, t); x2 = lz_add(x2, t);
                 } else {
                     const Fr w = twl(j, lb, ml);
-                    Fr t = x1 * w; x1 = x0 - t; x0 = x0 + t;
-                    t = x3 * w; x3 = x2 - t; x2 = x2 + t;
+                    Fr t = lz_mul(x1, w); x1 = lz_sub(x0, t); x0 = lz_add(x0, t);
+                    t = lz_mul(x3, w); x3 = lz_sub(x2, t); x2 = lz_add(x2, t);
                 }
                 // level lb + 1: (x0, x2) with low bits ml, (x1, x3) with ml + 2^lb
-                Fr t = x2 * twl(j, lb + 1, ml); x2 = x0 - t; x0 = x0 + t;
-                t = x3 * twl(j, lb + 1, ml + (1u << lb)); x3 = x1 - t; x1 = x1 + t;
+                Fr t = lz_mul(x2, twl(j, lb + 1, ml)); x2 = lz_sub(x0, t); x0 = lz_add(x0, t);
+                t = lz_mul(x3, twl(j, lb + 1, ml + (1u << lb))); x3 = lz_sub(x1, t); x1 = lz_add(x1, t);
             } else {
                 // level lb + 1: (x0, x2) with low bits ml, (x1, x3) with ml + 2^lb
-                Fr d = (x0 - x2) * twl(j, lb + 1, ml); x0 = x0 + x2; x2 = d;
-                d = (x1 - x3) * twl(j, lb + 1, ml + (1u << lb)); x1 = x1 + x3; x3 = d;
+                Fr d = lz_mul(lz_sub(x0, x2), twl(j, lb + 1, ml)); x0 = lz_add(x0, x2); x2 = d;
+                d = lz_mul(lz_sub(x1, x3), twl(j, lb + 1, ml + (1u << lb))); x1 = lz_add(x1, x3); x3 = d;
                 // level lb: (x0, x1), (x2, x3)
                 if (unit) {
-                    d = x0 - x1; x0 = x0 + x1; x1 = d;
-                    d = x2 - x3; x2 = x2 + x3; x3 = d;
+                    d = lz_sub(x0, x1); x0 = lz_add(x0, x1); x1 = d;
+                    d = lz_sub(x2, x3); x2 = lz_add(x2, x3); x3 = d;
                 } else {
                     const Fr w = twl(j, lb, ml);
-                    d = (x0 - x1) * w; x0 = x0 + x1; x1 = d;
-                    d = (x2 - x3) * w; x2 = x2 + x3; x3 = d;
+                    d = lz_mul(lz_sub(x0, x1), w); x0 = lz_add(x0, x1); x1 = d;
+                    d = lz_mul(lz_sub(x2, x3), w); x2 = lz_add(x2, x3); x3 = d;
                 }
             }
             lds_put(lds_lo, lds_hi, e0, x0);
@@ -330,15 +368,15 @@ __global__ __launch_bounds__(NTT4_THREADS) void k_ntt_pass4(uint64_t *data, cons
             const uint64_t j = (gid0 + g) & (hlo - 1);
             Fr a = lds_get(lds_lo, lds_hi, e0), b = lds_get(lds_lo, lds_hi, e1), s2, d;
             if (unit) {
-                s2 = a + b;
-                d = a - b;
+                s2 = lz_add(a, b);
+                d = lz_sub(a, b);
             } else if (DIT) {
-                const Fr t = b * twl(j, l, (uint32_t)mlow);
-                s2 = a + t;
-                d = a - t;
+                const Fr t = lz_mul(b, twl(j, l, (uint32_t)mlow));
+                s2 = lz_add(a, t);
+                d = lz_sub(a, t);
             } else {
-                s2 = a + b;
-                d = (a - b) * twl(j, l, (uint32_t)mlow);
+                s2 = lz_add(a, b);
+                d = lz_mul(lz_sub(a, b), twl(j, l, (uint32_t)mlow));
             }
             lds_put(lds_lo, lds_hi, e0, s2);
             lds_put(lds_lo, lds_hi, e1, d);
@@ -350,13 +388,11 @@ __global__ __launch_bounds__(NTT4_THREADS) void k_ntt_pass4(uint64_t *data, cons
         const uint64_t gid = gid0 + g;
         const uint64_t j = gid & (hlo - 1), b = gid >> lg_hlo;
         const uint64_t idx = (b << (lg_hlo + K)) + j + ((uint64_t)m << lg_hlo);
-        if (post) {
+        // canonical out: the reducing product (x < 2r, post < r) or one subtraction
+        if (post)
             store_fr(data, idx, lds_get(lds_lo, lds_hi, e) * load_fr(post, idx));
-        } else {
-            uint4 *dst = reinterpret_cast<uint4 *>(data + 4 * idx);
-            dst[0] = lds_lo[e];
-            dst[1] = lds_hi[e];
-        }
+        else
+            store_fr(data, idx, lz_canon(lds_get(lds_lo, lds_hi, e)));
     }
 }
 
