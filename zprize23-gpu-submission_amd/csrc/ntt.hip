@@ -227,7 +227,10 @@ __global__ __launch_bounds__(NTT_THREADS) void k_ntt_pass(uint64_t *data, const 
 // makes half the LDS round trips and barriers of k_ntt_pass; an odd K ends
 // (DIF) or ends (DIT) with one radix-2 level.  Same indexing and twiddles as
 // k_ntt_pass (level l, group element m: pair distance 2^l in m).
-constexpr int NTT4_THREADS = 256;
+#ifndef PNP_NTT4_THREADS
+#define PNP_NTT4_THREADS 256
+#endif
+constexpr int NTT4_THREADS = PNP_NTT4_THREADS;
 __device__ __forceinline__ Fr lds_get(const uint4 *lo, const uint4 *hi, int e) {
     const uint4 a = lo[e], b = hi[e];
     Fr x;
@@ -293,7 +296,7 @@ __global__ __launch_bounds__(NTT4_THREADS) void k_ntt_pass4(uint64_t *data, cons
         const uint64_t idx = (b << (lg_hlo + K)) + j + ((uint64_t)m << lg_hlo);
         if (src) {
             Fr x = load_fr(src, idx & src_mask);
-            if (pre) x = x * load_fr(pre, idx);
+            if (pre) x = lz_mul(x, load_fr(pre, idx));  // [0, 2r): the tile is lazy
             lds_put(lds_lo, lds_hi, e, x);
         } else {
             const uint4 *p = reinterpret_cast<const uint4 *>(data + 4 * idx);
@@ -747,6 +750,9 @@ static void ntt_core(NttTables &t, uint64_t *d, uint32_t lg, bool inverse, bool 
         break;
                 PNP_CASE4(2) PNP_CASE4(3) PNP_CASE4(4) PNP_CASE4(5) PNP_CASE4(6)
                 PNP_CASE4(7) PNP_CASE4(8) PNP_CASE4(9) PNP_CASE4(10)
+#if PNP_NTT_LGTILE >= 11
+                PNP_CASE4(11)
+#endif
 #undef PNP_CASE4
                 default:
                     set_error("bad NTT pass size %d", k);
