@@ -49,8 +49,10 @@ class WindowExchange:
         out = self.buf[: w * self.world]
         mine = out[self.rank * w:(self.rank + 1) * w]
         if self.buf.is_cuda and self.backend == "nccl":
-            # RCCL in-place all-gather (input is this rank's chunk of the output)
-            dist.all_gather_into_tensor(out, mine, group=self.group)
+            # RCCL all-gather; the input is a copy of this rank's slot (B x 192 B)
+            # rather than a view into the output, so no overlap rule of the
+            # torch / RCCL versions at hand can reject it
+            dist.all_gather_into_tensor(out, mine.clone(), group=self.group)
             torch.cuda.current_stream().synchronize()
         else:
             host_mine = mine.cpu().clone()
