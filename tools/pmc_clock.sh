@@ -5,7 +5,7 @@
 set -o pipefail
 R=$(pwd)
 TAG=${1:-pmc_clock}
-RX='k_accumulate29|k_ntt_pass|k_quotient|k_tree_leafw29|k_merge_pieces29|k_fine_sort|k_coarse_scatter'
+RX='k_accumulate29|k_ntt_pass|k_quotient|k_tree_leafw29|k_merge_tails29|k_fine_sort|k_coarse_scatter'
 cd /tmp && export TMPDIR=/tmp
 mkdir -p $R/gpurun_out/$TAG
 timeout -s KILL 150 rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_BUSY_CYCLES SQ_WAVES SQ_INSTS_VALU --kernel-include-regex "$RX" -f csv \

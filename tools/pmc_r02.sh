@@ -4,7 +4,7 @@
 set -o pipefail
 R=$(pwd)
 TAG=${1:-pmc}
-RX='k_accumulate29|k_ntt_pass|k_quotient|k_tree_leafw29|k_merge_pieces29'
+RX='k_accumulate29|k_ntt_pass|k_quotient|k_tree_leafw29|k_merge_tails29'
 cd /tmp && export TMPDIR=/tmp
 mkdir -p $R/gpurun_out/$TAG
 i=0
