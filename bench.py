@@ -57,7 +57,7 @@ class Synthetic:
         import torch
         from pnp import abi
         n, N8 = 1 << lg_n, 8 << lg_n
-        self.n, self.lg_n = n, lg_n
+        self.n, self.lg_n, self.seed = n, lg_n, seed
         dev = "cuda"
         keep = self.keep = {}
 
@@ -200,42 +200,136 @@ def pmc_traffic():
         return None
 
 
-CPU_SCALING_FILE = os.path.join(REPO, "profiles", "r02_cpu_scaling.json")
+CPU_SCALING_FILE = os.path.join(REPO, "profiles", "r03_cpu_scaling_box.json")
 
 
-def cpu_exponent():
-    """Fitted exponent b of t = a n^b for the CPU restatement's gen_proof
-    (tools/cpu_scaling.py over 2^15 .. 2^22, profiles/r02_cpu_scaling.json)."""
+def cpu_scaling():
+    """The CPU restatement's gen_proof on the Merkle circuit measured on a GPU
+    box's host (tools/cpu_scaling.py --circuit merkle on the box: 2^16 .. 2^20
+    and the full 2^22 instance): the fitted exponent b of t = a n^b and the
+    measured 2^22 time, or None."""
     try:
         with open(CPU_SCALING_FILE) as f:
-            return float(json.load(f)["fit"]["exponent"])
-    except (OSError, ValueError, KeyError):
+            return json.load(f)
+    except (OSError, ValueError):
         return None
 
 
-def cpu_baseline(lg: int, seconds_budget: float):
-    """Time the CPU restatement (oracle/, test infrastructure) on one bounded
-    gen_proof sample of the bench's own instance shape (tests/synth_cpu.py =
-    bench.Synthetic on the CPU); rank 0 only."""
+def host_copy(syn):
+    """(CircuitC, ProverKeyC, CommitKeyC) over host copies of bench.Synthetic's
+    device arrays, as the Rust caller hands them over (prover.rs:727-901), +
+    the numpy arrays that keep them alive."""
+    import numpy as np
+    from pnp import abi
+    host = {}
+
+    def hp(p):
+        addr = C.cast(p, C.c_void_p).value
+        if addr not in host:
+            for t in syn.keep.values():
+                if t.data_ptr() == addr:
+                    host[addr] = np.ascontiguousarray(t.cpu().numpy())
+                    break
+        return abi.ptr(host[addr].ctypes.data)
+
+    cs = syn.cs
+    cs_h = abi.CircuitC(n=cs.n, lookup_len=cs.lookup_len, intended_pi_pos=cs.intended_pi_pos,
+                        q_lookup=hp(cs.q_lookup), pi=cs.pi, w_l=hp(cs.w_l), w_r=hp(cs.w_r),
+                        w_o=hp(cs.w_o), w_4=hp(cs.w_4))
+    pk_h = abi.ProverKeyC()
+    for f in abi.PK_FIELDS:
+        setattr(pk_h, f, hp(getattr(syn.pk, f)))
+    ck_h = abi.CommitKeyC(powers_of_g=hp(syn.ck.powers_of_g), powers_of_gamma_g=hp(syn.ck.powers_of_gamma_g))
+    return cs_h, pk_h, ck_h, host
+
+
+def cpu_baseline(ctx, lg: int, circuit: str):
+    """Time the CPU restatement (oracle/, test infrastructure; OpenMP on all
+    host threads) on one bounded gen_proof of the bench's own circuit at
+    n = 2^lg: the instance is bench.Synthetic's (generated on the GPU, copied to
+    host memory, generation not timed); its proof must equal the GPU's.  Rank 0
+    at N = 1 only, after the timed region."""
     sys.path.insert(0, os.path.join(REPO, "tests"))
+    import torch
+    from pnp import abi
     from pnp_testlib import oracle
-    from synth_cpu import SyntheticCPU
     lib = oracle()
-    gates = int(HEIGHT15_GATES / (1 << 22) * (1 << lg))
-    syn = SyntheticCPU(lg, gates, seed=1)
+    syn = Synthetic(ctx, lg, int(HEIGHT15_GATES / (1 << 22) * (1 << lg)), seed=1, circuit=circuit)
+    cs_h, pk_h, ck_h, keep = host_copy(syn)
+    gpu = prove_resident(ctx, syn)
+    out = abi.ProofC()
     t0 = time.perf_counter()
-    syn.oracle_proof()
+    rc = lib.or_gen_proof(C.byref(cs_h), C.byref(pk_h), C.byref(ck_h), C.byref(out))
     dt = time.perf_counter() - t0
-    b = cpu_exponent()
-    out = {"value": round(dt, 3), "unit": f"s per gen_proof at n=2^{lg}",
+    del keep, syn
+    torch.cuda.empty_cache()
+    res = {"value": round(dt, 3), "unit": f"s per gen_proof at n=2^{lg}",
            "cores": int(lib.or_num_threads()), "kind": "port",
-           "sample": f"one gen_proof at n=2^{lg} ({gates} gates, bench.Synthetic's --circuit arith "
-                     f"instance: same gate count per domain, selector density and PI handling cost as "
-                     f"the Merkle circuit) with the C restatement (oracle/, OpenMP), instance generation "
-                     f"excluded"}
-    if b is not None:
-        out["extrapolated_full_s"] = round(dt * (2.0 ** ((22 - lg) * b)), 1)
-        out["extrapolation"] = f"t ~ n^{b:.3f} fitted over measured 2^15..2^22 (profiles/r02_cpu_scaling.json)"
+           "sample": (f"one gen_proof of the bench's {circuit} circuit at n=2^{lg}"
+                      + (f" (HEIGHT={lg - 7} Poseidon Merkle tree)" if circuit == "merkle" else "")
+                      + " with the C restatement (oracle/, OpenMP); instance generated on the GPU and "
+                        "copied to host memory (not timed)"),
+           "equals_gpu_proof": rc == 0 and abi.proof_to_bytes(out) == abi.proof_to_bytes(gpu)}
+    sc = cpu_scaling()
+    if sc and sc.get("circuit") == circuit:
+        b = float(sc["fit"]["exponent"])
+        res["extrapolated_full_s"] = round(dt * (2.0 ** ((22 - lg) * b)), 1)
+        res["extrapolation"] = (f"t ~ n^{b:.3f} fitted on the box's host over "
+                                f"{[p['lg'] for p in sc['points']]} ({os.path.relpath(CPU_SCALING_FILE, REPO)})")
+        full = [p for p in sc["points"] if p["lg"] == 22]
+        if full:
+            res["measured_full_s"] = full[0]["seconds"]
+            res["measured_full_cores"] = sc.get("threads")
+    return res
+
+
+def prove_resident(ctx, syn):
+    ctx.load_prover_key(syn.pk, syn.n, device_ptrs=True)
+    ctx.load_commit_key(syn.ck, syn.n, device_ptrs=True)
+    return ctx.prove(syn.cs, device_ptrs=True)
+
+
+def check_proof(syn, proof, circuit: str):
+    """Verify the last timed proof, as the reference harness verifies every
+    proof it times (benches/pnp_bench.rs:121-136): the restated verifier
+    (oracle/verifier.c, Proof::verify, proof.rs:123-431) with the verifier key
+    of the bench's prover key built from the SRS trapdoor ([p(tau)] G), the
+    KZG checks decided by the trapdoor and, where oracle/_ref holds the
+    reference's blst, by its pairing; and, for the seed-1 instances, the
+    bytes against the committed golden ProofC.  Checker only, after the timed
+    region."""
+    import numpy as np
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    from pnp import abi
+    from pnp_testlib import VK_POLYS, verifier_key_tau, verify, kzg_points, fr_unmont, from_limbs
+    t0 = time.perf_counter()
+    h = lambda t: np.ascontiguousarray(t.cpu().numpy()).view(np.uint64)
+    coeffs = {p: h(syn.keep[p + "_coeffs"]) for p in VK_POLYS if p + "_coeffs" in syn.keep}
+    tau = h(syn.keep["tau"])[0]
+    vk = verifier_key_tau(coeffs, syn.n, h(syn.keep["srs"])[0], tau)
+    pis = [(syn.cs.intended_pi_pos, sum(int(v) << (64 * k) for k, v in enumerate(syn.pi)))]
+    out = {"trapdoor": bool(verify(vk, proof, pis, tau))}
+    try:
+        from test_verifier import _blst, pairing_ok
+        blst = _blst()
+        if blst is not None:
+            rc, pts = kzg_points(vk, proof, pis)
+            t = fr_unmont(from_limbs(tau))
+            out["blst_pairing"] = bool(rc == 0 and pairing_ok(blst, pts[0], pts[1], t)
+                                       and pairing_ok(blst, pts[2], pts[3], t))
+    except Exception as e:  # the pairing is a second opinion; the trapdoor decides
+        out["blst_pairing_error"] = str(e)
+    gname = (f"merkle_h{syn.lg_n - 7}_seed{syn.seed}.json" if circuit == "merkle"
+             else f"full_2e{syn.lg_n}_seed{syn.seed}.json")
+    gpath = os.path.join(REPO, "tests", "golden", gname)
+    if os.path.exists(gpath):
+        with open(gpath) as f:
+            g = json.load(f)
+        if g["gates"] == syn.gates:
+            out["golden"] = gname
+            out["equals_golden"] = abi.proof_to_bytes(proof).hex() == g["proof_hex"]
+    out["verified"] = out["trapdoor"] and out.get("blst_pairing", True) and out.get("equals_golden", True)
+    out["seconds"] = round(time.perf_counter() - t0, 2)
     return out
 
 
@@ -244,29 +338,14 @@ def drop_in(ctx, syn, steps: int, v1: bool):
     headline: (a) v2 pnp_prove with the witness in HOST memory (CircuitC as
     prove_pnp builds it, prover.rs:727-762: ~4 x 3.16 M x 32 B over PCIe,
     inside the timed call); (b) the v1 symbol gen_proof with every key in host
-    memory: its first call copies the keys and builds the folded table, later
-    calls reuse them (key fingerprint, csrc/abi.cpp) and pay only the witness
-    upload.  Not `value`: the headline has inputs already in HBM."""
-    import numpy as np
+    memory, by default uploading both keys on every call as the reference does
+    (load.cu:311-358; the folded SRS table is kept when the uploaded SRS is
+    unchanged), and with PNP_V1_REUSE=1 (resident keys reused by fingerprint:
+    only the witness is uploaded).  Not `value`: the headline has inputs
+    already in HBM."""
     import torch
     from pnp import abi
-    host = {}
-
-    def h(addr):
-        if addr not in host:
-            for t in syn.keep.values():
-                if t.data_ptr() == addr:
-                    host[addr] = np.ascontiguousarray(t.cpu().numpy())
-                    break
-        return host[addr]
-
-    def hp(p):
-        return abi.ptr(h(C.cast(p, C.c_void_p).value).ctypes.data)
-
-    cs = syn.cs
-    cs_h = abi.CircuitC(n=cs.n, lookup_len=cs.lookup_len, intended_pi_pos=cs.intended_pi_pos,
-                        q_lookup=hp(cs.q_lookup), pi=cs.pi, w_l=hp(cs.w_l), w_r=hp(cs.w_r),
-                        w_o=hp(cs.w_o), w_4=hp(cs.w_4))
+    cs_h, pk_h, ck_h, keep = host_copy(syn)
     out = {}
     ctx.prove(cs_h, device_ptrs=False)
     ctx.sync()
@@ -277,22 +356,24 @@ def drop_in(ctx, syn, steps: int, v1: bool):
     out["v2_host_witness_s"] = round((time.perf_counter() - t0) / steps, 4)
     out["v2_host_witness_inputs_ms"] = round(dict(ctx.stage_times()).get("inputs", 0.0), 2)
     if v1:
-        pk_h = abi.ProverKeyC()
-        for f in abi.PK_FIELDS:
-            setattr(pk_h, f, hp(getattr(syn.pk, f)))
-        ck_h = abi.CommitKeyC(powers_of_g=hp(syn.ck.powers_of_g),
-                              powers_of_gamma_g=hp(syn.ck.powers_of_gamma_g))
         lib = ctx.lib
-        t0 = time.perf_counter()
-        first = lib.gen_proof(cs_h, pk_h, ck_h)
-        out["v1_first_call_s"] = round(time.perf_counter() - t0, 3)
-        t0 = time.perf_counter()
-        for _ in range(steps):
+        ref = abi.proof_to_bytes(ctx.prove(syn.cs, device_ptrs=True))
+        same = True
+        for mode in ("reload", "reuse"):
+            if mode == "reuse":
+                os.environ["PNP_V1_REUSE"] = "1"
+            t0 = time.perf_counter()
             p = lib.gen_proof(cs_h, pk_h, ck_h)
-        out["v1_gen_proof_s"] = round((time.perf_counter() - t0) / steps, 4)
-        ref = ctx.prove(syn.cs, device_ptrs=True)
-        out["v1_equals_v2"] = (abi.proof_to_bytes(p) == abi.proof_to_bytes(ref) ==
-                               abi.proof_to_bytes(first))
+            out[f"v1_{mode}_first_call_s"] = round(time.perf_counter() - t0, 3)
+            same &= abi.proof_to_bytes(p) == ref
+            t0 = time.perf_counter()
+            for _ in range(steps):
+                p = lib.gen_proof(cs_h, pk_h, ck_h)
+            out[f"v1_{mode}_gen_proof_s"] = round((time.perf_counter() - t0) / steps, 4)
+            same &= abi.proof_to_bytes(p) == ref
+        os.environ.pop("PNP_V1_REUSE", None)
+        out["v1_equals_v2"] = same
+    del keep
     torch.cuda.synchronize()
     return out
 
@@ -326,7 +407,11 @@ def main():
     ap.add_argument("--circuit", default="merkle", choices=("merkle", "arith"),
                     help="merkle: the reference's Poseidon Merkle circuit (HEIGHT = lg - 7); "
                          "arith: a random satisfying arithmetic circuit of --gates gates")
-    ap.add_argument("--cpu-lg", type=int, default=17, help="CPU baseline sample size; 0 = skip")
+    ap.add_argument("--cpu-lg", type=int, default=18, help="CPU baseline sample size; 0 = skip")
+    ap.add_argument("--no-verify", action="store_true", help="skip the proof check after the timed region")
+    ap.add_argument("--solo", default="", metavar="R/W",
+                    help="time rank R's share of a W-GPU proof alone on this GPU (loopback exchanges, "
+                         "proof discarded): the per-rank critical path of the multi-GPU bench")
     ap.add_argument("--stages", action="store_true", help="print per-stage ms to stderr")
     ap.add_argument("--drop-in", default="v1", choices=("", "v2", "v1"),
                     help="also time the host-witness v2 call ('v2') and the v1 symbol ('v1')")
@@ -359,10 +444,17 @@ def main():
     ctx = pnp.Context(local)
     gates = min(args.gates, 1 << args.lg)
     t0 = time.perf_counter()
+    solo = None
     if world > 1:  # sharded MSMs + distributed round 4, exchanges over RCCL
         from pnp.shard import WindowExchange, a2a_bytes_for
         ctx.set_msm_shard(WindowExchange(rank, world, device=torch.device("cuda", local),
                                          a2a_bytes=a2a_bytes_for(args.lg, world)))
+    elif args.solo:
+        from pnp.shard import SoloExchange, a2a_bytes_for
+        sr, sw = (int(v) for v in args.solo.split("/"))
+        solo = SoloExchange(sr, sw, device=torch.device("cuda", local), a2a_bytes=a2a_bytes_for(args.lg, sw))
+        ctx.set_msm_shard(solo)
+        args.no_verify, args.drop_in, args.cpu_lg = True, "", 0
     syn = Synthetic(ctx, args.lg, gates, seed=1, circuit=args.circuit)  # same instance on every rank
     gates = syn.gates
     ctx.load_prover_key(syn.pk, syn.n, device_ptrs=True)
@@ -381,7 +473,7 @@ def main():
     ctx.sync()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        ctx.prove(syn.cs, device_ptrs=True)
+        proof = ctx.prove(syn.cs, device_ptrs=True)
     ctx.sync()
     torch.cuda.synchronize()
     barrier()
@@ -436,7 +528,9 @@ def main():
                                    f"quotient on 2^{args.lg + 3} coset, pk+SRS+witness HBM-resident",
                        "circuit": args.circuit, "domain_log2": args.lg, "gates": gates,
                        "parallelism": (f"msm-point-range-shard + round4-block-shard x{world}"
-                                       if world > 1 else "single")},
+                                       if world > 1 else
+                                       f"solo rank {solo.rank} of {solo.world} (loopback exchanges, "
+                                       f"proof discarded)" if solo else "single")},
             "roofline": {"bound": "valu", "kernel": "k_accumulate29 (MSM bucket accumulation)",
                          "achieved": round(fq_achieved / 1e9, 2), "peak": round(fq_peak / 1e9, 2),
                          "unit": "G Fq-mul/s", "frac": round(fq_achieved / fq_peak, 4),
@@ -469,17 +563,36 @@ def main():
                                       "launch_ms": round(q_ms / max(q_n, 1), 3)}},
             "stages_ms": {k: round(v, 2) for k, v in stages},
         }
+        if solo:
+            out["solo"] = {"rank": solo.rank, "world": solo.world,
+                           "allgathers_per_proof": solo.calls / (args.steps + args.warmup),
+                           "alltoalls_per_proof": solo.a2a_calls / (args.steps + args.warmup),
+                           "allgather_bytes_per_proof": solo.gather_bytes / (args.steps + args.warmup),
+                           "alltoall_bytes_sent_per_proof": solo.a2a_bytes_moved / (args.steps + args.warmup),
+                           "note": "per-rank work of a W-GPU proof; the collectives are loopbacks "
+                                   "(their xGMI time is not included)"}
+        if not args.no_verify:
+            chk = check_proof(syn, proof, args.circuit)
+            out["verified"] = chk.pop("verified")
+            out["verification"] = chk
+            log(f"proof check: {out['verified']} {chk}")
         if args.drop_in and world == 1:
             out["drop_in"] = drop_in(ctx, syn, args.steps, v1=args.drop_in == "v1")
         if args.cpu_lg and world == 1:  # the CPU baseline: rank 0 at N = 1 only
+            del syn
+            import torch
+            torch.cuda.empty_cache()
             try:
-                out["cpu_baseline"] = cpu_baseline(args.cpu_lg, 30.0)
+                out["cpu_baseline"] = cpu_baseline(ctx, args.cpu_lg, args.circuit)
             except Exception as e:  # the CPU leg must never hide the GPU number
-                out["cpu_baseline"] = {"error": str(e)}
+                out["cpu_baseline"] = {"error": repr(e)}
         print(json.dumps(out), flush=True)
     ctx.close()
     if world > 1:
         dist.destroy_process_group()
+    if rank == 0 and out.get("verified") is False:
+        log("bench: the timed proof did NOT verify")
+        return 3
 
 
 if __name__ == "__main__":

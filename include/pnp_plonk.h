@@ -190,7 +190,21 @@ typedef struct {
 
 /* lib.rs:237-239 / hello.cu:4-6.  Structs by value, ProofC returned by value.
  * Synchronous, device 0.  On any device error it prints and exits, like the
- * reference's CUDA_CHECK (caffe/common.hpp:23-30). */
+ * reference's CUDA_CHECK (caffe/common.hpp:23-30).  Like the reference
+ * (load.cu:311-358) it uploads the prover key and commit key on every call,
+ * so a caller may rewrite its key buffers between calls; the folded MSM table
+ * of the SRS is kept when the uploaded SRS is byte-identical to the last one.
+ * Environment switches (read per call):
+ *   PNP_V1_REUSE=1   reuse the keys resident from an earlier call while their
+ *                    fingerprint (field pointers, domain, 257 sampled words
+ *                    per array) is unchanged: no upload.  Only for callers
+ *                    that never mutate key contents in place.
+ *   PNP_V1_STRICT=1  exit with PNP_E_ENVELOPE for keys outside the reference
+ *                    GPU path's circuit class (non-zero q_m / custom-gate /
+ *                    q_lookup selectors or lookup tables): there this backend
+ *                    returns the ZK-Garage prover's proof (combine_split,
+ *                    widgets, the true z2 shift), which differs byte for byte
+ *                    from the reference GPU path's. */
 ProofC gen_proof(CircuitC circuit, ProverKeyC pk, CommitKeyC ck);
 
 /* ------------------------------------------------------------------ */
@@ -201,8 +215,8 @@ ProofC gen_proof(CircuitC circuit, ProverKeyC pk, CommitKeyC ck);
 #define PNP_E_ARG          -1   /* bad argument / size                      */
 #define PNP_E_DEVICE       -2   /* HIP runtime error                        */
 #define PNP_E_NOKEY        -3   /* prover / commit key not loaded           */
-#define PNP_E_ENVELOPE     -4   /* input outside the supported circuit class (unused since
-                                       the general prover: kept for ABI stability) */
+#define PNP_E_ENVELOPE     -4   /* key outside the reference GPU path's circuit class
+                                       (v1 with PNP_V1_STRICT=1 only) */
 #define PNP_E_NOMEM        -5   /* device allocation failed                 */
 
 typedef struct pnp_ctx pnp_ctx;
@@ -222,6 +236,35 @@ int pnp_load_prover_key(pnp_ctx *ctx, const ProverKeyC *pk, uint64_t domain_size
                         int device_ptrs);
 int pnp_load_commit_key(pnp_ctx *ctx, const CommitKeyC *ck, uint64_t n_points,
                         int device_ptrs);
+
+/* The commit key straight from arkworks' memory, without the per-proof
+ * conversion prove_pnp does today (prover.rs:700-711 rebuilds (x, y) tuples
+ * of all 2^24+1 SRS points on every call): `points` = the address of
+ * commit_key.powers_of_g (Vec<ark_bls12_381::G1Affine>, ark-ec 0.3
+ * GroupAffine: x, y Fp384 = 6 u64 Montgomery limbs each (R = 2^384), an
+ * `infinity` bool, padding).  The Rust struct's field order is not fixed by
+ * the language, so the caller passes the layout it was compiled with:
+ * stride = size_of::<G1Affine>() (104 on x86-64), x_off / y_off / inf_off =
+ * offset_of!(G1Affine, x / y / infinity).  Only the first n_points points are
+ * read (n_points >= the domain size).  A point flagged infinity is refused
+ * (PNP_E_ARG: an SRS [tau^i] G never holds it).  device_ptrs: `points` is
+ * an HBM address.  Otherwise as pnp_load_commit_key (an unchanged SRS keeps
+ * its folded table). */
+typedef struct {
+    uint64_t stride, x_off, y_off, inf_off;
+} pnp_affine_layout;
+int pnp_load_commit_key_strided(pnp_ctx *ctx, const void *points, uint64_t n_points,
+                                const pnp_affine_layout *layout, int device_ptrs);
+
+/* Which of the 19 commitments of a ProofC (v1 or v2) are the point at
+ * infinity: bit k = the k-th CommitmentC of ProofC in declaration order
+ * (a_comm 0, b 1, c 2, d 3, z 4, f 5, h_1 6, h_2 7, z_2 8, t_1 .. t_8
+ * 9 .. 16, aw_opening 17, saw_opening 18).  Infinity is encoded (x = 0, y = Fq one in Montgomery
+ * form), which no curve point has (x = 0 gives y = +-2).  Replaces the
+ * hard-coded flags of merkle-tree/src/main.rs:112-123 (f, h1, h2, t7, t8 =
+ * true), wrong for any circuit with lookups or a quotient of degree >= 6n. */
+#define PNP_PROOF_COMMITMENTS 19
+uint32_t pnp_proof_infinity_mask(const ProofC *p);
 
 /* Prove with the resident keys.  `device_ptrs`: the CircuitC witness pointers
  * (q_lookup, w_*) are HBM pointers; pi is always a host pointer. */

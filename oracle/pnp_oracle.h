@@ -111,6 +111,9 @@ typedef struct {
 void or_vk_slots(or_verifier_key *vk, uint64_t (*dst[OR_VK_POLYS])[12]);
 void or_verifier_key_from_coeffs(or_verifier_key *vk, uint64_t n, const uint64_t *srs,
                                  const uint64_t *const coeffs[OR_VK_POLYS]);
+/* the same key from the trapdoor: commit(p) = [p(tau)] G (g_aff = SRS_0) */
+void or_verifier_key_tau(or_verifier_key *vk, uint64_t n, const uint64_t g_aff[12],
+                         const uint64_t *const coeffs[OR_VK_POLYS], const uint64_t tau_mont[4]);
 /* the two KZG openings reduced to G1: out = {L_aw, W_aw, L_saw, W_saw} with
  * L = sum ch^i C_i - (sum ch^i v_i) G + x W; accept iff e(L, H) = e(W, [tau]H) */
 int or_verify_kzg_points(const or_verifier_key *vk, const ProofC *p, const char *label,
@@ -126,6 +129,11 @@ void or_synth_random_fr(uint64_t *d, uint64_t n, uint64_t seed);
 void or_synth_circuit(uint64_t *const w[4], uint64_t *const sel[9], uint64_t *const sigma[4],
                       uint64_t n, uint64_t ng, uint64_t pi_pos, const uint64_t pi_canon[4]);
 void or_synth_coset_consts(uint64_t *vh, uint64_t *x, uint32_t lg);
+/* pnp_synth_merkle: the reference's Poseidon Merkle circuit of `height`;
+ * pc_mont = 199 Montgomery constants (rk[189], MDS row-major, tag) */
+int or_synth_merkle(uint32_t height, const uint64_t *pc_mont, const uint64_t *leaves, const uint64_t *blind,
+                    uint64_t *nodes, uint64_t *const w[4], uint64_t *const sel[9], uint64_t *const sigma[4],
+                    uint64_t n, uint64_t root_canon[4]);
 
 /* threads used by the OpenMP loops (for cpu_baseline.cores) */
 int or_num_threads(void);

@@ -457,6 +457,32 @@ void or_verifier_key_from_coeffs(or_verifier_key *vk, uint64_t n, const uint64_t
     }
 }
 
+/* The same verifier key from the SRS trapdoor: SRS_i = [tau^i] G, so
+ * commit(p) = sum_i p_i [tau^i] G = [p(tau)] G — one Horner evaluation and one
+ * scalar multiplication per polynomial instead of an n-point MSM (a checker
+ * for instances whose tau is known, e.g. bench.py's). */
+void or_verifier_key_tau(or_verifier_key *vk, uint64_t n, const uint64_t g_aff[12],
+                         const uint64_t *const coeffs[OR_VK_POLYS], const uint64_t tau_mont[4]) {
+    vk->n = n;
+    memcpy(vk->g, g_aff, 96);
+    uint64_t(*dst[OR_VK_POLYS])[12];
+    or_vk_slots(vk, dst);
+#pragma omp parallel for schedule(dynamic, 1)
+    for (int k = 0; k < OR_VK_POLYS; k++) {
+        if (!coeffs[k]) {
+            memset(dst[k][0], 0, 48);
+            fq_copy(dst[k][0] + 6, OR_FQ_ONE);
+            continue;
+        }
+        uint64_t acc[4] = {0, 0, 0, 0};
+        for (uint64_t i = n; i-- > 0;) {
+            or_fr_mul(acc, acc, tau_mont);
+            or_fr_add(acc, acc, coeffs[k] + 4 * i);
+        }
+        or_commit(g_aff, acc, 1, dst[k][0]);
+    }
+}
+
 void or_vk_slots(or_verifier_key *vk, uint64_t (*dst[OR_VK_POLYS])[12]) {
     uint64_t(*s[OR_VK_POLYS])[12] = {
         &vk->q_m, &vk->q_l, &vk->q_r, &vk->q_o, &vk->q_4, &vk->q_c, &vk->q_hl, &vk->q_hr, &vk->q_h4,

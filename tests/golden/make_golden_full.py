@@ -34,11 +34,13 @@ def main():
     ap.add_argument("--lg", type=int, default=22)
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--out", default=None)
+    ap.add_argument("--circuit", default="arith", choices=("arith", "merkle"))
     args = ap.parse_args()
     gates = int(HEIGHT15_GATES / (1 << 22) * (1 << args.lg)) if args.lg != 22 else HEIGHT15_GATES
     lib = oracle()
     t0 = time.perf_counter()
-    syn = SyntheticCPU(args.lg, gates, args.seed)
+    syn = SyntheticCPU(args.lg, gates, args.seed, circuit=args.circuit)
+    gates = syn.gates
     t1 = time.perf_counter()
     print(f"instance 2^{args.lg} ({gates} gates): {t1 - t0:.1f} s", flush=True)
     proof = syn.oracle_proof()
@@ -59,8 +61,8 @@ def main():
         print(f"blst pairing verify: {pairing}", flush=True)
         assert pairing
     out = {
-        "what": "oracle (CPU restatement) proof of bench.Synthetic(lg, gates, seed)",
-        "lg": args.lg, "gates": gates, "seed": args.seed,
+        "what": f"oracle (CPU restatement) proof of bench.Synthetic(lg, gates, seed, circuit={args.circuit!r})",
+        "circuit": args.circuit, "lg": args.lg, "gates": gates, "seed": args.seed,
         "pi_pos": syn.pi_pos, "pi": syn.pi_canon,
         "tau_mont": [int(v) for v in syn.tau_mont[0]],
         "proof_hex": abi.proof_to_bytes(proof).hex(),
@@ -69,7 +71,12 @@ def main():
         "cpu_seconds": {"instance": round(t1 - t0, 1), "gen_proof": round(t2 - t1, 1),
                         "threads": int(lib.or_num_threads()), "host": "build container"},
     }
-    path = args.out or os.path.join(HERE, f"full_2e{args.lg}_seed{args.seed}.json")
+    if args.circuit == "merkle":
+        out["height"] = syn.height
+        out["root"] = hex(syn.root)
+    name = (f"merkle_h{args.lg - 7}_seed{args.seed}.json" if args.circuit == "merkle"
+            else f"full_2e{args.lg}_seed{args.seed}.json")
+    path = args.out or os.path.join(HERE, name)
     with open(path, "w") as f:
         json.dump(out, f, indent=1)
     print("wrote", path)

@@ -348,6 +348,26 @@ def verifier_key(coeffs: dict, n: int, srs: np.ndarray) -> np.ndarray:
     return vk
 
 
+def verifier_key_tau(coeffs: dict, n: int, g_aff: np.ndarray, tau_mont) -> np.ndarray:
+    """verifier_key from the SRS trapdoor: commit(p) = [p(tau)] G, one Horner
+    evaluation + one scalar multiplication per polynomial (oracle
+    or_verifier_key_tau); equal to verifier_key when srs_i = [tau^i] G."""
+    lib = oracle()
+    _sig_verifier(lib)
+    if not getattr(lib, "_vk_tau_sig", False):
+        lib.or_verifier_key_tau.argtypes = [C.c_void_p, C.c_uint64, C.c_void_p,
+                                            C.c_void_p * len(VK_POLYS), C.c_void_p]
+        lib._vk_tau_sig = True
+    vk = np.zeros(VK_WORDS, dtype=np.uint64)
+    keep = [np.ascontiguousarray(coeffs[k]) if k in coeffs else None for k in VK_POLYS]
+    ptrs = (C.c_void_p * len(VK_POLYS))(*[C.c_void_p(a.ctypes.data) if a is not None else None
+                                          for a in keep])
+    g = np.ascontiguousarray(np.asarray(g_aff, dtype=np.uint64).reshape(12))
+    tau = np.ascontiguousarray(np.asarray(tau_mont, dtype=np.uint64).reshape(4))
+    lib.or_verifier_key_tau(vp(vk), n, vp(g), ptrs, vp(tau))
+    return vk
+
+
 def _pi_args(pis):
     pos = np.array([p for p, _ in pis], dtype=np.uint64)
     vals = np.array([to_limbs(v, 4) for _, v in pis], dtype=np.uint64).reshape(-1, 4)

@@ -27,17 +27,29 @@ def _lib():
         lib.or_synth_circuit.argtypes = [C.c_void_p * 4, C.c_void_p * 9, C.c_void_p * 4, C.c_uint64,
                                          C.c_uint64, C.c_uint64, v]
         lib.or_synth_coset_consts.argtypes = [v, v, C.c_uint32]
+        lib.or_synth_merkle.argtypes = [C.c_uint32, v, v, v, v, C.c_void_p * 4, C.c_void_p * 9,
+                                        C.c_void_p * 4, C.c_uint64, v]
+        lib.or_synth_merkle.restype = C.c_int
         lib._synth_sig = True
     return lib
 
 
-class SyntheticCPU:
-    """bench.Synthetic(ctx, lg, gates, seed) rebuilt on the CPU."""
+def merkle_gates(height: int) -> int:
+    return 193 * ((1 << (height - 1)) - 1) + 5
 
-    def __init__(self, lg_n: int, gates: int, seed: int, keep_evals: bool = True):
+
+class SyntheticCPU:
+    """bench.Synthetic(ctx, lg, gates, seed, circuit) rebuilt on the CPU.
+
+    circuit="merkle": the reference's Poseidon Merkle circuit of HEIGHT
+    lg - 7 (or_synth_merkle mirrors pnp_synth_merkle; `gates` is ignored),
+    random leaves / blinding values from the same seeds as bench.py, PI =
+    -root at the root row.  circuit="arith": the round-1 stand-in."""
+
+    def __init__(self, lg_n: int, gates: int, seed: int, keep_evals: bool = True, circuit: str = "arith"):
         lib = _lib()
         n, N8 = 1 << lg_n, 8 << lg_n
-        self.n, self.lg_n, self.gates, self.seed = n, lg_n, gates, seed
+        self.n, self.lg_n, self.seed, self.circuit_kind = n, lg_n, seed, circuit
         a = self.arrays = {}
         s = seed * 1000
 
@@ -46,21 +58,48 @@ class SyntheticCPU:
             lib.or_synth_random_fr(vp(x), cnt, sd)
             return x
 
-        a["w_l"] = rnd(gates, s + 1)
-        a["w_4"] = rnd(gates, s + 4)
-        a["w_r"] = np.zeros((gates, 4), dtype=np.uint64)
-        a["w_o"] = np.zeros((gates, 4), dtype=np.uint64)
+        nev = {p: np.zeros((n, 4), dtype=np.uint64) for p in POLYS}
+        if circuit == "merkle":
+            from poseidon import PoseidonConstants, flat_constants
+            from pnp_testlib import fr_mont, ints_to_arr, R_MOD
+            height = self.height = lg_n - 7
+            gates = merkle_gates(height)
+            for k in ("w_l", "w_r", "w_o", "w_4"):
+                a[k] = np.zeros((gates, 4), dtype=np.uint64)
+            leaves, blind = rnd(1 << (height - 1), s + 1), rnd(8, s + 2)
+            self.nodes = np.zeros(((1 << (height - 1)) - 1, 4), dtype=np.uint64)
+            pc = ints_to_arr([fr_mont(v) for v in flat_constants(PoseidonConstants())])
+            W = (C.c_void_p * 4)(*[a[k].ctypes.data for k in ("w_l", "w_r", "w_o", "w_4")])
+            S = (C.c_void_p * 9)(*[nev[k].ctypes.data for k in SEL_IN + ("q_arith",)])
+            G = (C.c_void_p * 4)(*[nev[k].ctypes.data for k in ("left_sigma", "right_sigma", "out_sigma",
+                                                                 "fourth_sigma")])
+            root = np.zeros(4, dtype=np.uint64)
+            rc = lib.or_synth_merkle(height, vp(pc), vp(leaves), vp(blind), vp(self.nodes), W, S, G, n,
+                                     vp(root))
+            assert rc == 0, rc
+            self.root = sum(int(root[k]) << (64 * k) for k in range(4))
+            neg = (-self.root) % R_MOD
+            self.pi_canon = [(neg >> (64 * k)) & (2**64 - 1) for k in range(4)]
+            self.pi_pos = gates - 1
+        else:
+            a["w_l"] = rnd(gates, s + 1)
+            a["w_4"] = rnd(gates, s + 4)
+            a["w_r"] = np.zeros((gates, 4), dtype=np.uint64)
+            a["w_o"] = np.zeros((gates, 4), dtype=np.uint64)
+            self.pi_canon = [123456789 + seed, 0, 0, 0]
+            self.pi_pos = PI_POS
+            for i, p in enumerate(SEL_IN):
+                nev[p] = rnd(n, s + 100 + i)
+            W = (C.c_void_p * 4)(*[a[k].ctypes.data for k in ("w_l", "w_r", "w_o", "w_4")])
+            S = (C.c_void_p * 9)(*[nev[k].ctypes.data for k in SEL_IN + ("q_arith",)])
+            G = (C.c_void_p * 4)(*[nev[k].ctypes.data for k in ("left_sigma", "right_sigma", "out_sigma",
+                                                                 "fourth_sigma")])
+            pi = np.array(self.pi_canon, dtype=np.uint64)
+            lib.or_synth_circuit(W, S, G, n, gates, PI_POS, vp(pi))
+        self.gates = gates
         a["q_lookup"] = np.zeros((gates, 4), dtype=np.uint64)
-        self.pi_canon = [123456789 + seed, 0, 0, 0]
         a["pi"] = np.array(self.pi_canon, dtype=np.uint64)
-        nev = {p: rnd(n, s + 100 + i) for i, p in enumerate(SEL_IN)}
-        for p in ("q_arith", "left_sigma", "right_sigma", "out_sigma", "fourth_sigma"):
-            nev[p] = np.zeros((n, 4), dtype=np.uint64)
-        W = (C.c_void_p * 4)(*[a[k].ctypes.data for k in ("w_l", "w_r", "w_o", "w_4")])
-        S = (C.c_void_p * 9)(*[nev[k].ctypes.data for k in SEL_IN + ("q_arith",)])
-        G = (C.c_void_p * 4)(*[nev[k].ctypes.data for k in ("left_sigma", "right_sigma", "out_sigma",
-                                                             "fourth_sigma")])
-        lib.or_synth_circuit(W, S, G, n, gates, PI_POS, vp(a["pi"]))
+        self.nevals = {p: nev[p].copy() for p in POLYS} if lg_n <= 16 else None
         for p in POLYS:
             c = nev.pop(p)
             lib.or_ntt(vp(c), lg_n, 1, 0)  # coefficients of the n-domain evaluations
@@ -80,12 +119,11 @@ class SyntheticCPU:
         a["srs"] = np.zeros((n, 12), dtype=np.uint64)
         lib.or_srs(vp(a["srs"]), n, vp(self.tau_mont))
         a["gamma_g"] = np.zeros((2, 12), dtype=np.uint64)
-        self.pi_pos = PI_POS
         self._structs(keep_evals)
 
     def _structs(self, keep_evals):
         a = self.arrays
-        self.circuit = abi.CircuitC(n=self.gates, lookup_len=0, intended_pi_pos=PI_POS,
+        self.circuit = abi.CircuitC(n=self.gates, lookup_len=0, intended_pi_pos=self.pi_pos,
                                     q_lookup=ptr_of(a["q_lookup"]), pi=ptr_of(a["pi"]),
                                     w_l=ptr_of(a["w_l"]), w_r=ptr_of(a["w_r"]), w_o=ptr_of(a["w_o"]),
                                     w_4=ptr_of(a["w_4"]))
@@ -116,4 +154,4 @@ class SyntheticCPU:
                             a["srs"])
 
     def pis(self):
-        return [(PI_POS, self.pi_canon[0])]
+        return [(self.pi_pos, sum(int(v) << (64 * k) for k, v in enumerate(self.pi_canon)))]

@@ -30,3 +30,35 @@ def test_struct_layouts():
     assert C.sizeof(abi.CircuitC) == 72
     off = abi.ProofC.evaluations.offset
     assert off == 19 * 96
+
+
+def test_proof_infinity_mask_host():
+    """pnp_proof_infinity_mask (host code, no GPU): (0, Fq one) is infinity,
+    (0, 2) is a finite curve point (y^2 = x^3 + 4), other points are finite;
+    the bit order is ProofC's commitment order."""
+    import pnp
+    from pnp import abi
+    from pnp_testlib import to_limbs, Q_MOD
+    one = to_limbs((1 << 384) % Q_MOD, 6)
+    two = to_limbs((2 << 384) % Q_MOD, 6)
+    p = abi.ProofC()
+    for k, name in enumerate(abi.PROOF_COMMITMENTS):
+        c = getattr(p, name)
+        c.x[0] = k + 1  # finite
+        c.y[:] = two
+    for name in ("f_comm", "h_1_comm", "h_2_comm", "t_7_comm", "t_8_comm"):
+        c = getattr(p, name)
+        c.x[:] = [0] * 6
+        c.y[:] = one
+    p.z_comm.x[:] = [0] * 6  # (0, 2): on the curve, not infinity
+    m = pnp.infinity_mask(p)
+    assert m == (1 << 5) | (1 << 6) | (1 << 7) | (1 << 15) | (1 << 16)
+    flags = pnp.infinity_flags(p)
+    assert [k for k, v in flags.items() if v] == ["f_comm", "h_1_comm", "h_2_comm", "t_7_comm", "t_8_comm"]
+
+
+def test_ark_g1_affine_layout_shape():
+    from pnp import abi
+    L = abi.ARK_G1_AFFINE
+    assert C.sizeof(abi.AffineLayout) == 32
+    assert (L.stride, L.x_off, L.y_off, L.inf_off) == (104, 0, 48, 96)

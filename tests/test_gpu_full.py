@@ -25,6 +25,7 @@ pytestmark = pytest.mark.gpu
 if REPO not in sys.path:
     sys.path.insert(0, REPO)
 GOLDEN = os.path.join(REPO, "tests", "golden", "full_2e22_seed1.json")
+GOLDEN_MERKLE = os.path.join(REPO, "tests", "golden", "merkle_h15_seed1.json")
 N22 = 1 << 22
 
 
@@ -125,21 +126,66 @@ def test_synthetic_gpu_equals_cpu_small():
         ctx.close()
 
 
-@pytest.mark.skipif(not os.path.exists(GOLDEN), reason="golden 2^22 proof not generated")
-def test_height15_proof_matches_golden():
+def test_synthetic_merkle_gpu_equals_cpu_small():
+    """bench.Synthetic(circuit="merkle") on the GPU (pnp_synth_merkle) and
+    SyntheticCPU(circuit="merkle") (or_synth_merkle) at HEIGHT 5 (2^12): the
+    same circuit, witness, root and key; proofs byte-identical, verified."""
     import pnp
     from pnp import abi
     from bench import Synthetic
-    with open(GOLDEN) as f:
-        g = json.load(f)
+    from synth_cpu import SyntheticCPU
+    lg, seed = 12, 6
+    cpu = SyntheticCPU(lg, 0, seed, circuit="merkle")
+    exp = cpu.oracle_proof()
     ctx = pnp.Context(0)
     try:
-        syn = Synthetic(ctx, g["lg"], g["gates"], seed=g["seed"])
+        syn = Synthetic(ctx, lg, 0, seed=seed, circuit="merkle")
+        assert (syn.gates, syn.height) == (cpu.gates, 5)
+        assert list(syn.pi) == [int(v) for v in cpu.pi_canon]
+        for w in ("w_l", "w_r", "w_o", "w_4"):
+            assert np.array_equal(syn.keep[w].cpu().numpy().view(np.uint64), cpu.arrays[w]), w
+        ctx.load_prover_key(syn.pk, syn.n, device_ptrs=True)
+        ctx.load_commit_key(syn.ck, syn.n, device_ptrs=True)
+        got = ctx.prove(syn.cs, device_ptrs=True)
+        assert abi.proof_to_bytes(got) == abi.proof_to_bytes(exp)
+        assert verify(cpu.vk(), got, cpu.pis(), cpu.tau_mont[0])
+    finally:
+        ctx.close()
+
+
+def _golden_case(path, circuit):
+    import pnp
+    from pnp import abi
+    from bench import Synthetic
+    with open(path) as f:
+        g = json.load(f)
+    assert g.get("circuit", "arith") == circuit
+    ctx = pnp.Context(0)
+    try:
+        syn = Synthetic(ctx, g["lg"], g["gates"], seed=g["seed"], circuit=circuit)
+        assert syn.gates == g["gates"]
         ctx.load_prover_key(syn.pk, syn.n, device_ptrs=True)
         ctx.load_commit_key(syn.ck, syn.n, device_ptrs=True)
         got = ctx.prove(syn.cs, device_ptrs=True)
         assert abi.proof_to_bytes(got).hex() == g["proof_hex"]
         vk = np.frombuffer(bytes.fromhex(g["vk_hex"]), dtype=np.uint64).copy()
-        assert verify(vk, got, [(g["pi_pos"], g["pi"][0])], np.array(g["tau_mont"], dtype=np.uint64))
+        pi = sum(int(v) << (64 * k) for k, v in enumerate(g["pi"]))
+        assert verify(vk, got, [(g["pi_pos"], pi)], np.array(g["tau_mont"], dtype=np.uint64))
     finally:
         ctx.close()
+
+
+@pytest.mark.skipif(not os.path.exists(GOLDEN), reason="golden 2^22 proof not generated")
+def test_height15_proof_matches_golden():
+    """The round-1 stand-in (random satisfying arithmetic circuit, 3,161,924 gates)."""
+    _golden_case(GOLDEN, "arith")
+
+
+@pytest.mark.skipif(not os.path.exists(GOLDEN_MERKLE), reason="golden HEIGHT=15 Merkle proof not generated")
+def test_height15_merkle_proof_matches_golden():
+    """The bench's default input: the reference's HEIGHT=15 Poseidon Merkle
+    circuit (pnp_synth_merkle, seed 1), byte-identical to the ProofC the CPU
+    restatement produced for the same instance (or_synth_merkle,
+    tests/golden/make_golden_full.py --circuit merkle) and accepted by the
+    restated verifier with the golden verifier key."""
+    _golden_case(GOLDEN_MERKLE, "merkle")

@@ -278,3 +278,67 @@ def test_msm_folded_equal_pieces_exact_fallback(c, monkeypatch):
         ctx.kernel_timing(False)
     finally:
         ctx.close()
+
+
+def test_commit_key_strided_ark_layout():
+    """pnp_load_commit_key_strided: the SRS handed over in arkworks' G1Affine
+    memory layout (104-byte stride, x / y / infinity, garbage padding) gives
+    the same commitments as the packed CommitKeyC, host and device pointers;
+    a point flagged infinity is refused."""
+    import numpy as np
+    import pnp
+    from pnp import abi
+    from gpu_util import to_dev, empty_dev
+    from pnp_testlib import oracle, vp
+    n = 1 << 12
+    tau = np.array([[123456789, 5, 0, 7]], dtype=np.uint64)
+    srs = np.zeros((n, 12), dtype=np.uint64)
+    oracle().or_srs(vp(srs), n, vp(tau))
+    rng = np.random.default_rng(5)
+    ark = rng.integers(0, 256, size=(n, 104), dtype=np.uint8)  # padding bytes are garbage
+    ark[:, 0:96] = srs.view(np.uint8).reshape(n, 96)
+    ark[:, 96] = 0
+    ctx = pnp.Context(0)
+    try:
+        sc = empty_dev(n)
+        ctx.random_fr(sc.data_ptr(), n, 77)
+        ctx.sync()
+        ctx.load_commit_key(abi.CommitKeyC(powers_of_g=abi.ptr(srs.ctypes.data),
+                                           powers_of_gamma_g=abi.ptr(srs.ctypes.data)), n, device_ptrs=False)
+        exp = ctx.commit_ck(sc.data_ptr(), n)
+        ctx.load_commit_key_strided(ark.ctypes.data, n)
+        got = ctx.commit_ck(sc.data_ptr(), n)
+        assert list(got.x) == list(exp.x) and list(got.y) == list(exp.y)
+        d = to_dev(ark.view(np.uint64).reshape(n, 13))
+        ctx.load_commit_key_strided(d.data_ptr(), n, device_ptrs=True)
+        got = ctx.commit_ck(sc.data_ptr(), n)
+        assert list(got.x) == list(exp.x) and list(got.y) == list(exp.y)
+        ark[77, 96] = 1
+        with pytest.raises(pnp.PnpError, match="infinity"):
+            ctx.load_commit_key_strided(ark.ctypes.data, n)
+        bad = abi.AffineLayout(stride=100, x_off=0, y_off=48, inf_off=96)
+        with pytest.raises(pnp.PnpError, match="PNP_E_ARG"):
+            ctx.load_commit_key_strided(ark.ctypes.data, n, layout=bad)
+    finally:
+        ctx.close()
+
+
+def test_proof_infinity_mask_of_gpu_proof():
+    """The mask of a GPU proof of a Merkle-class circuit: f, h1, h2, t7, t8 at
+    infinity (the flags merkle-tree/src/main.rs:112-123 hard-codes), nothing
+    else; with live lookups f / h1 / h2 are finite."""
+    import pnp
+    from pnp_testlib import Inputs
+    inp = Inputs(8, 2)
+    p = pnp.load().gen_proof(inp.circuit, inp.pk, inp.ck)
+    flags = pnp.infinity_flags(p)
+    assert sorted(k for k, v in flags.items() if v) == ["f_comm", "h_1_comm", "h_2_comm", "t_7_comm", "t_8_comm"]
+    inp2 = Inputs(8, 47, lookup_rows=17)
+    ctx = pnp.Context(0)
+    try:
+        ctx.load_prover_key(inp2.pk, inp2.n, device_ptrs=False)
+        ctx.load_commit_key(inp2.ck, inp2.n, device_ptrs=False)
+        flags = pnp.infinity_flags(ctx.prove(inp2.circuit, device_ptrs=False))
+        assert not flags["f_comm"] and not flags["h_1_comm"] and not flags["h_2_comm"]
+    finally:
+        ctx.close()

@@ -179,3 +179,88 @@ def test_full_size_height15_properties(circuit):
     assert list(p1.z_2_comm.x) == [int(v) for v in g0[:6]]
     assert list(p1.z_2_comm.y) == [int(v) for v in g0[6:]]
     ctx.close()
+
+
+def test_v1_reloads_mutated_key(monkeypatch):
+    """The v1 symbol keeps the reference's per-call key copy (load.cu:311-358):
+    a caller that rewrites its key buffers in place between two calls (same
+    pointers, a change in words the reuse fingerprint does not sample) gets a
+    proof over the NEW key, byte-identical to the oracle's; an unchanged SRS
+    keeps its folded table (device-side comparison) and the proof stays exact.
+    With PNP_V1_REUSE=1 (opt-in: the caller promises immutable keys) the
+    resident copy is reused and the second proof is the stale one."""
+    import pnp
+    monkeypatch.delenv("PNP_V1_REUSE", raising=False)
+    lib = pnp.load()
+    inp = Inputs(10, 44, n_gates=1000, pi_pos=17)
+    first = lib.gen_proof(inp.circuit, inp.pk, inp.ck)
+    assert abi.proof_to_bytes(first) == abi.proof_to_bytes(inp.oracle_proof())
+    # element 3 of q_c's 8n evaluations: words 12..15, between the sampled
+    # words 0 and (32n - 1) / 256 of the fingerprint
+    qc = inp.arrays["q_c_evals"]
+    assert (qc.size - 1) // 256 > 15
+    saved = qc[3].copy()
+    qc[3] = qc[5]
+    exp = inp.oracle_proof()
+    assert abi.proof_to_bytes(exp) != abi.proof_to_bytes(first)
+    second = lib.gen_proof(inp.circuit, inp.pk, inp.ck)
+    assert abi.proof_to_bytes(second) == abi.proof_to_bytes(exp)
+    # the opt-in reuse: a third call on a reverted key returns the resident
+    # (mutated-key) proof, then a reload once the switch is off again
+    qc[3] = saved
+    monkeypatch.setenv("PNP_V1_REUSE", "1")
+    lib.gen_proof(inp.circuit, inp.pk, inp.ck)          # loads (fingerprint unknown)
+    qc[3] = qc[5]
+    stale = lib.gen_proof(inp.circuit, inp.pk, inp.ck)  # same fingerprint: reused
+    assert abi.proof_to_bytes(stale) == abi.proof_to_bytes(first)
+    monkeypatch.delenv("PNP_V1_REUSE")
+    fresh = lib.gen_proof(inp.circuit, inp.pk, inp.ck)
+    assert abi.proof_to_bytes(fresh) == abi.proof_to_bytes(exp)
+
+
+def test_v1_srs_change_rebuilds_table():
+    """v1 with a different SRS in the SAME buffer: the device-side comparison
+    sees the change and the folded MSM table is rebuilt (proof == oracle)."""
+    import numpy as np
+    import pnp
+    from pnp_testlib import oracle, vp
+    lib = pnp.load()
+    inp = Inputs(9, 45)
+    assert abi.proof_to_bytes(lib.gen_proof(inp.circuit, inp.pk, inp.ck)) == \
+        abi.proof_to_bytes(inp.oracle_proof())
+    tau2 = np.array([[7, 0, 0, 0]], dtype=np.uint64)
+    oracle().or_srs(vp(inp.arrays["srs"]), inp.n, vp(tau2))   # new SRS written in place
+    got = lib.gen_proof(inp.circuit, inp.pk, inp.ck)
+    assert abi.proof_to_bytes(got) == abi.proof_to_bytes(inp.oracle_proof())
+
+
+def test_v1_strict_envelope(monkeypatch, tmp_path):
+    """PNP_V1_STRICT=1 refuses (print + exit, the v1 error contract) a key with
+    live q_m / q_lookup selectors, where the reference GPU path and this
+    backend return different proofs; a Merkle-class key proves normally."""
+    import subprocess
+    import sys
+    import textwrap
+    code = textwrap.dedent("""
+        import os, sys
+        sys.path.insert(0, %r)
+        import conftest  # noqa: F401  (sys.path)
+        import pnp
+        from pnp import abi
+        from pnp_testlib import Inputs
+        inp = Inputs(8, 47, qm_qlookup_evals=(sys.argv[1] == "live"))
+        p = pnp.load().gen_proof(inp.circuit, inp.pk, inp.ck)
+        print("ok", abi.proof_to_bytes(p) == abi.proof_to_bytes(inp.oracle_proof()))
+    """ % os_path_tests())
+    env = dict(__import__("os").environ, PNP_V1_STRICT="1")
+    ok = subprocess.run([sys.executable, "-c", code, "merkle"], env=env, capture_output=True, text=True,
+                        timeout=300)
+    assert ok.returncode == 0 and "ok True" in ok.stdout, ok.stderr[-2000:]
+    bad = subprocess.run([sys.executable, "-c", code, "live"], env=env, capture_output=True, text=True,
+                         timeout=300)
+    assert bad.returncode != 0 and "PNP_V1_STRICT" in bad.stderr, bad.stderr[-2000:]
+
+
+def os_path_tests():
+    import os
+    return os.path.dirname(os.path.abspath(__file__))

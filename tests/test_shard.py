@@ -66,17 +66,20 @@ def test_sharded_gen_proof_parity(tmp_path, world):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("world", [2, 4, 8])
-def test_sharded_full_size_matches_golden(tmp_path, world):
-    """The HEIGHT=15 instance (n = 2^22, bench.Synthetic seed 1) proved by
-    `world` ranks sharing the GPU — point-range MSMs (c = 20 down to the
-    2^19-point ranks of world 8), distributed round 4 over 8/world blocks and
-    the all-to-all — equals the golden ProofC the CPU restatement produced
-    (tests/golden/full_2e22_seed1.json) on every rank."""
+@pytest.mark.parametrize("golden,world", [("full_2e22_seed1.json", 2), ("full_2e22_seed1.json", 4),
+                                          ("full_2e22_seed1.json", 8), ("merkle_h15_seed1.json", 2),
+                                          ("merkle_h15_seed1.json", 8)])
+def test_sharded_full_size_matches_golden(tmp_path, golden, world):
+    """The HEIGHT=15 instances (n = 2^22, bench.Synthetic seed 1: the round-1
+    arithmetic stand-in and the bench's default, the reference's Poseidon
+    Merkle circuit) proved by `world` ranks sharing the GPU — point-range MSMs
+    (c = 20 down to the 2^19-point ranks of world 8), distributed round 4 over
+    8/world blocks and the all-to-all — equal the golden ProofC the CPU
+    restatement produced (tests/golden/make_golden_full.py) on every rank."""
     import json
-    path = os.path.join(HERE, "golden", "full_2e22_seed1.json")
+    path = os.path.join(HERE, "golden", golden)
     if not os.path.exists(path):
-        pytest.skip("golden 2^22 proof not generated")
+        pytest.skip(f"golden {golden} not generated")
     with open(path) as f:
         g = json.load(f)
     # the ranks share this GPU's HBM with this (pytest) process: hand back the
@@ -86,7 +89,8 @@ def test_sharded_full_size_matches_golden(tmp_path, world):
         torch.cuda.synchronize()
         torch.cuda.empty_cache()
     prefix = str(tmp_path / "full")
-    _launch(world, ["full", prefix, str(g["lg"]), str(g["gates"]), str(g["seed"])], tmp_path, 900)
+    _launch(world, ["full", prefix, str(g["lg"]), str(g["gates"]), str(g["seed"]), g.get("circuit", "arith")],
+            tmp_path, 900)
     for r in range(world):
         assert open(f"{prefix}.{r}", "rb").read().hex() == g["proof_hex"], f"rank {r}"
 
@@ -96,25 +100,12 @@ def test_sharded_full_size_matches_golden(tmp_path, world):
 def test_sharded_merkle_circuit(tmp_path, world):
     """The reference's Poseidon Merkle circuit (bench.Synthetic(circuit=
     "merkle"), HEIGHT = 8 at 2^15: PI at the last gate, the real selector and
-    copy-cycle pattern) proved by `world` ranks equals the single-GPU proof of
-    the same instance (which tests/test_gpu_merkle.py pins to the oracle)."""
-    import torch
-    import pnp
+    copy-cycle pattern) proved by `world` ranks equals the CPU restatement's
+    proof of the same instance (tests/synth_cpu.py SyntheticCPU, merkle)."""
     from pnp import abi
-    sys.path.insert(0, os.path.dirname(HERE))
-    from bench import Synthetic
+    from synth_cpu import SyntheticCPU
     lg, seed = 15, 4
-    ctx = pnp.Context(0)
-    try:
-        syn = Synthetic(ctx, lg, 0, seed=seed, circuit="merkle")
-        ctx.load_prover_key(syn.pk, syn.n, device_ptrs=True)
-        ctx.load_commit_key(syn.ck, syn.n, device_ptrs=True)
-        exp = abi.proof_to_bytes(ctx.prove(syn.cs, device_ptrs=True))
-    finally:
-        ctx.close()
-    del syn
-    torch.cuda.synchronize()
-    torch.cuda.empty_cache()
+    exp = abi.proof_to_bytes(SyntheticCPU(lg, 0, seed, circuit="merkle").oracle_proof())
     prefix = str(tmp_path / "mk")
     _launch(world, ["full", prefix, str(lg), "0", str(seed), "merkle"], tmp_path, 600)
     for r in range(world):

@@ -132,3 +132,16 @@ def test_wrong_statement_rejected():
     assert not verify(vk, proof, [(pos, val)], t, label=b"plonk")
     bad = Inputs(6, 7, satisfying=False)
     assert not verify(inputs_vk(bad), bad.oracle_proof(), inputs_pis(bad), bad.tau_mont[0])
+
+
+def test_verifier_key_tau_equals_msm_key():
+    """or_verifier_key_tau ([p(tau)] G) == or_verifier_key_from_coeffs (MSM over
+    the SRS): the trapdoor key bench.py's self-check uses is the real key."""
+    from pnp_testlib import verifier_key_tau, VK_POLYS
+    inp = Inputs(8, 12, qm_qlookup_evals=True)
+    a = inp.arrays
+    coeffs = {k: a[k + "_coeffs"] for k in VK_POLYS if k + "_coeffs" in a}
+    assert "q_m" in coeffs and "q_lookup" in coeffs
+    exp = inputs_vk(inp)
+    got = verifier_key_tau(coeffs, inp.n, a["srs"][0], inp.tau_mont[0])
+    assert np.array_equal(got, exp)

@@ -504,6 +504,31 @@ int pnp_load_prover_key(pnp_ctx *ctx, const ProverKeyC *pk, uint64_t D, int devi
     });
 }
 
+}  // extern "C"
+
+namespace {
+
+// make `up` (n_points packed affine points in HBM) the resident SRS.  The
+// folded MSM table built from the previous SRS stays valid when the bytes are
+// the same (a per-call upload of an unchanged key, as the v1 symbol does).
+void adopt_ck(pnp_ctx *ctx, pnp::DevBuf &up, uint64_t n_points) {
+    const bool same = ctx->ck_owned.p && ctx->ck_dev == ctx->ck_owned.u64() && ctx->ck_points == n_points &&
+                      !pnp::k_any_diff(up.u64(), ctx->ck_owned.u64(), 12 * n_points, ctx->scratch_b, ctx->stream);
+    PNP_HIP(hipStreamSynchronize(ctx->stream));
+    if (!same) {
+        std::swap(ctx->ck_owned, up);
+        ctx->ck_dev = ctx->ck_owned.u64();
+        ctx->ck_table_n = 0;  // rebuilt from the new key on the next commitment
+        ctx->ck_table.release();
+    }
+    ctx->ck_points = n_points;
+    ctx->ck_loaded = true;
+}
+
+}  // namespace
+
+extern "C" {
+
 int pnp_load_commit_key(pnp_ctx *ctx, const CommitKeyC *ck, uint64_t n_points, int device_ptrs) {
     if (!ctx || !ck || !ck->powers_of_g || n_points == 0) return PNP_E_ARG;
     PNP_TRY({
@@ -512,18 +537,64 @@ int pnp_load_commit_key(pnp_ctx *ctx, const CommitKeyC *ck, uint64_t n_points, i
         if (device_ptrs) {
             ctx->ck_owned.release();
             ctx->ck_dev = ck->powers_of_g;
+            ctx->ck_points = n_points;
+            ctx->ck_table_n = 0;
+            ctx->ck_table.release();
+            ctx->ck_loaded = true;
         } else {
-            ctx->ck_owned.alloc(n_points * 96);
-            PNP_HIP(hipMemcpyAsync(ctx->ck_owned.p, ck->powers_of_g, n_points * 96,
-                                   hipMemcpyHostToDevice, ctx->stream));
-            PNP_HIP(hipStreamSynchronize(ctx->stream));
-            ctx->ck_dev = ctx->ck_owned.u64();
+            // upload (as the reference does per call, load.cu:348-358)
+            pnp::DevBuf up(n_points * 96);
+            PNP_HIP(hipMemcpyAsync(up.p, ck->powers_of_g, n_points * 96, hipMemcpyHostToDevice, ctx->stream));
+            adopt_ck(ctx, up, n_points);
         }
-        ctx->ck_points = n_points;
-        ctx->ck_table_n = 0;  // rebuilt from the new key on the next commitment
-        ctx->ck_table.release();
-        ctx->ck_loaded = true;
     });
+}
+
+int pnp_load_commit_key_strided(pnp_ctx *ctx, const void *points, uint64_t n_points,
+                                const pnp_affine_layout *layout, int device_ptrs) {
+    if (!ctx || !points || !layout || n_points == 0) return PNP_E_ARG;
+    const pnp_affine_layout L = *layout;
+    if (L.stride % 8 || L.x_off % 8 || L.y_off % 8 || L.x_off + 48 > L.stride || L.y_off + 48 > L.stride ||
+        L.inf_off >= L.stride || (L.x_off < L.y_off + 48 && L.y_off < L.x_off + 48) ||
+        (L.inf_off >= L.x_off && L.inf_off < L.x_off + 48) || (L.inf_off >= L.y_off && L.inf_off < L.y_off + 48)) {
+        pnp::set_error("affine layout: stride %llu, x at %llu, y at %llu, infinity at %llu is not a G1Affine layout",
+                       (unsigned long long)L.stride, (unsigned long long)L.x_off, (unsigned long long)L.y_off,
+                       (unsigned long long)L.inf_off);
+        return PNP_E_ARG;
+    }
+    PNP_TRY({
+        PNP_HIP(hipSetDevice(ctx->device));
+        ctx->ck_loaded = false;
+        pnp::DevBuf raw;
+        const uint8_t *src = static_cast<const uint8_t *>(points);
+        if (!device_ptrs) {
+            raw.alloc(n_points * L.stride);
+            PNP_HIP(hipMemcpyAsync(raw.p, points, n_points * L.stride, hipMemcpyHostToDevice, ctx->stream));
+            src = static_cast<const uint8_t *>(raw.p);
+        }
+        pnp::DevBuf up(n_points * 96);
+        if (!pnp::k_pack_affine(src, n_points, L.stride, L.x_off, L.y_off, L.inf_off, up.u64(), ctx->scratch_b,
+                                ctx->stream)) {
+            pnp::set_error("commit key holds the point at infinity (an SRS [tau^i] G never does)");
+            throw pnp::Error(PNP_E_ARG);
+        }
+        raw.release();
+        adopt_ck(ctx, up, n_points);
+    });
+}
+
+uint32_t pnp_proof_infinity_mask(const ProofC *p) {
+    if (!p) return 0;
+    const CommitmentC *c = reinterpret_cast<const CommitmentC *>(p);
+    uint64_t one[6];
+    to_u64_limbs(Fq::one(), one);
+    uint32_t m = 0;
+    for (int k = 0; k < PNP_PROOF_COMMITMENTS; k++) {
+        bool x0 = true;
+        for (int j = 0; j < 6; j++) x0 &= c[k].x[j] == 0;
+        if (x0 && !memcmp(c[k].y, one, 48)) m |= 1u << k;
+    }
+    return m;
 }
 
 int pnp_prove(pnp_ctx *ctx, const CircuitC *cs, int device_ptrs, ProofC *out) {
@@ -563,16 +634,29 @@ int pnp_last_stage_times(pnp_ctx *ctx, double *ms, const char **names, int cap) 
 
 namespace {
 
-// v1 key reuse.  The Rust caller hands the same ProverKey / CommitKey buffers
-// to every proof (prover.rs:765-901 reinterprets the prover key's Vecs in
-// place); the reference copies all of them to the device on every call
+// v1 keys.  The reference copies every key array to the device on every call
 // (load.cu:311-358, gen_proof.cuh:64-78, 166-180, 280-314: ~22 GiB at
-// HEIGHT=15).  Here the resident copy made by the first call is reused while
-// the fingerprint of the key (every field pointer, the domain, and 257 evenly
-// spaced words of every array the prover reads, first and last included)
-// is unchanged; any difference reloads everything (the full copy and key
-// checks of pnp_load_*).  PNP_V1_RELOAD=1 reloads on every call, as the
-// reference does.
+// HEIGHT=15), so a caller may rewrite its key buffers in place between calls.
+// The v1 symbol keeps that contract by default: every call uploads the whole
+// prover key and commit key (pnp_load_*), and the proof reads only what this
+// call uploaded.  The one expensive derived object, the folded MSM table of
+// the SRS, is kept when the uploaded SRS equals the resident one byte for byte
+// (compared on the device, pnp_load_commit_key).
+// PNP_V1_REUSE=1 (opt-in, for callers that never mutate their keys, like
+// merkle-tree's main.rs and pnp_bench.rs): the resident copy made by an
+// earlier call is reused while the key's fingerprint (every field pointer, the
+// domain, and 257 evenly spaced words of every array the prover reads) is
+// unchanged, saving the ~22 GiB upload.
+// PNP_V1_STRICT=1: reject prover keys outside the reference GPU path's
+// envelope (non-zero custom-gate selectors, q_lookup or lookup tables), for
+// which this backend returns the ZK-Garage prover's proof while the reference
+// GPU path would return a different one.
+bool key_tables_zero(pnp_ctx *ctx) {
+    const uint64_t *t[4] = {ctx->pk_dev.table1, ctx->pk_dev.table2, ctx->pk_dev.table3, ctx->pk_dev.table4};
+    for (const uint64_t *p : t)
+        if (p && pnp::k_any_nonzero(p, 4 * ctx->pk_n, ctx->scratch_b, ctx->stream)) return false;
+    return true;
+}
 uint64_t mix64(uint64_t h, uint64_t v) {
     h ^= v + 0x9e3779b97f4a7c15ULL + (h << 6) + (h >> 2);
     return h * 0xff51afd7ed558ccdULL;
@@ -606,13 +690,17 @@ uint64_t ck_fingerprint(const CommitKeyC &ck, uint64_t D) {
 extern "C" {
 
 // v1: lib/hello.cu:4-6.  Same contract as the reference (structs by value,
-// synchronous, device 0, print-and-exit on errors, caffe/common.hpp:23-30);
-// keys are re-copied only when they change (see pk_fingerprint).
+// synchronous, device 0, keys uploaded per call, print-and-exit on errors,
+// caffe/common.hpp:23-30); see the v1 keys note above for the switches.
 ProofC gen_proof(CircuitC circuit, ProverKeyC pk, CommitKeyC ck) {
     static pnp_ctx *ctx = nullptr;
     static bool have_pk = false, have_ck = false;
     static uint64_t fp_pk = 0, fp_ck = 0;
-    static const bool reload = getenv("PNP_V1_RELOAD") != nullptr;
+    auto env_on = [](const char *name) {  // read per call: a caller may switch modes
+        const char *e = getenv(name);
+        return e && atoi(e) != 0;
+    };
+    const bool reuse = env_on("PNP_V1_REUSE"), strict = env_on("PNP_V1_STRICT");
     ProofC out;
     memset(&out, 0, sizeof out);
     auto die = [](int rc) {
@@ -625,14 +713,21 @@ ProofC gen_proof(CircuitC circuit, ProverKeyC pk, CommitKeyC ck) {
     uint64_t D = 1;
     while (D < bound) D <<= 1;
     if (!ck.powers_of_g) die(PNP_E_ARG);
-    const uint64_t fpk = pk_fingerprint(pk, D), fck = ck_fingerprint(ck, D);
-    if (reload || !have_pk || fpk != fp_pk || !ctx->pk_loaded) {
+    const uint64_t fpk = reuse ? pk_fingerprint(pk, D) : 0, fck = reuse ? ck_fingerprint(ck, D) : 0;
+    if (!reuse || !have_pk || fpk != fp_pk || !ctx->pk_loaded) {
         have_pk = false;
         if ((rc = pnp_load_prover_key(ctx, &pk, D, 0)) != PNP_OK) die(rc);
+        if (strict && (!ctx->pk_qm_zero || !ctx->pk_qlookup_zero || ctx->pk_custom_nz[0] ||
+                       ctx->pk_custom_nz[1] || ctx->pk_custom_nz[2] || ctx->pk_custom_nz[3] ||
+                       !key_tables_zero(ctx))) {
+            set_error("PNP_V1_STRICT: prover key outside the reference GPU path's envelope (custom-gate "
+                      "selectors, q_m, q_lookup or lookup tables non-zero)");
+            die(PNP_E_ENVELOPE);
+        }
         have_pk = true;
         fp_pk = fpk;
     }
-    if (reload || !have_ck || fck != fp_ck || !ctx->ck_loaded) {
+    if (!reuse || !have_ck || fck != fp_ck || !ctx->ck_loaded) {
         have_ck = false;
         if ((rc = pnp_load_commit_key(ctx, &ck, D, 0)) != PNP_OK) die(rc);
         have_ck = true;

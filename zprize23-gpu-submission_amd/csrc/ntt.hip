@@ -923,6 +923,22 @@ static const uint32_t *block_twist_table29(NttTables &t, uint32_t lg_n, bool inv
                         8ULL << lg_n, s);
 }
 
+// Every table a proof of domain 2^lg_n reads, built on stream s.  The tables
+// are otherwise built lazily by their first user; a proof forks LDEs onto a
+// side stream, so prove_impl builds them on its main stream before the first
+// fork (the side stream then waits for them through the fork event).
+void ntt_warm(NttTables &t, uint32_t lg_n, hipStream_t s) {
+    for (bool inv : {false, true}) {
+        ntt_twiddles(t, lg_n, inv, s);
+        block_twist_table(t, lg_n, inv, s);
+        if (ntt29_enabled()) {
+            ntt_twiddles29(t, lg_n, inv, s);
+            block_twist_table29(t, lg_n, inv, s);
+        }
+    }
+    ntt_prepare_coset(t, s);
+}
+
 void lde_blocks(NttTables &t, const uint64_t *in, uint64_t *out, uint32_t lg_n, int m0, int nb,
                 hipStream_t s) {
     const uint64_t n = 1ULL << lg_n;

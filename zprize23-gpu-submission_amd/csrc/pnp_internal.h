@@ -73,6 +73,9 @@ void coset_lde8(NttTables &t, const uint64_t *in, uint64_t *out8, uint32_t lg_n,
 
 // block layout of the 8n coset (point i = 8 j + m -> block m, index j):
 // LDE of n coefficients into blocks m0 .. m0+nb-1 (any nb, m0 + nb <= 8)
+// build every NTT table of domain 2^lg_n on stream s (before forking work
+// that reads them onto another stream)
+void ntt_warm(NttTables &t, uint32_t lg_n, hipStream_t s);
 void lde_blocks(NttTables &t, const uint64_t *in, uint64_t *out, uint32_t lg_n, int m0, int nb,
                 hipStream_t s);
 // per block: unscaled inverse size-n DFT then twist by w_8n^(-m u)

@@ -72,6 +72,11 @@ void k_any_nonzero_n(const uint64_t *v, uint64_t words, uint64_t stride, int cnt
                      hipStream_t s);
 // any word of a differs from b
 bool k_any_diff(const uint64_t *a, const uint64_t *b, uint64_t words, DevBuf &scratch, hipStream_t s);
+// strided affine points (x / y: 6 u64 each at x_off / y_off, an infinity byte
+// at inf_off, `stride` bytes per point) -> packed 12-u64 points; false when a
+// point is flagged infinity (synchronous)
+bool k_pack_affine(const uint8_t *src, uint64_t n, uint64_t stride, uint64_t x_off, uint64_t y_off,
+                   uint64_t inf_off, uint64_t *dst, DevBuf &scratch, hipStream_t s);
 // out_i = a * in_i + b
 void k_affine(uint64_t *out, const uint64_t *in, const Fr &a, const Fr &b, uint64_t n, hipStream_t s);
 void k_quotient(const QuotArgs &q, uint64_t N8, uint64_t *out, hipStream_t s);

@@ -198,6 +198,37 @@ bool k_any_diff(const uint64_t *a, const uint64_t *b, uint64_t words, DevBuf &sc
     return h != 0;
 }
 
+// Strided affine points (arkworks' in-memory G1Affine: x, y Montgomery Fp384
+// limbs, an infinity bool, padding; layout given by offsets) -> packed
+// {x[6], y[6]}; *bad = 1 when a point is flagged infinity.
+__global__ void k_pack_affine_(const uint8_t *src, uint64_t n, uint64_t stride, uint64_t x_off, uint64_t y_off,
+                               uint64_t inf_off, uint64_t *dst, unsigned *bad) {
+    const uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint8_t *p = src + i * stride;
+    const uint64_t *x = reinterpret_cast<const uint64_t *>(p + x_off);
+    const uint64_t *y = reinterpret_cast<const uint64_t *>(p + y_off);
+#pragma unroll
+    for (int k = 0; k < 6; k++) {
+        dst[12 * i + k] = x[k];
+        dst[12 * i + 6 + k] = y[k];
+    }
+    if (p[inf_off]) atomicOr(bad, 1u);
+}
+bool k_pack_affine(const uint8_t *src, uint64_t n, uint64_t stride, uint64_t x_off, uint64_t y_off,
+                   uint64_t inf_off, uint64_t *dst, DevBuf &scratch, hipStream_t s) {
+    if (scratch.bytes < 16) scratch.alloc(16);
+    unsigned *bad = static_cast<unsigned *>(scratch.p);
+    PNP_HIP(hipMemsetAsync(bad, 0, 4, s));
+    hipLaunchKernelGGL(k_pack_affine_, dim3(nblk(n)), dim3(256), 0, s, src, n, stride, x_off, y_off, inf_off, dst,
+                       bad);
+    PNP_HIP(hipGetLastError());
+    unsigned h = 0;
+    PNP_HIP(hipMemcpyAsync(&h, bad, 4, hipMemcpyDeviceToHost, s));
+    PNP_HIP(hipStreamSynchronize(s));
+    return h == 0;
+}
+
 __global__ void k_affine_(uint64_t *out, const uint64_t *in, Fr a, Fr b, uint64_t n) {
     uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
     if (i < n) store_fr(out, i, load_fr(in, i) * a + b);

@@ -180,6 +180,10 @@ int prove_impl(pnp_ctx *ctx, const CircuitC *cs, int device_ptrs, ProofC *out, c
     Timer tm(ctx);
     auto &nt = ctx->ntt;
     k_proof_marker(s);
+    // the twiddle / twist tables are built lazily; build them here, on the main
+    // stream, so the side-stream LDEs (after fork()) and the main-stream LDEs
+    // both read finished tables
+    ntt_warm(nt, lg, s);
     // round-4 distribution (pnp_set_exchange_a2a, fixed at key load): this
     // rank's coset blocks [mb0, mb0 + nb) and coefficient range [q0, q0 + len)
     const int world = ctx->msm.world;

@@ -34,7 +34,7 @@ SYMBOLS = ("gen_proof", "pnp_last_error", "pnp_ctx_create", "pnp_ctx_destroy",
            "pnp_sync", "pnp_ntt", "pnp_coset_lde8", "pnp_commit", "pnp_commit_ck", "pnp_poly_eval",
            "pnp_poly_div_linear", "pnp_prefix_product", "pnp_batch_inverse",
            "pnp_synth_random_fr", "pnp_synth_srs", "pnp_synth_coset_consts", "pnp_synth_circuit",
-           "pnp_synth_merkle")
+           "pnp_synth_merkle", "pnp_load_commit_key_strided", "pnp_proof_infinity_mask")
 
 
 # int allgather(void *user, uint64_t bytes_per_rank) — pnp_set_msm_shard
@@ -97,11 +97,25 @@ def load(path: str = LIB_PATH):
                                       u64, vp]
     lib.pnp_synth_merkle.argtypes = [vp, C.c_uint32, vp, vp, vp, vp, C.c_void_p * 4, C.c_void_p * 9,
                                      C.c_void_p * 4, u64, vp]
+    lib.pnp_load_commit_key_strided.argtypes = [vp, vp, u64, C.POINTER(abi.AffineLayout), i32]
+    lib.pnp_proof_infinity_mask.argtypes = [C.POINTER(abi.ProofC)]
     for name in SYMBOLS:
         if name.startswith("pnp_") and name not in ("pnp_last_error", "pnp_ctx_destroy"):
             getattr(lib, name).restype = C.c_int if name != "pnp_last_error" else C.c_char_p
+    lib.pnp_proof_infinity_mask.restype = C.c_uint32
     _LIB = lib
     return lib
+
+
+def infinity_mask(proof: abi.ProofC) -> int:
+    """pnp_proof_infinity_mask: bit k set when the k-th commitment of the
+    ProofC (abi.PROOF_COMMITMENTS order) is the point at infinity."""
+    return int(load().pnp_proof_infinity_mask(C.byref(proof)))
+
+
+def infinity_flags(proof: abi.ProofC) -> dict:
+    m = infinity_mask(proof)
+    return {name: bool((m >> k) & 1) for k, name in enumerate(abi.PROOF_COMMITMENTS)}
 
 
 def check(rc: int, what: str = ""):
@@ -138,6 +152,13 @@ class Context:
     def load_commit_key(self, ck: abi.CommitKeyC, n_points: int, device_ptrs: bool):
         check(self.lib.pnp_load_commit_key(self.h, C.byref(ck), n_points, int(device_ptrs)),
               "pnp_load_commit_key")
+
+    def load_commit_key_strided(self, points: int, n_points: int, layout: abi.AffineLayout = abi.ARK_G1_AFFINE,
+                                device_ptrs: bool = False):
+        """The SRS in arkworks' own G1Affine memory layout (prover.rs:700-711
+        without the per-call conversion)."""
+        check(self.lib.pnp_load_commit_key_strided(self.h, C.c_void_p(points), n_points, C.byref(layout),
+                                                   int(device_ptrs)), "pnp_load_commit_key_strided")
 
     def prove(self, cs: abi.CircuitC, device_ptrs: bool) -> abi.ProofC:
         out = abi.ProofC()

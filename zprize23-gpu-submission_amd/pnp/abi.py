@@ -82,6 +82,17 @@ class CommitKeyC(C.Structure):
     _fields_ = [("powers_of_g", U64P), ("powers_of_gamma_g", U64P)]
 
 
+class AffineLayout(C.Structure):
+    """pnp_affine_layout: where x, y (6 u64 Montgomery limbs each) and the
+    infinity byte sit in one arkworks G1Affine of `stride` bytes."""
+    _fields_ = [("stride", C.c_uint64), ("x_off", C.c_uint64), ("y_off", C.c_uint64),
+                ("inf_off", C.c_uint64)]
+
+
+# ark-ec 0.3 GroupAffine<g1::Parameters> as rustc lays it out on x86-64
+# (x: Fp384, y: Fp384, infinity: bool, 7 bytes of padding)
+ARK_G1_AFFINE = AffineLayout(stride=104, x_off=0, y_off=48, inf_off=96)
+
 assert C.sizeof(ProofC) == 2656
 assert C.sizeof(CircuitC) == 72
 assert C.sizeof(ProverKeyC) == 44 * 8

@@ -108,6 +108,44 @@ class WindowExchange:
         return ALLTOALL_FN(cb)
 
 
+class SoloExchange(WindowExchange):
+    """One rank of a `world`-GPU proof run ALONE on one GPU (bench.py --solo):
+    the library does exactly rank `rank`'s share of the work (its MSM point
+    ranges, its round-4 blocks and coefficient range), and the collectives
+    are loopbacks (every slot gets this rank's data; the all-to-all returns
+    what was sent).  The proof is meaningless; the time is the per-rank
+    critical path of the multi-GPU proof without the xGMI transfers, which
+    the caller accounts for separately (`calls`, `bytes`)."""
+
+    def __init__(self, rank: int, world: int, device=None, a2a_bytes: int = 0):
+        import torch
+        self.rank, self.world, self.group = rank, world, None
+        self.buf = torch.zeros((1 << 20) // 8, dtype=torch.int64, device=device)
+        self.a2a = torch.zeros(a2a_bytes // 8, dtype=torch.int64, device=device) if a2a_bytes else None
+        torch.cuda.synchronize()
+        self.backend = "loopback"
+        self.calls = self.a2a_calls = 0
+        self.gather_bytes = self.a2a_bytes_moved = 0
+        self.error = None
+
+    def gather(self, bytes_per_rank: int) -> None:
+        import torch
+        w = bytes_per_rank // 8
+        mine = self.buf[self.rank * w:(self.rank + 1) * w].clone()
+        self.buf[: w * self.world].view(self.world, w).copy_(mine.expand(self.world, w))
+        torch.cuda.current_stream().synchronize()
+        self.calls += 1
+        self.gather_bytes += bytes_per_rank * self.world
+
+    def alltoall(self, bytes_per_peer: int) -> None:
+        import torch
+        w = bytes_per_peer // 8
+        self.a2a[w * self.world: 2 * w * self.world].copy_(self.a2a[: w * self.world])
+        torch.cuda.current_stream().synchronize()
+        self.a2a_calls += 1
+        self.a2a_bytes_moved += bytes_per_peer * (self.world - 1)
+
+
 def a2a_bytes_for(lg_n: int, world: int) -> int:
     """All-to-all buffer of the distributed round 4 (0 when world does not
     divide 8): send + receive slots of (8/world blocks) x (n/world) Fr."""
