@@ -136,6 +136,111 @@ __device__ __forceinline__ F29 mul2_29(const F29 &a, const F29 &b, const F29 &c,
     return r;
 }
 
+// ---- Karatsuba forms of the a b half (round 3 A/B, tools/ubench_kara.hip).
+// a = a0 + X^7 a1 (X = 2^29, 7-limb halves), likewise b:
+//   a b = L + X^7 (M - L - H) + X^14 H,  L = a0 b0, H = a1 b1,
+//   M = (a0 + a1)(b0 + b1)  (limb sums < 2^30: 7 products < 2^60 per column)
+// 3 x 49 = 147 multiply-adds instead of 196; the column of a b at step k is
+//   T_k = L_k + M_(k-7) - L_(k-7) - H_(k-7) + H_(k-14),
+// assembled inside the same finely integrated Montgomery loop (the column's
+// true value is >= 0 and < 2^63 whatever the order of the +/- terms, so the
+// 64-bit accumulator may wrap transiently).  L_j is kept from step j to j+7,
+// H_j from step j+7 to j+14.
+struct KaraHalves {
+    uint32_t sa[7], sb[7];
+};
+__device__ __forceinline__ void kara_sums(const F29 &a, const F29 &b, KaraHalves &h) {
+#pragma unroll
+    for (int i = 0; i < 7; i++) {
+        h.sa[i] = a.l[i] + a.l[i + 7];
+        h.sb[i] = b.l[i] + b.l[i + 7];
+    }
+}
+// column j (0..12) of a 7x7 product x y, x / y given as limb pointers
+#define PNP_KCOL(acc, x, y, j)                                                              \
+    _Pragma("unroll") for (int i_ = ((j) > 6 ? (j) - 6 : 0); i_ <= ((j) < 6 ? (j) : 6); i_++) \
+        acc = mad29((x)[i_], (y)[(j) - i_], acc)
+__device__ __forceinline__ F29 mul29k(const F29 &a, const F29 &b) {
+    KaraHalves h;
+    kara_sums(a, b, h);
+    uint32_t m[14];
+    uint64_t Lk[13], Hk[13];
+    F29 r;
+    uint64_t acc = 0;
+#pragma unroll
+    for (int k = 0; k < 27; k++) {
+        if (k <= 12) {
+            uint64_t l = 0;
+            PNP_KCOL(l, a.l, b.l, k);
+            Lk[k] = l;
+            acc += l;
+        }
+        if (k >= 7 && k <= 19) {
+            const int j = k - 7;
+            uint64_t hh = 0;
+            PNP_KCOL(hh, a.l + 7, b.l + 7, j);
+            Hk[j] = hh;
+            PNP_KCOL(acc, h.sa, h.sb, j);
+            acc -= Lk[j] + hh;
+        }
+        if (k >= 14) acc += Hk[k - 14];
+#pragma unroll
+        for (int i = (k > 13 ? k - 13 : 0); i < (k < 14 ? k : 14); i++) acc = mad29q(m[i], F29_Q[k - i], acc);
+        if (k < 14) {
+            m[k] = ((uint32_t)acc * F29_QINV) & F29_M;
+            acc = mad29q(m[k], F29_Q[0], acc);
+        } else {
+            r.l[k - 14] = (uint32_t)acc & F29_M;
+        }
+        acc >>= 29;
+    }
+    r.l[13] = (uint32_t)acc;
+    return r;
+}
+// a b + c d, both halves Karatsuba, one reduction (bounds as mul2_29)
+__device__ __forceinline__ F29 mul2_29k(const F29 &a, const F29 &b, const F29 &c, const F29 &d) {
+    KaraHalves h1, h2;
+    kara_sums(a, b, h1);
+    kara_sums(c, d, h2);
+    uint32_t m[14];
+    uint64_t Lk[13], Hk[13];
+    F29 r;
+    uint64_t acc = 0;
+#pragma unroll
+    for (int k = 0; k < 27; k++) {
+        if (k <= 12) {
+            uint64_t l = 0;
+            PNP_KCOL(l, a.l, b.l, k);
+            PNP_KCOL(l, c.l, d.l, k);
+            Lk[k] = l;
+            acc += l;
+        }
+        if (k >= 7 && k <= 19) {
+            const int j = k - 7;
+            uint64_t hh = 0;
+            PNP_KCOL(hh, a.l + 7, b.l + 7, j);
+            PNP_KCOL(hh, c.l + 7, d.l + 7, j);
+            Hk[j] = hh;
+            PNP_KCOL(acc, h1.sa, h1.sb, j);
+            PNP_KCOL(acc, h2.sa, h2.sb, j);
+            acc -= Lk[j] + hh;
+        }
+        if (k >= 14) acc += Hk[k - 14];
+#pragma unroll
+        for (int i = (k > 13 ? k - 13 : 0); i < (k < 14 ? k : 14); i++) acc = mad29q(m[i], F29_Q[k - i], acc);
+        if (k < 14) {
+            m[k] = ((uint32_t)acc * F29_QINV) & F29_M;
+            acc = mad29q(m[k], F29_Q[0], acc);
+        } else {
+            r.l[k - 14] = (uint32_t)acc & F29_M;
+        }
+        acc >>= 29;
+    }
+    r.l[13] = (uint32_t)acc;
+    return r;
+}
+#undef PNP_KCOL
+
 // a + K - b (K = F29_KA or F29_KB, b < K), carries normalised
 __device__ __forceinline__ F29 sub29(const F29 &a, const F29 &b, const uint32_t *K) {
     F29 r;

@@ -449,19 +449,31 @@ __global__ __launch_bounds__(256) void k_accumulate_flat(const uint64_t *points,
 // stored coordinates < 2^389, every product input < 2^391 (Y3 < 2^382 comes
 // from mul2_29).  No equal /
 // opposite / infinity cases: those make ZZ = 0 mod q, detected per piece.
+// PNP_F29_KARA=1: the Karatsuba a*b halves (field29.cuh mul29k / mul2_29k, 13%
+// fewer multiply-adds, same issue cycles; A/B in DESIGN.md)
+#ifndef PNP_F29_KARA
+#define PNP_F29_KARA 0
+#endif
+#if PNP_F29_KARA
+#define MUL29 mul29k
+#define MUL2_29 mul2_29k
+#else
+#define MUL29 mul29
+#define MUL2_29 mul2_29
+#endif
 __device__ __forceinline__ void madd29(Xyzz29 &p, const F29 &x2, const F29 &y2) {
-    F29 u2 = mul29(x2, p.zz);
-    F29 s2 = mul29(y2, p.zzz);
+    F29 u2 = MUL29(x2, p.zz);
+    F29 s2 = MUL29(y2, p.zzz);
     F29 P = sub29(u2, p.x, F29_KB);
     F29 R = sub29(s2, p.y, F29_KB);
     F29 pp = sqr29(P);
-    F29 ppp = mul29(P, pp);
-    F29 q = mul29(p.x, pp);
+    F29 ppp = MUL29(P, pp);
+    F29 q = MUL29(p.x, pp);
     F29 x3 = sub29(sub29(sub29(sqr29(R), ppp, F29_KA), q, F29_KA), q, F29_KA);
     // Y3 = R (Q - X3) - Y PPP as R (Q - X3) + Y (KA - PPP), one reduction
-    F29 y3 = mul2_29(R, sub29(q, x3, F29_KB), p.y, neg29(ppp, F29_KA));
-    p.zz = mul29(p.zz, pp);
-    p.zzz = mul29(p.zzz, ppp);
+    F29 y3 = MUL2_29(R, sub29(q, x3, F29_KB), p.y, neg29(ppp, F29_KA));
+    p.zz = MUL29(p.zz, pp);
+    p.zzz = MUL29(p.zzz, ppp);
     p.x = x3;
     p.y = y3;
 }
