@@ -485,6 +485,7 @@ def main():
     q_ms, q_n = ctx.kernel_stats("quotient")
     q_bytes = ctx.kernel_bytes("quotient")
     redo_lanes = ctx.kernel_bytes("msm_redo_lanes")
+    exact_fallbacks = ctx.kernel_bytes("msm_exact_fallback")
     ctx.kernel_timing(False)
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda" if backend == "nccl" else "cpu")
@@ -555,6 +556,7 @@ def main():
                                          "held_clock_basis": "GRBM_GUI_ACTIVE / 8 XCDs / kernel time "
                                                              "(profiles/r02_pmc_clock.txt)"},
                          "redo_lanes_per_proof": round(redo_lanes / args.steps, 2),
+                         "exact_fallbacks_per_proof": round(exact_fallbacks / args.steps, 2),
                          "hbm": {"achieved_gbs": round(achieved, 1), "peak_gbs": HBM_PEAK_GBS,
                                  "frac": round(achieved / HBM_PEAK_GBS, 5),
                                  "basis": "algorithmic bytes n*(96+32) per window sweep"},

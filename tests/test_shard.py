@@ -29,14 +29,23 @@ def _launch(world, args, tmp_path, timeout):
     for r in range(world):
         env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), LOCAL_RANK="0",
                    MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        log = open(tmp_path / f"rank{r}.log", "wb")  # a file, not a pipe: nothing can block on it
         procs.append(subprocess.Popen([sys.executable, os.path.join(HERE, "shard_worker.py")]
-                                      + args, env=env, stdout=subprocess.PIPE,
-                                      stderr=subprocess.STDOUT))
+                                      + args, env=env, stdout=log, stderr=subprocess.STDOUT))
     outs = []
     try:
-        for p in procs:
-            out, _ = p.communicate(timeout=timeout)
-            outs.append(out.decode(errors="replace"))
+        # a heartbeat on the real stderr (pytest captures sys.stderr): a GPU box
+        # takes a run that prints nothing for minutes for a hung one
+        import time
+        t0 = time.time()
+        while any(p.poll() is None for p in procs) and time.time() - t0 < timeout:
+            time.sleep(1)
+            if int(time.time() - t0) % 30 == 0:
+                print(f"  [{world} ranks: {sum(p.poll() is None for p in procs)} running, "
+                      f"{time.time() - t0:.0f} s]", file=sys.__stderr__, flush=True)
+        for r, p in enumerate(procs):
+            p.wait(timeout=max(1, timeout - (time.time() - t0)))
+            outs.append((tmp_path / f"rank{r}.log").read_bytes().decode(errors="replace"))
     finally:
         for p in procs:
             if p.poll() is None:

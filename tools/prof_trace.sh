@@ -8,4 +8,4 @@ STEPS=${2:-2}
 mkdir -p $R/gpurun_out/$TAG
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d $R/gpurun_out/$TAG -o run -- \
-    python3 $R/bench.py --steps $STEPS --warmup 1 --cpu-lg 0 > $R/gpurun_out/$TAG/bench.log 2>&1
+    python3 $R/bench.py --steps $STEPS --warmup 1 --cpu-lg 0 --drop-in "" --no-verify $BENCH_ARGS > $R/gpurun_out/$TAG/bench.log 2>&1

@@ -819,7 +819,11 @@ static void accumulate_group(MsmWork &wk, MsmGroup &gb, const GroupPlan &gp, con
         }
         const uint64_t per = (nent + slots - 1) / slots;  // entries per lane in one round
         const uint64_t rounds = std::max<uint64_t>(1, per / S);
-        S = (uint32_t)((per + rounds - 1) / rounds);
+        // a batch smaller than one round at S = 64 (one MSM of a 2^19-point
+        // rank range: ~35 entries per lane) takes shorter segments and fills
+        // the chip instead of leaving part of it idle (more bucket pieces to
+        // merge, a few % of the additions)
+        S = (uint32_t)std::max<uint64_t>(16, (per + rounds - 1) / rounds);
     }
     const uint64_t nthr = (nent + S - 1) / S;
     if (table) {

@@ -256,6 +256,14 @@ void msm_merge_pieces29_exact(const uint32_t *offs, uint64_t U, uint32_t S, uint
 __device__ __forceinline__ Xyzz29 bucket29(const uint32_t *bk, const uint32_t *offs, uint64_t u) {
     return offs[u] == offs[u + 1] ? inf29() : load_xyzz29(bk + 56 * u);
 }
+// Running sums from the top bucket down: S = sum_(j>=k) B_j, T = sum (j-k+1) B_j.
+// T == S as points exactly while the only non-empty bucket above k is k + 1
+// (T - S = sum_(j>k+1) (j-k-1) B_j): then an EMPTY bucket k makes the update
+// T + S a doubling, which the incomplete addition cannot do (it would flag the
+// whole group for the exact 32-bit redo).  `tis` tracks T == S; that step is
+// done as 2 T.  Empty buckets are rare at 2^22 points (~100 entries per
+// bucket) but not at the 2^19-point ranks of an 8-GPU proof (~13: e^-13 per
+// bucket, ~2 such leaves per proof).
 template <int LW>
 __global__ __launch_bounds__(256) void k_tree_leafw29(const uint32_t *bk, const uint32_t *offs, uint64_t nout,
                                                       uint32_t *out, uint32_t *exc) {
@@ -263,10 +271,20 @@ __global__ __launch_bounds__(256) void k_tree_leafw29(const uint32_t *bk, const 
     if (t >= nout) return;
     const uint64_t u0 = (uint64_t)LW * t;
     Xyzz29 S = bucket29(bk, offs, u0 + LW - 1), T = S;
+    bool tis = true;  // T == S
 #pragma unroll 1
     for (int k = LW - 2; k >= 0; k--) {
-        S = xadd29_inf(S, bucket29(bk, offs, u0 + k), exc);
-        T = xadd29_inf(T, S, exc);
+        const bool empty = offs[u0 + k] == offs[u0 + k + 1];
+        if (empty) {
+            // S unchanged; T + S = 2 T when T == S
+            T = tis ? xdbl29_inf(T) : xadd29_inf(T, S, exc);
+            tis = tis && zero29(T.zz);  // still equal only while both are infinity
+        } else {
+            S = xadd29_inf(S, load_xyzz29(bk + 56 * (u0 + k)), exc);
+            const bool tinf = zero29(T.zz);
+            T = xadd29_inf(T, S, exc);  // T != S here: S gained a bucket T lacks
+            tis = tinf;                 // inf + S = S
+        }
     }
     uint32_t *o = out + 168 * t;
     store_xyzz29(o, S);
