@@ -128,10 +128,19 @@ class SoloExchange(WindowExchange):
         self.gather_bytes = self.a2a_bytes_moved = 0
         self.error = None
 
+    # the 8-word exchange of the quotient chunks' non-zero flags (prover.cpp):
+    # the loopback all-to-all hands this rank its own blocks in every slot, so
+    # its t_7 / t_8 come out non-zero where the real distributed quotient of a
+    # satisfying circuit has them zero; the flags say zero, as every real
+    # rank would, so the rank commits the same 6 chunks as in the real run
+    T_FLAGS_BYTES = 64
+
     def gather(self, bytes_per_rank: int) -> None:
         import torch
         w = bytes_per_rank // 8
         mine = self.buf[self.rank * w:(self.rank + 1) * w].clone()
+        if bytes_per_rank == self.T_FLAGS_BYTES:
+            mine[6:8] = 0
         self.buf[: w * self.world].view(self.world, w).copy_(mine.expand(self.world, w))
         torch.cuda.current_stream().synchronize()
         self.calls += 1
