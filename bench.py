@@ -445,14 +445,18 @@ def main():
     gates = min(args.gates, 1 << args.lg)
     t0 = time.perf_counter()
     solo = None
+    # MSM sharding: bucket ranges (default) or point ranges (PNP_MSM_SHARD=points)
+    from pnp.shard import v_bytes_for
+    vb = (lambda w: 0) if os.environ.get("PNP_MSM_SHARD") == "points" else (lambda w: v_bytes_for(args.lg, w))
     if world > 1:  # sharded MSMs + distributed round 4, exchanges over RCCL
         from pnp.shard import WindowExchange, a2a_bytes_for
         ctx.set_msm_shard(WindowExchange(rank, world, device=torch.device("cuda", local),
-                                         a2a_bytes=a2a_bytes_for(args.lg, world)))
+                                         a2a_bytes=a2a_bytes_for(args.lg, world), v_bytes=vb(world)))
     elif args.solo:
         from pnp.shard import SoloExchange, a2a_bytes_for
         sr, sw = (int(v) for v in args.solo.split("/"))
-        solo = SoloExchange(sr, sw, device=torch.device("cuda", local), a2a_bytes=a2a_bytes_for(args.lg, sw))
+        solo = SoloExchange(sr, sw, device=torch.device("cuda", local), a2a_bytes=a2a_bytes_for(args.lg, sw),
+                            v_bytes=vb(sw))
         ctx.set_msm_shard(solo)
         args.no_verify, args.drop_in, args.cpu_lg = True, "", 0
     syn = Synthetic(ctx, args.lg, gates, seed=1, circuit=args.circuit)  # same instance on every rank
@@ -528,7 +532,8 @@ def main():
                                    + f" gen_proof: {gates} gates, domain 2^{args.lg}, "
                                    f"quotient on 2^{args.lg + 3} coset, pk+SRS+witness HBM-resident",
                        "circuit": args.circuit, "domain_log2": args.lg, "gates": gates,
-                       "parallelism": (f"msm-point-range-shard + round4-block-shard x{world}"
+                       "parallelism": (f"msm-{'point' if os.environ.get('PNP_MSM_SHARD') == 'points' else 'bucket'}"
+                                       f"-range-shard + round4-block-shard x{world}"
                                        if world > 1 else
                                        f"solo rank {solo.rank} of {solo.world} (loopback exchanges, "
                                        f"proof discarded)" if solo else "single")},
@@ -571,6 +576,8 @@ def main():
                            "alltoalls_per_proof": solo.a2a_calls / (args.steps + args.warmup),
                            "allgather_bytes_per_proof": solo.gather_bytes / (args.steps + args.warmup),
                            "alltoall_bytes_sent_per_proof": solo.a2a_bytes_moved / (args.steps + args.warmup),
+                           "bucket_alltoallvs_per_proof": solo.v_calls / (args.steps + args.warmup),
+                           "bucket_bytes_sent_per_proof": solo.v_bytes_moved / (args.steps + args.warmup),
                            "note": "per-rank work of a W-GPU proof; the collectives are loopbacks "
                                    "(their xGMI time is not included)"}
         if not args.no_verify:

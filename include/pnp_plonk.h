@@ -321,10 +321,27 @@ int pnp_kernel_bytes(pnp_ctx *ctx, const char *name, double *bytes);
  * d_a2a + (world + s) * bytes_per_peer. */
 typedef int (*pnp_allgather_fn)(void *user, uint64_t bytes_per_rank);
 typedef int (*pnp_alltoall_fn)(void *user, uint64_t bytes_per_peer);
+/* pnp_set_exchange_v (optional, before the first commitment; world must
+ * divide the bucket count): the folded MSMs shard BUCKET ranges instead of
+ * point ranges — rank s owns buckets [s NB/world, (s+1) NB/world) of every MSM
+ * of a batch, so each rank sorts, accumulates and reduces 1/world of the
+ * buckets (the point-range scheme reduces all of them on every rank).  Each
+ * rank digitises its own point range and sends every entry (8 bytes) to its
+ * bucket's owner: the library writes world segments to d_send (segment s,
+ * send_bytes[s] bytes, for rank s, back to back in rank order) and calls
+ * alltoallv(user, send_bytes, recv_bytes), which must leave the segment rank s
+ * sent to this rank at offset recv_bytes[0] + ... + recv_bytes[s-1] of d_recv
+ * (recv_bytes comes from a preceding all-gather of the counts).  A batch whose
+ * segments would not fit `capacity_bytes` (pathological scalars that crowd one
+ * bucket range) falls back to point ranges.  The commit key's folded table then
+ * covers all n points on every rank (6.5 GiB at n = 2^22). */
+typedef int (*pnp_alltoallv_fn)(void *user, const uint64_t *send_bytes, const uint64_t *recv_bytes);
 int pnp_set_msm_shard(pnp_ctx *ctx, int rank, int world, pnp_allgather_fn allgather,
                       void *user, uint64_t *d_xbuf, uint64_t xbuf_bytes);
 int pnp_set_exchange_a2a(pnp_ctx *ctx, pnp_alltoall_fn alltoall, void *user, uint64_t *d_a2a,
                          uint64_t a2a_bytes);
+int pnp_set_exchange_v(pnp_ctx *ctx, pnp_alltoallv_fn alltoallv, void *user, uint64_t *d_send,
+                       uint64_t *d_recv, uint64_t capacity_bytes);
 
 /* ------------------------------------------------------------------ */
 /* 3. Operator API on HBM pointers (mirrors PLONK/utils/function.cuh) */

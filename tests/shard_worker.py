@@ -10,12 +10,19 @@ gpu: every rank proves the same seeded instance on cuda:0 with point-range
      exchanges through host memory, since the ranks share one GPU) and writes
      its ProofC bytes to OUT_PREFIX.<rank>.
 full: the same over bench.Synthetic at full size (keys GPU-resident)."""
+import ctypes as C
 import os
 import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, HERE)
 sys.path.insert(0, os.path.join(os.path.dirname(HERE), "zprize23-gpu-submission_amd"))
+
+
+def _v_bytes(lg, world):
+    """PNP_TEST_MSM_SHARD=points: point-range MSMs; default: bucket ranges"""
+    from pnp.shard import v_bytes_for
+    return 0 if os.environ.get("PNP_TEST_MSM_SHARD") == "points" else v_bytes_for(lg, world)
 
 
 def main():
@@ -43,6 +50,23 @@ def main():
         for s in range(world):
             got = ex2.a2a[5 * (world + s):5 * (world + s) + 5]
             assert torch.equal(got, torch.arange(5) + 100 * s + 10 * rank), (s, got)
+        # variable all-to-all (bucket-range MSMs): rank r sends (r + 1) * (s + 1)
+        # words to rank s, valued 1000 r + s
+        ex3 = WindowExchange(rank, world, capacity_bytes=1 << 12, v_bytes=1 << 12)
+        send = [(rank + 1) * (s + 1) for s in range(world)]
+        at = 0
+        for s_, k in enumerate(send):
+            ex3.vsend[at:at + k] = 1000 * rank + s_
+            at += k
+        recv = [(r + 1) * (rank + 1) for r in range(world)]
+        ex3.alltoallv([8 * k for k in send], [8 * k for k in recv])
+        at = 0
+        for r, k in enumerate(recv):
+            assert torch.equal(ex3.vrecv[at:at + k], torch.full((k,), 1000 * r + rank)), (r, ex3.vrecv[at:at + k])
+            at += k
+        cbv = ex3.c_alltoallv()
+        arr = C.c_uint64 * world
+        assert cbv(None, arr(*[8 * k for k in send]), arr(*[8 * k for k in recv])) == 0 and ex3.v_calls == 2
         cb = ex.c_callback()
         assert cb(None, 24 * 8) == 0 and ex.calls == 4
         assert cb(None, 1 << 20) == 1 and ex.error is not None  # oversize slot -> error code
@@ -58,7 +82,8 @@ def main():
         from bench import Synthetic
         from pnp.shard import a2a_bytes_for
         ctx = pnp.Context(0)
-        ex = WindowExchange(rank, world, device="cuda", a2a_bytes=a2a_bytes_for(lg, world))
+        ex = WindowExchange(rank, world, device="cuda", a2a_bytes=a2a_bytes_for(lg, world),
+                            v_bytes=_v_bytes(lg, world))
         ctx.set_msm_shard(ex)
         syn = Synthetic(ctx, lg, gates, seed=seed, circuit=circuit)
         ctx.load_prover_key(syn.pk, syn.n, device_ptrs=True)
@@ -77,6 +102,8 @@ def main():
             raise
         assert ex.calls > 0
         assert (ex.a2a_calls > 0) == (8 % world == 0)
+        if os.environ.get("PNP_EXPECT_BUCKETS"):
+            assert (ex.v_calls > 0) == (os.environ["PNP_EXPECT_BUCKETS"] == "1"), ex.v_calls
         with open(f"{out}.{rank}", "wb") as f:
             f.write(abi.proof_to_bytes(proof))
         ctx.close()
@@ -88,13 +115,17 @@ def main():
         inp = Inputs(lg, seed)
         ctx = pnp.Context(0)
         from pnp.shard import a2a_bytes_for
-        ex = WindowExchange(rank, world, device="cuda", a2a_bytes=a2a_bytes_for(lg, world))
+        ex = WindowExchange(rank, world, device="cuda", a2a_bytes=a2a_bytes_for(lg, world),
+                            v_bytes=_v_bytes(lg, world))
         ctx.set_msm_shard(ex)
         ctx.load_prover_key(inp.pk, inp.n, device_ptrs=False)
         ctx.load_commit_key(inp.ck, inp.n, device_ptrs=False)
         proof = ctx.prove(inp.circuit, device_ptrs=False)
         assert ex.calls > 0
         assert (ex.a2a_calls > 0) == (8 % world == 0)
+        # bucket ranges whenever the bucket count splits (not 3 ranks, not tiny MSMs)
+        if os.environ.get("PNP_EXPECT_BUCKETS"):
+            assert (ex.v_calls > 0) == (os.environ["PNP_EXPECT_BUCKETS"] == "1"), ex.v_calls
         with open(f"{out}.{rank}", "wb") as f:
             f.write(abi.proof_to_bytes(proof))
         ctx.close()

@@ -23,12 +23,12 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _launch(world, args, tmp_path, timeout):
+def _launch(world, args, tmp_path, timeout, **extra_env):
     port = _free_port()
     procs = []
     for r in range(world):
         env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), LOCAL_RANK="0",
-                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), **extra_env)
         log = open(tmp_path / f"rank{r}.log", "wb")  # a file, not a pipe: nothing can block on it
         procs.append(subprocess.Popen([sys.executable, os.path.join(HERE, "shard_worker.py")]
                                       + args, env=env, stdout=log, stderr=subprocess.STDOUT))
@@ -62,23 +62,33 @@ def test_window_exchange_gloo_world2(tmp_path):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("world", [2, 3, 4, 8])
-def test_sharded_gen_proof_parity(tmp_path, world):
+@pytest.mark.parametrize("world,shard", [(2, "buckets"), (3, "buckets"), (4, "buckets"), (8, "buckets"),
+                                         (2, "points"), (8, "points")])
+def test_sharded_gen_proof_parity(tmp_path, world, shard):
+    """n = 2^13 (c = 10: 512 buckets per MSM): bucket ranges of 256 / 128 /
+    64 buckets at 2 / 4 / 8 ranks (3 ranks do not split the buckets and take
+    point ranges), and point ranges on request (PNP_TEST_MSM_SHARD=points)."""
     from pnp_testlib import Inputs
     from pnp import abi
-    lg, seed = 11, 3
+    lg, seed = 13, 3
     exp = abi.proof_to_bytes(Inputs(lg, seed).oracle_proof())
     prefix = str(tmp_path / "proof")
-    _launch(world, ["gpu", prefix, str(lg), str(seed)], tmp_path, 600)
+    buckets = shard == "buckets" and world != 3
+    # (the library takes bucket ranges from 4 ranks on; the 2-rank case lowers it)
+    _launch(world, ["gpu", prefix, str(lg), str(seed)], tmp_path, 600, PNP_TEST_MSM_SHARD=shard,
+            PNP_EXPECT_BUCKETS="1" if buckets else "0", PNP_MSM_BUCKETS_MIN_WORLD="2")
     for r in range(world):
         assert open(f"{prefix}.{r}", "rb").read() == exp, f"rank {r}"
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("golden,world", [("full_2e22_seed1.json", 2), ("full_2e22_seed1.json", 4),
-                                          ("full_2e22_seed1.json", 8), ("merkle_h15_seed1.json", 2),
-                                          ("merkle_h15_seed1.json", 8)])
-def test_sharded_full_size_matches_golden(tmp_path, golden, world):
+@pytest.mark.parametrize("golden,world,shard", [("full_2e22_seed1.json", 2, "buckets"),
+                                                ("full_2e22_seed1.json", 4, "buckets"),
+                                                ("full_2e22_seed1.json", 8, "buckets"),
+                                                ("merkle_h15_seed1.json", 2, "buckets"),
+                                                ("merkle_h15_seed1.json", 8, "buckets"),
+                                                ("merkle_h15_seed1.json", 8, "points")])
+def test_sharded_full_size_matches_golden(tmp_path, golden, world, shard):
     """The HEIGHT=15 instances (n = 2^22, bench.Synthetic seed 1: the round-1
     arithmetic stand-in and the bench's default, the reference's Poseidon
     Merkle circuit) proved by `world` ranks sharing the GPU — point-range MSMs
@@ -99,7 +109,8 @@ def test_sharded_full_size_matches_golden(tmp_path, golden, world):
         torch.cuda.empty_cache()
     prefix = str(tmp_path / "full")
     _launch(world, ["full", prefix, str(g["lg"]), str(g["gates"]), str(g["seed"]), g.get("circuit", "arith")],
-            tmp_path, 900)
+            tmp_path, 900, PNP_TEST_MSM_SHARD=shard, PNP_EXPECT_BUCKETS="1" if shard == "buckets" else "0",
+            PNP_MSM_BUCKETS_MIN_WORLD="2")
     for r in range(world):
         assert open(f"{prefix}.{r}", "rb").read().hex() == g["proof_hex"], f"rank {r}"
 

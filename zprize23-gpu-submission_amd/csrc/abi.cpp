@@ -42,8 +42,8 @@ void DevBuf::release() {
 // folded table of this rank's point range (msm_point_range) of the first n
 // SRS points, rebuilt when n or the sharding changes
 const uint64_t *commit_table(pnp_ctx *ctx, uint64_t n) {
-    uint64_t p0, p1;
-    msm_point_range(n, ctx->msm.rank, ctx->msm.world, p0, p1);
+    uint64_t p0 = 0, p1 = n;
+    if (!ctx->msm.full_table()) msm_point_range(n, ctx->msm.rank, ctx->msm.world, p0, p1);
     if (ctx->ck_table_n != n || ctx->ck_table_p0 != p0 || ctx->ck_table_p1 != p1) {
         ctx->ck_table_n = 0;
         msm_build_table(ctx->ck_table, ctx->ck_dev + 12 * p0, p1 - p0, ctx->msm.fold_c, ctx->stream);
@@ -224,6 +224,19 @@ int pnp_set_exchange_a2a(pnp_ctx *ctx, pnp_alltoall_fn alltoall, void *user, uin
     ctx->msm.a2a_user = user;
     ctx->msm.a2a = alltoall ? d_a2a : nullptr;
     ctx->msm.a2a_bytes = alltoall ? a2a_bytes : 0;
+    return PNP_OK;
+}
+
+int pnp_set_exchange_v(pnp_ctx *ctx, pnp_alltoallv_fn alltoallv, void *user, uint64_t *d_send,
+                       uint64_t *d_recv, uint64_t capacity_bytes) {
+    if (!ctx || (alltoallv && (!d_send || !d_recv || capacity_bytes < 8))) return PNP_E_ARG;
+    ctx->msm.alltoallv = alltoallv;
+    ctx->msm.v_user = user;
+    ctx->msm.v_send = alltoallv ? d_send : nullptr;
+    ctx->msm.v_recv = alltoallv ? d_recv : nullptr;
+    ctx->msm.v_bytes = alltoallv ? capacity_bytes : 0;
+    ctx->ck_table_n = 0;  // the folded table's point range changes
+    ctx->ck_table.release();
     return PNP_OK;
 }
 

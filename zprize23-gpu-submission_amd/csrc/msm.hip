@@ -86,6 +86,7 @@ struct KeyRows {
     int vstride, off, rows;
     uint32_t id_row0;
     uint64_t id_mul;
+    uint64_t id_base = 0;  // added to every entry id (a rank's first point in the full folded table)
 };
 
 // ---------------------------------------------------------------- 2. coarse pass
@@ -104,9 +105,19 @@ constexpr int SORT_CB = PNP_SORT_CB;
 constexpr int SORT_FB_MAX = 11;
 // three 2^CB-entry u32 LDS arrays + the 2 x 16 KiB tile of k_coarse_scatter
 static_assert(SORT_CB >= 1 && SORT_CB <= 12, "PNP_SORT_CB out of range (LDS budget of k_coarse_scatter)");
+// counts / offsets index of (virtual window v, coarse bin b, chunk ch):
+// v-major; or, with wmaj > 1 destinations (bucket-range sharding: the top
+// log2(wmaj) bits of b name the rank owning the bucket), destination-major,
+// so every destination's entries are one contiguous run
+__device__ __forceinline__ uint64_t cidx(int v, int nv, uint32_t b, int NBc, int wmaj, int ch, int nch) {
+    if (wmaj <= 1) return ((uint64_t)v * NBc + b) * nch + ch;
+    const uint32_t nbl = (uint32_t)NBc / wmaj;
+    return (((uint64_t)(b / nbl) * nv + v) * nbl + b % nbl) * nch + ch;
+}
+
 __global__ __launch_bounds__(1024) void k_coarse_hist(const uint32_t *keys, KeyRows kr, int fb,
                                                       int NBc, uint64_t chunk, int nch,
-                                                      uint32_t *counts) {
+                                                      uint32_t *counts, int wmaj = 1) {
     __shared__ uint32_t hist[1 << SORT_CB];
     const int v = blockIdx.y, ch = blockIdx.x;
     for (int b = threadIdx.x; b < NBc; b += blockDim.x) hist[b] = 0;
@@ -133,8 +144,7 @@ __global__ __launch_bounds__(1024) void k_coarse_hist(const uint32_t *keys, KeyR
         }
     }
     __syncthreads();
-    for (int b = threadIdx.x; b < NBc; b += blockDim.x)
-        counts[((uint64_t)v * NBc + b) * nch + ch] = hist[b];
+    for (int b = threadIdx.x; b < NBc; b += blockDim.x) counts[cidx(v, gridDim.y, b, NBc, wmaj, ch, nch)] = hist[b];
 }
 
 // ---------------------------------------------------------------- 3. scan
@@ -224,16 +234,18 @@ __device__ __forceinline__ void tile_scan(uint32_t *lh, uint32_t *lofs, int nb) 
     }
 }
 
+// rec != nullptr: entries leave as 8-byte records entry | fine key << 32 (the
+// bucket-range exchange format) instead of the ent / fk arrays
 __global__ __launch_bounds__(1024) void k_coarse_scatter(const uint32_t *keys, KeyRows kr, int fb,
                                                          int NBc, uint64_t chunk, int nch,
                                                          const uint32_t *offs, uint32_t *ent,
-                                                         uint16_t *fk) {
+                                                         uint16_t *fk, int wmaj = 1, uint64_t *rec = nullptr) {
     __shared__ uint32_t cur[1 << SORT_CB], lh[1 << SORT_CB], lofs[1 << SORT_CB];
     __shared__ uint32_t st_e[TILE_K];
     __shared__ uint32_t st_m[TILE_K];
     const int v = blockIdx.y, ch = blockIdx.x;
     for (int b = threadIdx.x; b < NBc; b += blockDim.x) {
-        cur[b] = offs[((uint64_t)v * NBc + b) * nch + ch];
+        cur[b] = offs[cidx(v, gridDim.y, b, NBc, wmaj, ch, nch)];
         lh[b] = 0;
     }
     __syncthreads();
@@ -244,7 +256,7 @@ __global__ __launch_bounds__(1024) void k_coarse_scatter(const uint32_t *keys, K
     const bool vec = ((n | chunk) & 3) == 0;
     for (int r = 0; r < kr.rows; r++) {
         const uint32_t *k = kb + (uint64_t)r * n;
-        const uint32_t idb = (uint32_t)((kr.id_row0 + r) * kr.id_mul);
+        const uint32_t idb = (uint32_t)((kr.id_row0 + r) * kr.id_mul + kr.id_base);
         for (uint64_t tb = lo; tb < hi; tb += TILE_K) {
             const uint64_t i0 = tb + 4 * threadIdx.x;
             uint32_t key[4], rank[4];
@@ -273,8 +285,12 @@ __global__ __launch_bounds__(1024) void k_coarse_scatter(const uint32_t *keys, K
             for (uint32_t x = threadIdx.x; x < total; x += blockDim.x) {
                 uint32_t mag = st_m[x], bn = mag >> fb;
                 uint32_t pos = cur[bn] + x - lofs[bn];
-                ent[pos] = st_e[x];
-                fk[pos] = (uint16_t)(mag & fmask);
+                if (rec) {
+                    rec[pos] = st_e[x] | ((uint64_t)(mag & fmask) << 32);
+                } else {
+                    ent[pos] = st_e[x];
+                    fk[pos] = (uint16_t)(mag & fmask);
+                }
             }
             __syncthreads();
             for (int b = threadIdx.x; b < NBc; b += blockDim.x) {
@@ -367,6 +383,76 @@ __global__ __launch_bounds__(1024) void k_fine_sort(const uint32_t *ent, const u
             lh[q] = 0;
         }
         __syncthreads();
+    }
+}
+
+// pass B over received records (bucket-range sharding): bin p's entries are
+// `W` runs runs[p W + r] = {start, len} of 8-byte records (entry | fine << 32)
+// in the receive buffer, one per source rank; the bin's sorted entries go to
+// [out0[p], out0[p] + sum of lens) — otherwise as k_fine_sort
+__global__ __launch_bounds__(1024) void k_fine_sort_runs(const uint64_t *rec, const uint2 *runs, int W,
+                                                         const uint32_t *out0, int fb, uint32_t *bstart,
+                                                         uint32_t *sorted) {
+    __shared__ uint32_t h[1 << SORT_FB_MAX], lh[1 << SORT_FB_MAX], lofs[1 << SORT_FB_MAX];
+    __shared__ uint32_t st_e[TILE_F];
+    __shared__ uint16_t st_f[TILE_F];
+    const uint64_t p = blockIdx.x;
+    const int NF = 1 << fb;
+    for (int f = threadIdx.x; f < NF; f += blockDim.x) h[f] = lh[f] = 0;
+    __syncthreads();
+    for (int r = 0; r < W; r++) {
+        const uint2 run = runs[p * W + r];
+        for (uint32_t k = threadIdx.x; k < run.y; k += blockDim.x)
+            atomicAdd(&h[(uint32_t)(rec[run.x + k] >> 32) & 0xFFFFu], 1u);
+    }
+    __syncthreads();
+    tile_scan(h, lofs, NF);
+    __syncthreads();
+    const uint32_t ps = out0[p];
+    for (int f = threadIdx.x; f < NF; f += blockDim.x) h[f] = ps + lofs[f];  // cursor of fine bin f
+    __syncthreads();
+    for (int f = threadIdx.x; f < NF; f += blockDim.x) bstart[p * NF + f] = h[f];
+    constexpr int PER = TILE_F / 1024;
+    for (int r = 0; r < W; r++) {
+        const uint2 run = runs[p * W + r];
+        for (uint32_t tb = 0; tb < run.y; tb += TILE_F) {
+            uint32_t e[PER], rank[PER], f[PER];
+#pragma unroll
+            for (int j = 0; j < PER; j++) {
+                const uint32_t k = tb + threadIdx.x + j * 1024;
+                f[j] = 0;
+                if (k < run.y) {
+                    const uint64_t x = rec[run.x + k];
+                    e[j] = (uint32_t)x;
+                    f[j] = (uint32_t)(x >> 32) & 0xFFFFu;
+                    rank[j] = atomicAdd(&lh[f[j]], 1u);
+                }
+            }
+            __syncthreads();
+            tile_scan(lh, lofs, NF);
+            __syncthreads();
+#pragma unroll
+            for (int j = 0; j < PER; j++) {
+                const uint32_t k = tb + threadIdx.x + j * 1024;
+                if (k < run.y) {
+                    const uint32_t at = lofs[f[j]] + rank[j];
+                    st_e[at] = e[j];
+                    st_f[at] = (uint16_t)f[j];
+                }
+            }
+            __syncthreads();
+            const uint32_t total = run.y - tb < (uint32_t)TILE_F ? run.y - tb : (uint32_t)TILE_F;
+            for (uint32_t x = threadIdx.x; x < total; x += blockDim.x) {
+                const uint32_t bn = st_f[x];
+                sorted[h[bn] + x - lofs[bn]] = st_e[x];
+            }
+            __syncthreads();
+            for (int q = threadIdx.x; q < NF; q += blockDim.x) {
+                h[q] += lh[q];
+                lh[q] = 0;
+            }
+            __syncthreads();
+        }
     }
 }
 
@@ -791,11 +877,15 @@ static void sort_group(MsmWork &wk, MsmGroup &gb, const uint32_t *keys, const Gr
 }
 
 // buckets of the group (XYZZ, R384) into gb.buckets
+// nent: entries (upper bound) in the sorted list; alg_bytes: SURVEY 8(d)
+// bytes credited to the launch (0: the group's points x 128 B per window)
 static void accumulate_group(MsmWork &wk, MsmGroup &gb, const GroupPlan &gp, const MsmCfg &g,
-                             const uint64_t *pts, const uint64_t *table, hipStream_t s) {
+                             const uint64_t *pts, const uint64_t *table, hipStream_t s, uint64_t nent = 0,
+                             double alg_bytes = 0) {
     const int nv = gp.nv;
     const uint64_t n = gp.kr.n, WB = (uint64_t)nv * g.NB;
-    const uint64_t nent = (uint64_t)nv * gp.kr.rows * n;
+    if (!nent) nent = (uint64_t)nv * gp.kr.rows * n;
+    if (alg_bytes == 0) alg_bytes = (double)n * 128.0 * nv * gp.kr.rows / g.W;
     auto need = [](DevBuf &b, size_t bytes) { if (b.bytes < bytes) b.alloc(bytes); };
     need(gb.buckets, (WB * 24 + WB * 72 + 64) * 8);  // buckets + reduction tree scratch
     const uint32_t *bstart = static_cast<const uint32_t *>(gb.offsets.p);
@@ -864,7 +954,7 @@ static void accumulate_group(MsmWork &wk, MsmGroup &gb, const GroupPlan &gp, con
     // algorithmic bytes: each point (96 B) and scalar (32 B)
     // once per window sweep
     if (wk.timer) {
-        wk.timer->end("msm_accumulate", s, ev0, (double)n * 128.0 * nv * gp.kr.rows / g.W);
+        wk.timer->end("msm_accumulate", s, ev0, alg_bytes);
         wk.timer->credit("msm_entries", (double)nent);  // ~ mixed additions (zero digits drop out)
     }
 }
@@ -905,15 +995,19 @@ static hipEvent_t ev_get(MsmWork &wk, int i) {
 // Optionally (PNP_MSM_PIPE) the batch is split into two groups (halves of the
 // MSMs, or of the windows when B = 1) pipelined over two streams: group 1's
 // sort beside group 0's accumulation, group 0's bucket tree beside group 1's.
+// n_table / id_base: a folded table built over n_table points of which this
+// call's points are [id_base, id_base + n) (bucket-range mode keeps the full
+// table; a point-range batch then indexes into it); 0 = the table is this range
 static void msm_local_batch(MsmWork &wk, const uint64_t *d_points, const uint64_t *const *d_scalars,
                             int B, uint64_t n, uint64_t *h_xyzz, hipStream_t s,
-                            const uint64_t *table) {
+                            const uint64_t *table, uint64_t n_table = 0, uint64_t id_base = 0) {
     if (n == 0 || B == 0) {
         for (int b = 0; b < B; b++) put_xyzz(Xyzz::inf(), h_xyzz + 24 * b);
         return;
     }
     const bool folded = table != nullptr;
-    const MsmCfg g = msm_cfg(n, folded ? wk.fold_c : 0, folded);
+    if (!n_table) n_table = n;
+    const MsmCfg g = msm_cfg(n_table, folded ? wk.fold_c : 0, folded);
     auto need = [](DevBuf &b, size_t bytes) { if (b.bytes < bytes) b.alloc(bytes); };
     need(wk.digits, (uint64_t)g.W * B * n * 4);
     uint32_t *keys = static_cast<uint32_t *>(wk.digits.p);
@@ -935,11 +1029,12 @@ static void msm_local_batch(MsmWork &wk, const uint64_t *d_points, const uint64_
         kr.vstride = 1, kr.off = 0, kr.rows = 1, kr.id_row0 = 0, kr.id_mul = 0;
         gp[0] = {kr, B * g.W};
     } else if (no_pipe) {
-        kr.vstride = g.W, kr.off = 0, kr.rows = g.W, kr.id_row0 = 0, kr.id_mul = n;
+        kr.vstride = g.W, kr.off = 0, kr.rows = g.W, kr.id_row0 = 0, kr.id_mul = n_table;
+        kr.id_base = id_base;
         gp[0] = {kr, B};
     } else if (B >= 2) {
         const int h = (B + 1) / 2;
-        kr.vstride = g.W, kr.off = 0, kr.rows = g.W, kr.id_row0 = 0, kr.id_mul = n;
+        kr.vstride = g.W, kr.off = 0, kr.rows = g.W, kr.id_row0 = 0, kr.id_mul = n_table, kr.id_base = id_base;
         gp[0] = {kr, h};
         kr.off = h * g.W;
         gp[1] = {kr, B - h};
@@ -947,13 +1042,13 @@ static void msm_local_batch(MsmWork &wk, const uint64_t *d_points, const uint64_
         ng = 2;
     } else if (g.W >= 2) {  // one MSM: split its windows
         const int h = g.W / 2;
-        kr.vstride = g.W, kr.off = 0, kr.rows = h, kr.id_row0 = 0, kr.id_mul = n;
+        kr.vstride = g.W, kr.off = 0, kr.rows = h, kr.id_row0 = 0, kr.id_mul = n_table, kr.id_base = id_base;
         gp[0] = {kr, 1};
         kr.off = h, kr.rows = g.W - h, kr.id_row0 = h;
         gp[1] = {kr, 1};
         ng = 2;
     } else {
-        kr.vstride = g.W, kr.off = 0, kr.rows = g.W, kr.id_row0 = 0, kr.id_mul = n;
+        kr.vstride = g.W, kr.off = 0, kr.rows = g.W, kr.id_row0 = 0, kr.id_mul = n_table, kr.id_base = id_base;
         gp[0] = {kr, 1};
     }
     const uint64_t *pts = folded ? table : d_points;
@@ -1022,6 +1117,217 @@ static void msm_local_batch(MsmWork &wk, const uint64_t *d_points, const uint64_
     }
 }
 
+// k * P on the host (double and add; k < 2^64)
+static Xyzz mul_small(const Xyzz &p, uint64_t k) {
+    Xyzz acc = Xyzz::inf();
+    for (int b = 63; b >= 0; b--) {
+        acc = dbl(acc);
+        if ((k >> b) & 1) acc = add(acc, p);
+    }
+    return acc;
+}
+
+// Bucket-range sharding of a folded batch (MsmWork::alltoallv): rank r owns
+// buckets [r NB/W, (r+1) NB/W) of every MSM.  It digitises its own points
+// [p0, p1) (scalars sc[b] already offset to them) and runs the usual pass A
+// with 512 coarse bins, whose top log2(W) bits are the owning rank, in
+// destination-major order (cidx), writing 8-byte records (entry | fine key <<
+// 32) straight into the send buffer: destination d's part is one run.  After
+// the all-to-all (bin counts first, then the records) every rank sorts its own
+// bins from the W received runs (k_fine_sort_runs), then accumulates, merges
+// and reduces only its NB/W buckets per MSM: 1/W of the bucket tail that the
+// point-range scheme repeats on every rank.  Its share of MSM b is
+// T_b + lo S_b (T: the local tree's weighted sum, S: the plain bucket sum,
+// lo = r NB/W: the weight offset of its buckets).  Returns false (nothing
+// exchanged; every rank reaches the same verdict from the all-gathered
+// counts) when the records would overflow the exchange buffers: the caller
+// then takes point ranges.
+static bool msm_bucket_batch(MsmWork &wk, const uint64_t *const *sc, int B, uint64_t n_full, uint64_t p0,
+                             uint64_t p1, uint64_t *part, hipStream_t s, const uint64_t *table) {
+    const int W = wk.world;
+    // Bucket ranges pay from 4 ranks on (solo-rank times per proof at n = 2^22,
+    // points vs buckets: 2 ranks 91.1 vs 94.0 ms, 4 ranks 56.0 vs 55.3, 8 ranks
+    // 37.5 vs 34.6, profiles/r03_solo): below that the extra exchange and sort
+    // cost more than the halved bucket tail saves.  PNP_MSM_BUCKETS_MIN_WORLD
+    // moves the threshold (tests cover 2 ranks with it).
+    static const int min_world = [] {
+        const char *e = getenv("PNP_MSM_BUCKETS_MIN_WORLD");
+        return e ? atoi(e) : 4;
+    }();
+    if (W < min_world) return false;
+    const MsmCfg g = msm_cfg(n_full, wk.fold_c, true);
+    int lgW = 0;
+    while ((1 << lgW) < W) lgW++;
+    const int cbits = std::min(SORT_CB, g.c - 1);  // coarse bits of the whole bucket index
+    if ((1 << lgW) != W || lgW >= cbits || g.c - 1 - cbits > SORT_FB_MAX) return false;
+    const int fb = g.c - 1 - cbits, NBc = 1 << cbits, nbl = NBc / W;  // nbl coarse bins per rank
+    const uint64_t NBloc = (uint64_t)g.NB / W, n = p1 - p0;
+    if (NBloc < 32) return false;
+    auto need = [](DevBuf &b, size_t bytes) { if (b.bytes < bytes) b.alloc(bytes); };
+    MsmGroup &gb = wk.grp[0];
+    // 1. digits of this rank's points
+    need(wk.digits, (uint64_t)g.W * B * std::max<uint64_t>(n, 1) * 4);
+    uint32_t *keys = static_cast<uint32_t *>(wk.digits.p);
+    for (int b = 0; b < B && n; b++) {
+        hipLaunchKernelGGL(k_digits, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, s, sc[b], n, g.c, g.W,
+                           keys + (uint64_t)b * g.W * n);
+        PNP_HIP(hipGetLastError());
+    }
+    // 2. pass A, destination-major (chunks as sort_group: ~512 workgroups)
+    KeyRows kr;
+    kr.n = n, kr.vstride = g.W, kr.off = 0, kr.rows = g.W, kr.id_row0 = 0, kr.id_mul = n_full, kr.id_base = p0;
+    const int nch0 = std::max(1, 512 / B);
+    const uint64_t chunk = std::max<uint64_t>(1024, (n + nch0 - 1) / nch0);
+    const int nch = (int)std::max<uint64_t>(1, (n + chunk - 1) / chunk);
+    const uint64_t ncount = (uint64_t)B * NBc * nch;
+    need(gb.counts, (ncount + 1) * 4);
+    uint32_t *counts = static_cast<uint32_t *>(gb.counts.p);
+    PNP_HIP(hipMemsetAsync(counts, 0, (ncount + 1) * 4, s));
+    const dim3 grid((uint32_t)nch, (uint32_t)B);
+    if (n) {
+        hipLaunchKernelGGL(k_coarse_hist, grid, dim3(1024), 0, s, keys, kr, fb, NBc, chunk, nch, counts, W);
+        PNP_HIP(hipGetLastError());
+    }
+    scan_u32(counts, ncount + 1, gb.scan_tmp, s);
+    std::vector<uint32_t> offs(ncount + 1);
+    PNP_HIP(hipMemcpyAsync(offs.data(), counts, (ncount + 1) * 4, hipMemcpyDeviceToHost, s));
+    PNP_HIP(hipStreamSynchronize(s));
+    // per destination: its bins' entry counts (B nbl words, bin (v, local) of
+    // destination d starts at offs[((d B + v) nbl + l) nch]) and its record bytes
+    const uint64_t per_d = (uint64_t)B * nbl;
+    auto bin_off = [&](uint64_t gbin) { return offs[gbin * nch]; };
+    std::vector<uint64_t> send_b(W + 1), recv_b(W);
+    for (int d = 0; d < W; d++) send_b[d] = 8ULL * (bin_off((d + 1) * per_d) - bin_off(d * per_d));
+    send_b[W] = 0xB0C4E7C0u;  // tag: a slot size and content no other exchange of the proof uses
+    // 3. every rank's totals (one all-gather of W + 1 words per rank): the
+    // receive sizes and the common overflow verdict
+    const uint64_t slot = 8ULL * (W + 1);
+    if (wk.xbuf_bytes < slot * W) {
+        set_error("msm bucket shard: exchange buffer %llu B < %llu B", (unsigned long long)wk.xbuf_bytes,
+                  (unsigned long long)(slot * W));
+        throw Error(PNP_E_ARG);
+    }
+    PNP_HIP(hipMemcpyAsync(wk.xbuf + (uint64_t)wk.rank * (W + 1), send_b.data(), slot, hipMemcpyHostToDevice, s));
+    PNP_HIP(hipStreamSynchronize(s));
+    if (int rc = wk.allgather(wk.user, slot)) {
+        set_error("msm bucket shard: count all-gather failed (%d)", rc);
+        throw Error(PNP_E_DEVICE);
+    }
+    std::vector<uint64_t> all((size_t)W * (W + 1));
+    PNP_HIP(hipMemcpyAsync(all.data(), wk.xbuf, all.size() * 8, hipMemcpyDeviceToHost, s));
+    PNP_HIP(hipStreamSynchronize(s));
+    auto cnt = [&](int from, int to) { return all[(size_t)from * (W + 1) + to]; };
+    const uint64_t bins_bytes = 4 * per_d * W;  // the bin-count exchange below
+    bool fits = bins_bytes <= wk.v_bytes;
+    for (int r = 0; r < W; r++) {
+        uint64_t out = 0, in = 0;
+        for (int d = 0; d < W; d++) {
+            out += cnt(r, d);
+            in += cnt(d, r);
+        }
+        fits &= out <= wk.v_bytes && in <= wk.v_bytes;
+    }
+    if (!fits) {
+        if (wk.timer) wk.timer->credit("msm_bucket_fallback", 1);
+        return false;
+    }
+    for (int r = 0; r < W; r++) recv_b[r] = cnt(r, wk.rank);
+    // 4. bin counts (u32, B nbl per destination), then the records
+    {
+        std::vector<uint32_t> bc((size_t)per_d * W);
+        for (uint64_t gbin = 0; gbin < per_d * W; gbin++) bc[gbin] = bin_off(gbin + 1) - bin_off(gbin);
+        PNP_HIP(hipMemcpyAsync(wk.v_send, bc.data(), bc.size() * 4, hipMemcpyHostToDevice, s));
+        PNP_HIP(hipStreamSynchronize(s));
+        std::vector<uint64_t> eq(W, 4 * per_d);
+        if (int rc = wk.alltoallv(wk.v_user, eq.data(), eq.data())) {
+            set_error("msm bucket shard: bin-count all-to-all failed (%d)", rc);
+            throw Error(PNP_E_DEVICE);
+        }
+    }
+    std::vector<uint32_t> rbc((size_t)per_d * W);  // [source][v][local bin]
+    PNP_HIP(hipMemcpyAsync(rbc.data(), wk.v_recv, rbc.size() * 4, hipMemcpyDeviceToHost, s));
+    if (n) {
+        hipLaunchKernelGGL(k_coarse_scatter, grid, dim3(1024), 0, s, keys, kr, fb, NBc, chunk, nch, counts,
+                           nullptr, nullptr, W, wk.v_send);
+        PNP_HIP(hipGetLastError());
+    }
+    PNP_HIP(hipStreamSynchronize(s));
+    if (int rc = wk.alltoallv(wk.v_user, send_b.data(), recv_b.data())) {
+        set_error("msm bucket shard: all-to-all failed (%d)", rc);
+        throw Error(PNP_E_DEVICE);
+    }
+    // 5. the W received runs of every bin (v, local coarse bin) and its output start
+    std::vector<uint32_t> runs(2 * per_d * W), out0(per_d + 1);
+    {
+        uint64_t base = 0;
+        for (int r = 0; r < W; r++) {
+            uint64_t at = base;
+            for (uint64_t p = 0; p < per_d; p++) {
+                const uint32_t c = rbc[(size_t)r * per_d + p];
+                runs[2 * (p * W + r)] = (uint32_t)at;
+                runs[2 * (p * W + r) + 1] = c;
+                at += c;
+            }
+            if (at - base != recv_b[r] / 8) {
+                set_error("msm bucket shard: rank %d sent %llu records, its bin counts say %llu", r,
+                          (unsigned long long)(recv_b[r] / 8), (unsigned long long)(at - base));
+                throw Error(PNP_E_DEVICE);
+            }
+            base = at;
+        }
+        uint64_t o = 0;
+        for (uint64_t p = 0; p < per_d; p++) {
+            out0[p] = (uint32_t)o;
+            for (int r = 0; r < W; r++) o += runs[2 * (p * W + r) + 1];
+        }
+        out0[per_d] = (uint32_t)o;
+    }
+    const uint64_t R = out0[per_d];
+    const uint64_t WB = (uint64_t)B * NBloc;
+    need(gb.offsets, (WB + 1) * 4);
+    need(gb.sorted, R * 4 + 4);
+    need(gb.ent, (runs.size() + out0.size()) * 4);  // run table + bin starts (ent is unused on this path)
+    uint32_t *bstart = static_cast<uint32_t *>(gb.offsets.p);
+    uint32_t *rt = static_cast<uint32_t *>(gb.ent.p), *o0 = rt + runs.size();
+    PNP_HIP(hipMemcpyAsync(rt, runs.data(), runs.size() * 4, hipMemcpyHostToDevice, s));
+    PNP_HIP(hipMemcpyAsync(o0, out0.data(), out0.size() * 4, hipMemcpyHostToDevice, s));
+    hipLaunchKernelGGL(k_fine_sort_runs, dim3((uint32_t)per_d), dim3(1024), 0, s, wk.v_recv,
+                       reinterpret_cast<const uint2 *>(rt), W, o0, fb, bstart, static_cast<uint32_t *>(gb.sorted.p));
+    PNP_HIP(hipGetLastError());
+    PNP_HIP(hipMemcpyAsync(bstart + WB, o0 + per_d, 4, hipMemcpyDeviceToDevice, s));
+    // 6. accumulate, merge and reduce this rank's buckets
+    MsmCfg gl = g;
+    gl.NB = (int)NBloc;
+    GroupPlan gp;
+    gp.kr = kr;
+    gp.nv = B;
+    std::vector<uint64_t> ts((size_t)B * 48);
+    for (int b = 0; b < 2 * B; b++) put_xyzz(Xyzz::inf(), &ts[24 * (size_t)b]);
+    if (R) {
+        accumulate_group(wk, gb, gp, gl, nullptr, table, s, R, (double)R * 128.0 / g.W);
+        const uint64_t *res = reduce_group(gb, gp, gl, s, true);
+        uint32_t exc = 0, nredo = 0;
+        PNP_HIP(hipMemcpyAsync(ts.data(), res, ts.size() * 8, hipMemcpyDeviceToHost, s));
+        PNP_HIP(hipMemcpyAsync(&exc, gb.exc.p, 4, hipMemcpyDeviceToHost, s));
+        PNP_HIP(hipMemcpyAsync(&nredo, gb.redo.p, 4, hipMemcpyDeviceToHost, s));
+        PNP_HIP(hipStreamSynchronize(s));
+        if (wk.timer) wk.timer->credit("msm_redo_lanes", (double)nredo);
+        if (exc) {
+            if (wk.timer) wk.timer->credit("msm_exact_fallback", 1);
+            res = reduce_group_exact(gb, gp, gl, s);
+            PNP_HIP(hipMemcpyAsync(ts.data(), res, ts.size() * 8, hipMemcpyDeviceToHost, s));
+            PNP_HIP(hipStreamSynchronize(s));
+        }
+        if (wk.timer) wk.timer->collect();
+    }
+    const uint64_t lo = (uint64_t)wk.rank * NBloc;
+    for (int b = 0; b < B; b++) {
+        const Xyzz T = get_xyzz(&ts[24 * (size_t)b]), S = get_xyzz(&ts[24 * ((size_t)B + b)]);
+        put_xyzz(lo ? add(T, mul_small(S, lo)) : T, part + 24 * (size_t)b);
+    }
+    return true;
+}
+
 void msm_point_range(uint64_t n, int rank, int world, uint64_t &p0, uint64_t &p1) {
     const uint64_t per = (n + world - 1) / world;
     p0 = std::min<uint64_t>((uint64_t)rank * per, n);
@@ -1043,7 +1349,11 @@ void msm_run_batch(MsmWork &wk, const uint64_t *d_points, const uint64_t *const 
     std::vector<const uint64_t *> sc(B);
     for (int b = 0; b < B; b++) sc[b] = scalars_local ? d_scalars[b] : d_scalars[b] + 4 * p0;
     std::vector<uint64_t> part((size_t)B * 24);
-    msm_local_batch(wk, d_points + 12 * p0, sc.data(), B, p1 - p0, part.data(), s, table);
+    // bucket ranges (the folded table covers all n points) or point ranges
+    const bool full = table && wk.full_table();
+    if (!(full && msm_bucket_batch(wk, sc.data(), B, n, p0, p1, part.data(), s, table)))
+        msm_local_batch(wk, d_points + 12 * p0, sc.data(), B, p1 - p0, part.data(), s, table, full ? n : 0,
+                        full ? p0 : 0);
     const uint64_t slot = (uint64_t)B * 24 * 8;
     if (wk.xbuf_bytes < slot * wk.world) {
         set_error("msm shard: exchange buffer %llu B < %llu B", (unsigned long long)wk.xbuf_bytes,

@@ -58,12 +58,13 @@ void msm_merge_pieces29_exact(const uint32_t *offs, uint64_t U, uint32_t S, uint
 
 // Sum_b (b+1) * B_b for each of `nwin` consecutive groups of NB XYZZ buckets
 // (bk[0 .. nwin*NB), NB a power of two); `scratch` must hold 72*nwin*NB u64.
-// Returns the device address of the nwin results (XYZZ, 24 u64 each).
+// Returns the device address of the nwin results (XYZZ, 24 u64 each),
+// followed by the nwin plain sums Sum_b B_b.
 
 const uint64_t *msm_reduce(const uint64_t *bk, uint64_t nwin, int NB, uint64_t *scratch,
                            hipStream_t s);
 // the same over radix-2^29 buckets (56 u32 each); `scratch` must hold
-// 126 * nwin * NB + 48 * nwin u32 (NB >= 4); results R384.  *exc is set when
+// 126 * nwin * NB + 96 * nwin u32 (NB >= 4); results R384 (T, then S).  *exc is set when
 // an addition met equal or opposite operands (never for random inputs): the
 // results are then wrong and the caller redoes the group with
 // msm_merge_pieces29_exact + msm_reduce (32-bit, exact)

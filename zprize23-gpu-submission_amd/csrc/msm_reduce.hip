@@ -312,10 +312,13 @@ __global__ __launch_bounds__(256) void k_tree_level29(const uint32_t *in, uint64
     store_xyzz29(out + 168 * t + 56 * c, r);
 }
 
-// the roots' T in R384 (the host's 24-u64 XYZZ)
+// the roots' T in R384 (the host's 24-u64 XYZZ), then their S (a window's
+// plain bucket sum: a bucket-range shard adds lo * S, msm.hip)
 __global__ void k_tree_roots29(const uint32_t *in, uint64_t n, uint64_t *out) {
     uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
-    if (t < n) store_xyzz(out + 24 * t, to32(load_xyzz29(in + 168 * t + 56)));
+    if (t >= n) return;
+    store_xyzz(out + 24 * t, to32(load_xyzz29(in + 168 * t + 56)));
+    store_xyzz(out + 24 * (n + t), to32(load_xyzz29(in + 168 * t)));
 }
 
 const uint64_t *msm_reduce29(const uint32_t *bk29, const uint32_t *offs, uint64_t nwin, int NB,
@@ -347,10 +350,12 @@ const uint64_t *msm_reduce29(const uint32_t *bk29, const uint32_t *offs, uint64_
 }
 
 // ---------------------------------------------------------------- tree
-// the roots' T, packed
+// the roots' T, packed, then their S
 __global__ void k_tree_roots(const uint64_t *in, uint64_t n, uint64_t *out) {
     uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
-    if (t < n) store_xyzz(out + 24 * t, load_xyzz(in + 72 * t + 24));
+    if (t >= n) return;
+    store_xyzz(out + 24 * t, load_xyzz(in + 72 * t + 24));
+    store_xyzz(out + 24 * (n + t), load_xyzz(in + 72 * t));
 }
 
 const uint64_t *msm_reduce(const uint64_t *bk, uint64_t nwin, int NB, uint64_t *scratch,

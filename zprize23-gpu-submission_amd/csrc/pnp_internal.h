@@ -148,6 +148,16 @@ struct MsmWork {
     void *a2a_user = nullptr;
     uint64_t *a2a = nullptr;
     uint64_t a2a_bytes = 0;
+    // variable all-to-all of the bucket-range sharded MSMs (pnp_set_exchange_v):
+    // rank s owns buckets [s NB/W, (s+1) NB/W) of every MSM, the entries travel
+    // to their bucket's owner; unset: point-range sharding
+    pnp_alltoallv_fn alltoallv = nullptr;
+    void *v_user = nullptr;
+    uint64_t *v_send = nullptr, *v_recv = nullptr;
+    uint64_t v_bytes = 0;
+    // the folded table covers ALL n points (bucket ranges gather any point)
+    bool full_table() const { return world > 1 && alltoallv != nullptr; }
+    DevBuf part_counts, rec_counts;  // bucket-range pass counts
 };
 // sum_i s_i P_i; scalars Montgomery Fr; result written to host as XYZZ Fq (4x6 u64)
 // `table` (optional): msm_build_table(d_points, n) — the folded layout

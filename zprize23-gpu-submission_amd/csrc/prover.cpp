@@ -619,10 +619,12 @@ int prove_impl(pnp_ctx *ctx, const CircuitC *cs, int device_ptrs, ProofC *out, c
                 PNP_HIP(hipStreamSynchronize(s));
                 for (int k = 0; k < 8; k++) nz[k] = k < npieces && ((bits >> k) & 1);
             }
-            if (dist) {  // a chunk is zero when it is zero on every rank
+            if (dist) {  // a chunk is zero when it is zero on every rank (own slot included)
                 std::vector<uint64_t> all = shard_allgather(ctx, nz, 8);
-                for (int k = 0; k < 8; k++)
+                for (int k = 0; k < 8; k++) {
+                    nz[k] = 0;
                     for (int r = 0; r < world; r++) nz[k] |= all[8 * r + k];
+                }
             }
             for (int k = 0; k < 8; k++) {
                 if (!nz[k]) {

@@ -34,13 +34,16 @@ SYMBOLS = ("gen_proof", "pnp_last_error", "pnp_ctx_create", "pnp_ctx_destroy",
            "pnp_sync", "pnp_ntt", "pnp_coset_lde8", "pnp_commit", "pnp_commit_ck", "pnp_poly_eval",
            "pnp_poly_div_linear", "pnp_prefix_product", "pnp_batch_inverse",
            "pnp_synth_random_fr", "pnp_synth_srs", "pnp_synth_coset_consts", "pnp_synth_circuit",
-           "pnp_synth_merkle", "pnp_load_commit_key_strided", "pnp_proof_infinity_mask")
+           "pnp_synth_merkle", "pnp_load_commit_key_strided", "pnp_proof_infinity_mask",
+           "pnp_set_exchange_v")
 
 
 # int allgather(void *user, uint64_t bytes_per_rank) — pnp_set_msm_shard
 ALLGATHER_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_uint64)
 # int alltoall(void *user, uint64_t bytes_per_peer) — pnp_set_exchange_a2a
 ALLTOALL_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_uint64)
+# int alltoallv(void *user, const uint64_t *send_bytes, const uint64_t *recv_bytes) — pnp_set_exchange_v
+ALLTOALLV_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64))
 
 
 class PnpError(RuntimeError):
@@ -81,6 +84,7 @@ def load(path: str = LIB_PATH):
     lib.pnp_kernel_bytes.argtypes = [vp, C.c_char_p, C.POINTER(C.c_double)]
     lib.pnp_set_msm_shard.argtypes = [vp, i32, i32, ALLGATHER_FN, vp, vp, u64]
     lib.pnp_set_exchange_a2a.argtypes = [vp, ALLTOALL_FN, vp, vp, u64]
+    lib.pnp_set_exchange_v.argtypes = [vp, ALLTOALLV_FN, vp, vp, vp, u64]
     lib.pnp_sync.argtypes = [vp]
     lib.pnp_ntt.argtypes = [vp, vp, C.c_uint32, i32, i32]
     lib.pnp_coset_lde8.argtypes = [vp, vp, vp, C.c_uint32]
@@ -199,6 +203,7 @@ class Context:
         if exchange is None or exchange.world == 1:
             check(self.lib.pnp_set_msm_shard(self.h, 0, 1, ALLGATHER_FN(), None, None, 0),
                   "pnp_set_msm_shard")
+            check(self.lib.pnp_set_exchange_v(self.h, ALLTOALLV_FN(), None, None, None, 0), "pnp_set_exchange_v")
             self._exchange = None
             return
         cb = exchange.c_callback()
@@ -211,6 +216,12 @@ class Context:
             check(self.lib.pnp_set_exchange_a2a(self.h, cb2, None, exchange.a2a.data_ptr(),
                                                 exchange.a2a.numel() * 8), "pnp_set_exchange_a2a")
             keep.append(cb2)
+        if getattr(exchange, "vsend", None) is not None:  # bucket-range MSMs
+            cb3 = exchange.c_alltoallv()
+            check(self.lib.pnp_set_exchange_v(self.h, cb3, None, exchange.vsend.data_ptr(),
+                                              exchange.vrecv.data_ptr(), exchange.vsend.numel() * 8),
+                  "pnp_set_exchange_v")
+            keep.append(cb3)
         self._exchange = keep  # keep the callbacks alive
 
     def kernel_stats(self, name: str):

@@ -16,7 +16,7 @@ RCCL (backend "nccl") runs both collectives on device buffers over xGMI; gloo
 """
 import ctypes as C
 
-from . import ALLGATHER_FN, ALLTOALL_FN
+from . import ALLGATHER_FN, ALLTOALL_FN, ALLTOALLV_FN
 
 
 class WindowExchange:
@@ -26,13 +26,17 @@ class WindowExchange:
     `a2a`: the all-to-all buffer, send slots then receive slots."""
 
     def __init__(self, rank: int, world: int, group=None, device=None,
-                 capacity_bytes: int = 1 << 20, a2a_bytes: int = 0):
+                 capacity_bytes: int = 1 << 20, a2a_bytes: int = 0, v_bytes: int = 0):
         import torch
         import torch.distributed as dist
         self.rank, self.world, self.group = rank, world, group
         self.buf = torch.zeros(capacity_bytes // 8, dtype=torch.int64, device=device)
         self.a2a = (torch.zeros(a2a_bytes // 8, dtype=torch.int64, device=device)
                     if a2a_bytes and world > 1 else None)
+        # bucket-range MSMs (pnp_set_exchange_v): send / receive record buffers
+        self.vsend = torch.empty(v_bytes // 8, dtype=torch.int64, device=device) if v_bytes and world > 1 else None
+        self.vrecv = torch.empty(v_bytes // 8, dtype=torch.int64, device=device) if v_bytes and world > 1 else None
+        self.v_calls = 0
         if self.buf.is_cuda:
             torch.cuda.synchronize()
         self.backend = dist.get_backend(group) if world > 1 else "none"
@@ -87,6 +91,38 @@ class WindowExchange:
                 torch.cuda.current_stream().synchronize()
         self.a2a_calls += 1
 
+    def alltoallv(self, send_bytes, recv_bytes) -> None:
+        """Segment s of `vsend` (send_bytes[s] bytes, back to back) goes to rank
+        s; what rank s sent lands at sum(recv_bytes[:s]) of `vrecv`."""
+        import torch
+        import torch.distributed as dist
+        ss = [int(b) // 8 for b in send_bytes]
+        rs = [int(b) // 8 for b in recv_bytes]
+        send = self.vsend[: sum(ss)]
+        recv = self.vrecv[: sum(rs)]
+        if self.vsend.is_cuda and self.backend == "nccl":
+            dist.all_to_all_single(recv, send, output_split_sizes=rs, input_split_sizes=ss, group=self.group)
+            torch.cuda.current_stream().synchronize()
+        else:
+            h_recv = torch.empty(sum(rs), dtype=torch.int64)
+            dist.all_to_all_single(h_recv, send.cpu(), output_split_sizes=rs, input_split_sizes=ss,
+                                   group=self.group)
+            recv.copy_(h_recv)
+            if self.vsend.is_cuda:
+                torch.cuda.current_stream().synchronize()
+        self.v_calls += 1
+
+    def c_alltoallv(self):
+        def cb(_user, send_bytes, recv_bytes):
+            try:
+                self.alltoallv([send_bytes[i] for i in range(self.world)],
+                               [recv_bytes[i] for i in range(self.world)])
+                return 0
+            except Exception as e:
+                self.error = e
+                return 1
+        return ALLTOALLV_FN(cb)
+
     def c_callback(self):
         def cb(_user, bytes_per_rank):
             try:
@@ -117,15 +153,17 @@ class SoloExchange(WindowExchange):
     critical path of the multi-GPU proof without the xGMI transfers, which
     the caller accounts for separately (`calls`, `bytes`)."""
 
-    def __init__(self, rank: int, world: int, device=None, a2a_bytes: int = 0):
+    def __init__(self, rank: int, world: int, device=None, a2a_bytes: int = 0, v_bytes: int = 0):
         import torch
         self.rank, self.world, self.group = rank, world, None
         self.buf = torch.zeros((1 << 20) // 8, dtype=torch.int64, device=device)
         self.a2a = torch.zeros(a2a_bytes // 8, dtype=torch.int64, device=device) if a2a_bytes else None
+        self.vsend = torch.empty(v_bytes // 8, dtype=torch.int64, device=device) if v_bytes else None
+        self.vrecv = torch.empty(v_bytes // 8, dtype=torch.int64, device=device) if v_bytes else None
         torch.cuda.synchronize()
         self.backend = "loopback"
-        self.calls = self.a2a_calls = 0
-        self.gather_bytes = self.a2a_bytes_moved = 0
+        self.calls = self.a2a_calls = self.v_calls = 0
+        self.gather_bytes = self.a2a_bytes_moved = self.v_bytes_moved = 0
         self.error = None
 
     # the 8-word exchange of the quotient chunks' non-zero flags (prover.cpp):
@@ -135,13 +173,24 @@ class SoloExchange(WindowExchange):
     # rank would, so the rank commits the same 6 chunks as in the real run
     T_FLAGS_BYTES = 64
 
+    # the bucket-range count exchange (msm.hip msm_bucket_batch): world counts
+    # + this tag word per rank
+    COUNT_TAG = 0xB0C4E7C0
+
     def gather(self, bytes_per_rank: int) -> None:
         import torch
         w = bytes_per_rank // 8
         mine = self.buf[self.rank * w:(self.rank + 1) * w].clone()
         if bytes_per_rank == self.T_FLAGS_BYTES:
             mine[6:8] = 0
-        self.buf[: w * self.world].view(self.world, w).copy_(mine.expand(self.world, w))
+        slots = self.buf[: w * self.world].view(self.world, w)
+        slots.copy_(mine.expand(self.world, w))
+        if w == self.world + 1 and int(mine[-1]) == self.COUNT_TAG:
+            # bucket-range counts: "rank s" sends this rank what this rank sends
+            # rank s (alltoallv below returns those segments), so this rank
+            # accumulates as many distinct entries as a real rank, spread over
+            # its bucket range like a real rank's
+            slots[:, self.rank] = mine[: self.world]
         torch.cuda.current_stream().synchronize()
         self.calls += 1
         self.gather_bytes += bytes_per_rank * self.world
@@ -153,6 +202,33 @@ class SoloExchange(WindowExchange):
         torch.cuda.current_stream().synchronize()
         self.a2a_calls += 1
         self.a2a_bytes_moved += bytes_per_peer * (self.world - 1)
+
+    def alltoallv(self, send_bytes, recv_bytes) -> None:
+        """Loopback: receive segment s = this rank's send segment s (the count
+        exchange above made the sizes agree): distinct entries of this rank's
+        points, bucket indices within a range, as many as a real rank gets."""
+        import torch
+        ss = [int(b) // 8 for b in send_bytes]
+        rs = [int(b) // 8 for b in recv_bytes]
+        assert rs == ss, (rs, ss)
+        n = sum(ss)
+        self.vrecv[:n].copy_(self.vsend[:n])
+        torch.cuda.current_stream().synchronize()
+        self.v_calls += 1
+        self.v_bytes_moved += sum(send_bytes) - send_bytes[self.rank]
+
+
+def v_bytes_for(lg_n: int, world: int, max_batch: int = 8, slack: float = 2.0) -> int:
+    """Capacity of each bucket-range record buffer (pnp_set_exchange_v): the
+    8-byte entries of the largest batch (max_batch MSMs x windows x points)
+    a rank sends or receives, with `slack` for uneven bucket ranges (a batch
+    that still overflows falls back to point ranges)."""
+    if world <= 1:
+        return 0
+    c = 20 if lg_n >= 19 else max(4, lg_n - 3)  # msm_cfg, folded layout
+    windows = (256 + c - 1) // c
+    per_rank = -(-(1 << lg_n) // world)
+    return int(slack * max_batch * windows * per_rank) * 8
 
 
 def a2a_bytes_for(lg_n: int, world: int) -> int:
