@@ -1117,10 +1117,12 @@ static void msm_local_batch(MsmWork &wk, const uint64_t *d_points, const uint64_
     }
 }
 
-// k * P on the host (double and add; k < 2^64)
+// k * P on the host (double and add from k's top bit: the bucket-range weight
+// offsets are < 2^19, ~20 doublings, a few microseconds each in host Fq)
 static Xyzz mul_small(const Xyzz &p, uint64_t k) {
     Xyzz acc = Xyzz::inf();
-    for (int b = 63; b >= 0; b--) {
+    if (!k) return acc;
+    for (int b = 63 - __builtin_clzll(k); b >= 0; b--) {
         acc = dbl(acc);
         if ((k >> b) & 1) acc = add(acc, p);
     }

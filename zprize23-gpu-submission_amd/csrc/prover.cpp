@@ -666,18 +666,38 @@ int prove_impl(pnp_ctx *ctx, const CircuitC *cs, int device_ptrs, ProofC *out, c
         ProofEvaluationsC *ev = &out->evaluations;
         {
             // evaluations at z
-            const uint64_t *pz[12] = {wpoly[0], wpoly[1], wpoly[2], wpoly[3], pk.left_sigma_coeffs,
-                                      pk.right_sigma_coeffs, pk.out_sigma_coeffs, pk.q_arith_coeffs,
-                                      pk.q_c_coeffs, pk.q_l_coeffs, pk.q_r_coeffs, pk.q_hl_coeffs};
+            // (distributed: every rank evaluates its coefficient range [q0, q0 + len)
+            // of these replicated polynomials, scales by x^q0, and one all-gather
+            // of the 18 partial values sums them)
+            const uint64_t eo = 4 * q0;
+            const uint64_t *pz[12] = {wpoly[0] + eo, wpoly[1] + eo, wpoly[2] + eo, wpoly[3] + eo,
+                                      pk.left_sigma_coeffs + eo, pk.right_sigma_coeffs + eo,
+                                      pk.out_sigma_coeffs + eo, pk.q_arith_coeffs + eo, pk.q_c_coeffs + eo,
+                                      pk.q_l_coeffs + eo, pk.q_r_coeffs + eo, pk.q_hl_coeffs + eo};
             Fr rz[12];
-            k_poly_eval_multi(pz, 12, n, zc, ctx->scratch_a, rz, s);
-            const uint64_t *pz2[2] = {pk.q_hr_coeffs, pk.q_h4_coeffs};
+            k_poly_eval_multi(pz, 12, len, zc, ctx->scratch_a, rz, s);
+            const uint64_t *pz2[2] = {pk.q_hr_coeffs + eo, pk.q_h4_coeffs + eo};
             Fr rz2[2];
-            k_poly_eval_multi(pz2, 2, n, zc, ctx->scratch_a, rz2, s);
+            k_poly_eval_multi(pz2, 2, len, zc, ctx->scratch_a, rz2, s);
             // evaluations at z * omega
-            const uint64_t *pw[4] = {z_poly, wpoly[0], wpoly[1], wpoly[3]};
+            const uint64_t *pw[4] = {z_poly + eo, wpoly[0] + eo, wpoly[1] + eo, wpoly[3] + eo};
             Fr rw[4];
-            k_poly_eval_multi(pw, 4, n, zw, ctx->scratch_a, rw, s);
+            k_poly_eval_multi(pw, 4, len, zw, ctx->scratch_a, rw, s);
+            if (dist) {
+                Fr *vals[18];
+                for (int k = 0; k < 12; k++) vals[k] = &rz[k];
+                vals[12] = &rz2[0], vals[13] = &rz2[1];
+                for (int k = 0; k < 4; k++) vals[14 + k] = &rw[k];
+                const Fr sz = pow_u64(zc, q0), sw = pow_u64(zw, q0);
+                uint64_t mine[4 * 18];
+                for (int k = 0; k < 18; k++) to_u64_limbs(*vals[k] * (k < 14 ? sz : sw), mine + 4 * k);
+                std::vector<uint64_t> all = shard_allgather(ctx, mine, 4 * 18);
+                for (int k = 0; k < 18; k++) {
+                    Fr acc = Fr::zero();
+                    for (int r = 0; r < world; r++) acc += from_u64_limbs<FrP>(&all[4 * (18 * r + k)]);
+                    *vals[k] = acc;
+                }
+            }
             Fr z2n = Fr::one();
             if (!z2_one) k_poly_eval(z2_poly, n, zw, ctx->scratch_a, &z2n, s);
             Fr f_eval = Fr::zero(), t_eval = Fr::zero(), t_next = Fr::zero();
