@@ -2,7 +2,7 @@
 
 Every comparison is bit-exact on Montgomery limbs / affine coordinates.
 Sizes reach BASELINE config 2 (NTT 2^20) and MSM 2^16 here; the full 2^22
-MSM is exercised by tests/test_gpu_prove.py via gen_proof properties.
+MSM is compared with the oracle directly in tests/test_gpu_full.py.
 """
 import ctypes as C
 import os

@@ -2,7 +2,7 @@
 # PMC passes over one bench proof (one counter group per run, no tracing
 # domains): FETCH_SIZE, WRITE_SIZE, SQ issue/wait breakdown.  Run on the GPU
 # box from the repo root:  bash tools/pmc_run.sh <tag>
-set -e
+set -e -o pipefail
 R=$(pwd)
 TAG=${1:-pmc}
 RX='k_accumulate29|k_ntt_pass|k_quotient|k_coarse_scatter|k_fine_sort|k_tree_level|k_t_combine'
