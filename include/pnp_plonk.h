@@ -371,6 +371,16 @@ int pnp_commit(pnp_ctx *ctx, const uint64_t *d_points, const uint64_t *d_scalars
  * first n SRS points, built on the first call for this n and kept).  */
 int pnp_commit_ck(pnp_ctx *ctx, const uint64_t *d_scalars, uint64_t n, CommitmentC *out);
 
+/* Extension (no reference counterpart; what gen_proof's round 1 uses): the
+ * KZG commitment of the polynomial given by its n evaluations on the order-n
+ * subgroup <omega> (natural order, Montgomery) — the same point as
+ * pnp_commit_ck over its coefficients iNTT(evals), computed as
+ * sum_i evals_i [L_i(tau)] G against the resident commit key in the Lagrange
+ * basis (derived from the first n SRS points on the first call for this n and
+ * kept; zero evaluations cost nothing).  n a power of two <= the key's points.
+ * PNP_E_ARG when the basis is unavailable (PNP_LAGRANGE=0, degenerate key).  */
+int pnp_commit_evals(pnp_ctx *ctx, const uint64_t *d_evals, uint64_t n, CommitmentC *out);
+
 /* evaluate (function.cu:162-173): sum_i c_i x^i; x and result Montgomery,
  * host-side scalars.  Synchronous. */
 int pnp_poly_eval(pnp_ctx *ctx, const uint64_t *d_coeffs, uint64_t n,

@@ -126,7 +126,11 @@ def oracle():
 
 
 def vp(a: np.ndarray):
-    return C.c_void_p(a.ctypes.data)
+    """Pointer to a's data that keeps a alive for as long as the pointer
+    (vp(x.copy()) would otherwise hand C a freed temporary)."""
+    p = C.c_void_p(a.ctypes.data)
+    p._keep = a
+    return p
 
 
 # ------------------------------------------------------------------ synthetic inputs

@@ -54,6 +54,62 @@ const uint64_t *commit_table(pnp_ctx *ctx, uint64_t n) {
     return ctx->ck_table.u64();
 }
 
+void ck_derived_reset(pnp_ctx *ctx) {
+    ctx->ck_table_n = 0;
+    ctx->ck_table.release();
+    ctx->lag_n = 0;
+    ctx->lag_ok = false;
+    ctx->lag_points.release();
+    ctx->lag_table_n = 0;
+    ctx->lag_table.release();
+}
+
+const uint64_t *lagrange_table(pnp_ctx *ctx, uint64_t n) {
+    static const bool enabled = [] {
+        const char *e = getenv("PNP_LAGRANGE");
+        return !e || atoi(e) != 0;
+    }();
+    if (!enabled || n < 2 || (n & (n - 1)) || n > ctx->ck_points) return nullptr;
+    if (ctx->lag_n != n) {
+        ctx->lag_table_n = 0;
+        ctx->lag_table.release();
+        ctx->lag_points.alloc(n * 96);
+        uint32_t lg = 0;
+        while ((1ULL << lg) < n) lg++;
+        ctx->lag_ok = srs_lagrange(ctx->ck_dev, n, inverse(root_of_unity(lg)), inverse(fr_from_u64(n)),
+                                   ctx->lag_points.u64(), ctx->stream);
+        ctx->lag_n = n;
+        if (!ctx->lag_ok) ctx->lag_points.release();
+    }
+    if (!ctx->lag_ok) return nullptr;
+    uint64_t p0 = 0, p1 = n;
+    if (!ctx->msm.full_table()) msm_point_range(n, ctx->msm.rank, ctx->msm.world, p0, p1);
+    if (ctx->lag_table_n != n || ctx->lag_table_p0 != p0 || ctx->lag_table_p1 != p1) {
+        ctx->lag_table_n = 0;
+        msm_build_table(ctx->lag_table, ctx->lag_points.u64() + 12 * p0, p1 - p0, ctx->msm.fold_c, ctx->stream);
+        ctx->lag_table_n = n;
+        ctx->lag_table_p0 = p0;
+        ctx->lag_table_p1 = p1;
+    }
+    return ctx->lag_table.u64();
+}
+
+void commit_evals_batch(pnp_ctx *ctx, const uint64_t *const *d_evals, int B, uint64_t n, CommitmentC *const *out) {
+    const uint64_t *table = lagrange_table(ctx, n);
+    if (!table) {
+        set_error("commit from evaluations: no Lagrange-basis key of size %llu", (unsigned long long)n);
+        throw Error(PNP_E_ARG);
+    }
+    std::vector<uint64_t> xyzz((size_t)B * 24);
+    msm_run_batch(ctx->msm, ctx->lag_points.u64(), d_evals, B, n, xyzz.data(), ctx->stream, table, false);
+    std::vector<uint64_t> aff((size_t)B * 12);
+    xyzz_to_affine_batch_host(xyzz.data(), B, aff.data());
+    for (int b = 0; b < B; b++) {
+        memcpy(out[b]->x, &aff[12 * b], 48);
+        memcpy(out[b]->y, &aff[12 * b + 6], 48);
+    }
+}
+
 void commit_affine(pnp_ctx *ctx, const uint64_t *d_scalars, uint64_t n, CommitmentC *out) {
     uint64_t xyzz[24], aff[12];
     msm_run(ctx->msm, ctx->ck_dev, d_scalars, n, xyzz, ctx->stream, commit_table(ctx, n));
@@ -235,8 +291,11 @@ int pnp_set_exchange_v(pnp_ctx *ctx, pnp_alltoallv_fn alltoallv, void *user, uin
     ctx->msm.v_send = alltoallv ? d_send : nullptr;
     ctx->msm.v_recv = alltoallv ? d_recv : nullptr;
     ctx->msm.v_bytes = alltoallv ? capacity_bytes : 0;
-    ctx->ck_table_n = 0;  // the folded table's point range changes
+    // the folded tables' point ranges change (the Lagrange points stay)
+    ctx->ck_table_n = 0;
     ctx->ck_table.release();
+    ctx->lag_table_n = 0;
+    ctx->lag_table.release();
     return PNP_OK;
 }
 
@@ -278,6 +337,24 @@ int pnp_commit_ck(pnp_ctx *ctx, const uint64_t *d_scalars, uint64_t n, Commitmen
         return PNP_E_ARG;
     }
     PNP_TRY(commit_affine(ctx, d_scalars, n, out));
+}
+
+int pnp_commit_evals(pnp_ctx *ctx, const uint64_t *d_evals, uint64_t n, CommitmentC *out) {
+    if (!ctx || !out || !d_evals) return PNP_E_ARG;
+    if (!ctx->ck_loaded) {
+        set_error("commit key not loaded");
+        return PNP_E_NOKEY;
+    }
+    if (n < 2 || (n & (n - 1)) || n > ctx->ck_points) {
+        set_error("commit from evaluations: n = %llu must be a power of two <= %llu", (unsigned long long)n,
+                  (unsigned long long)ctx->ck_points);
+        return PNP_E_ARG;
+    }
+    PNP_TRY({
+        CommitmentC *o[1] = {out};
+        const uint64_t *e[1] = {d_evals};
+        commit_evals_batch(ctx, e, 1, n, o);
+    });
 }
 
 int pnp_poly_eval(pnp_ctx *ctx, const uint64_t *d, uint64_t n, const uint64_t x[4], uint64_t out[4]) {
@@ -531,8 +608,7 @@ void adopt_ck(pnp_ctx *ctx, pnp::DevBuf &up, uint64_t n_points) {
     if (!same) {
         std::swap(ctx->ck_owned, up);
         ctx->ck_dev = ctx->ck_owned.u64();
-        ctx->ck_table_n = 0;  // rebuilt from the new key on the next commitment
-        ctx->ck_table.release();
+        pnp::ck_derived_reset(ctx);  // rebuilt from the new key on the next commitment
     }
     ctx->ck_points = n_points;
     ctx->ck_loaded = true;
@@ -551,8 +627,7 @@ int pnp_load_commit_key(pnp_ctx *ctx, const CommitKeyC *ck, uint64_t n_points, i
             ctx->ck_owned.release();
             ctx->ck_dev = ck->powers_of_g;
             ctx->ck_points = n_points;
-            ctx->ck_table_n = 0;
-            ctx->ck_table.release();
+            pnp::ck_derived_reset(ctx);
             ctx->ck_loaded = true;
         } else {
             // upload (as the reference does per call, load.cu:348-358)

@@ -50,6 +50,13 @@ struct pnp_ctx {
     // built on the first commitment of that size
     pnp::DevBuf ck_table;
     uint64_t ck_table_n = 0, ck_table_p0 = 0, ck_table_p1 = 0;
+    // the first lag_n SRS points in the Lagrange basis of the order-lag_n
+    // subgroup (srs_lagrange, affine) and their folded table: witness
+    // polynomials are committed from their evaluations (lagrange.hip); built
+    // on the first commitment of that size; lag_ok = false: degenerate key
+    pnp::DevBuf lag_points, lag_table;
+    uint64_t lag_n = 0, lag_table_n = 0, lag_table_p0 = 0, lag_table_p1 = 0;
+    bool lag_ok = false;
 
     // ---- per-proof working set (sized on first use, reused) ----
     std::map<std::string, pnp::DevBuf> work;
@@ -62,8 +69,20 @@ struct pnp_ctx {
 };
 
 namespace pnp {
+Fr root_of_unity(uint32_t lg);
+Fr fr_from_u64(uint64_t x);
+// drop everything derived from the resident SRS (folded tables, Lagrange basis)
+void ck_derived_reset(pnp_ctx *ctx);
 // commitments over the resident SRS (folded MSM)
 const uint64_t *commit_table(pnp_ctx *ctx, uint64_t n);
+// the folded table of the Lagrange-basis SRS of size n (this rank's point
+// range), nullptr when it is unavailable (PNP_LAGRANGE=0, n not a power of
+// two or above the key, degenerate key)
+const uint64_t *lagrange_table(pnp_ctx *ctx, uint64_t n);
+// B commitments of polynomials given by their n evaluations on the order-n
+// subgroup (Montgomery Fr, natural order): sum_i e_i L_i; requires
+// lagrange_table(ctx, n) != nullptr
+void commit_evals_batch(pnp_ctx *ctx, const uint64_t *const *d_evals, int B, uint64_t n, CommitmentC *const *out);
 void commit_affine(pnp_ctx *ctx, const uint64_t *d_scalars, uint64_t n, CommitmentC *out);
 // B commitments over the resident SRS in one batched MSM
 // local: on a multi-GPU run the scalars hold only this rank's point range

@@ -810,6 +810,16 @@ void msm_build_table(DevBuf &tab, const uint64_t *d_points, uint64_t n, int c, h
     PNP_HIP(hipStreamSynchronize(s));
 }
 
+void xyzz_to_affine_dev(const uint64_t *xyzz, uint64_t n, uint64_t *aff, hipStream_t s) {
+    const uint32_t CH = 64;
+    const uint64_t lanes = (n + CH - 1) / CH;
+    DevBuf pre(n * 48);
+    hipLaunchKernelGGL(k_table_affine, dim3((uint32_t)((lanes + 255) / 256)), dim3(256), 0, s, xyzz, n, CH,
+                       pre.u64(), aff);
+    PNP_HIP(hipGetLastError());
+    PNP_HIP(hipStreamSynchronize(s));
+}
+
 // ---------------------------------------------------------------- driver
 static void put_xyzz(const Xyzz &r, uint64_t *o) {
     to_u64_limbs(r.x, o);

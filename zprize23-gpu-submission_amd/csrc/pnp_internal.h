@@ -172,6 +172,14 @@ void msm_point_range(uint64_t n, int rank, int world, uint64_t &p0, uint64_t &p1
 // T[k*n + i] = 2^(c*k) P_i, k < W (msm_cfg(n)), affine, in the radix-2^29
 // form of field29.cuh (x, y: 14 u32 each, padded to 128 B per point)
 void msm_build_table(DevBuf &tab, const uint64_t *d_points, uint64_t n, int c, hipStream_t s);
+// n device XYZZ points (24 u64) -> affine (12 u64; infinity -> (0, 0)), synchronous
+void xyzz_to_affine_dev(const uint64_t *xyzz, uint64_t n, uint64_t *aff, hipStream_t s);
+// the first n (a power of two) commit-key points d_aff (affine, 12 u64 each) in
+// the Lagrange basis of the order-n subgroup (lagrange.hip): d_out[i] =
+// n_inv sum_j omega_inv^(i j) d_aff[j]; false when the key is degenerate
+// (an output at infinity or an exceptional addition); synchronous
+bool srs_lagrange(const uint64_t *d_aff, uint64_t n, const Fr &omega_inv, const Fr &n_inv, uint64_t *d_out,
+                  hipStream_t s);
 // host: XYZZ -> affine Montgomery (inf -> (0, one))
 void xyzz_to_affine_host(const uint64_t *xyzz, uint64_t *aff12);
 // B points (24 u64 each) -> B affine (12 u64 each), one inversion

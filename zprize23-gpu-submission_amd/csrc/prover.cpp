@@ -35,6 +35,19 @@
 
 namespace pnp {
 
+Fr fr_from_u64(uint64_t x) {
+    Fr r = Fr::zero();
+    r.v[0] = (uint32_t)x;
+    r.v[1] = (uint32_t)(x >> 32);
+    return to_mont(r);
+}
+
+Fr root_of_unity(uint32_t lg) {
+    const uint64_t root32[4] = {13381757501831005802ULL, 6564924994866501612ULL,
+                                789602057691799140ULL, 6625830629041353339ULL};
+    return pow_u64(from_u64_limbs<FrP>(root32), 1ULL << (32 - lg));
+}
+
 namespace {
 
 struct Timer {
@@ -48,19 +61,6 @@ struct Timer {
         t0 = t1;
     }
 };
-
-Fr fr_from_u64(uint64_t x) {
-    Fr r = Fr::zero();
-    r.v[0] = (uint32_t)x;
-    r.v[1] = (uint32_t)(x >> 32);
-    return to_mont(r);
-}
-
-Fr root_of_unity(uint32_t lg) {
-    const uint64_t root32[4] = {13381757501831005802ULL, 6564924994866501612ULL,
-                                789602057691799140ULL, 6625830629041353339ULL};
-    return pow_u64(from_u64_limbs<FrP>(root32), 1ULL << (32 - lg));
-}
 
 void append_comm(Transcript &t, const char *label, const CommitmentC &c) {
     t.append_point(label, c.x, c.y);
@@ -260,7 +260,12 @@ int prove_impl(pnp_ctx *ctx, const CircuitC *cs, int device_ptrs, ProofC *out, c
     for (int j = 0; j < 4; j++) lde_on(s_lo, wpoly[j], w8buf[j]);
     if (overlap) PNP_HIP(hipEventRecord(ctx->ev_w8, s_lo));
     CommitmentC *wc[4] = {&out->a_comm, &out->b_comm, &out->c_comm, &out->d_comm};
-    {
+    if (lagrange_table(ctx, n)) {
+        // from the padded evaluations over the Lagrange-basis key: the same
+        // commitments, the zero rows drop out of the MSM (lagrange.hip)
+        const uint64_t *sc[4] = {wsc[0], wsc[1], wsc[2], wsc[3]};
+        commit_evals_batch(ctx, sc, 4, n, wc);
+    } else {
         const uint64_t *sc[4] = {wpoly[0], wpoly[1], wpoly[2], wpoly[3]};
         commit_affine_batch(ctx, sc, 4, n, wc);
     }

@@ -31,7 +31,7 @@ SYMBOLS = ("gen_proof", "pnp_last_error", "pnp_ctx_create", "pnp_ctx_destroy",
            "pnp_last_stage_times",
            "pnp_kernel_timing", "pnp_kernel_stats", "pnp_kernel_bytes", "pnp_set_msm_shard",
            "pnp_set_exchange_a2a",
-           "pnp_sync", "pnp_ntt", "pnp_coset_lde8", "pnp_commit", "pnp_commit_ck", "pnp_poly_eval",
+           "pnp_sync", "pnp_ntt", "pnp_coset_lde8", "pnp_commit", "pnp_commit_ck", "pnp_commit_evals", "pnp_poly_eval",
            "pnp_poly_div_linear", "pnp_prefix_product", "pnp_batch_inverse",
            "pnp_synth_random_fr", "pnp_synth_srs", "pnp_synth_coset_consts", "pnp_synth_circuit",
            "pnp_synth_merkle", "pnp_load_commit_key_strided", "pnp_proof_infinity_mask",
@@ -90,6 +90,7 @@ def load(path: str = LIB_PATH):
     lib.pnp_coset_lde8.argtypes = [vp, vp, vp, C.c_uint32]
     lib.pnp_commit.argtypes = [vp, vp, vp, u64, C.POINTER(abi.CommitmentC)]
     lib.pnp_commit_ck.argtypes = [vp, vp, u64, C.POINTER(abi.CommitmentC)]
+    lib.pnp_commit_evals.argtypes = [vp, vp, u64, C.POINTER(abi.CommitmentC)]
     lib.pnp_poly_eval.argtypes = [vp, vp, u64, vp, vp]
     lib.pnp_poly_div_linear.argtypes = [vp, vp, u64, vp]
     lib.pnp_prefix_product.argtypes = [vp, vp, u64]
@@ -250,6 +251,13 @@ class Context:
         """Commitment against the resident commit key (folded fixed-base MSM)."""
         out = abi.CommitmentC()
         check(self.lib.pnp_commit_ck(self.h, C.c_void_p(scalars), n, C.byref(out)), "pnp_commit_ck")
+        return out
+
+    def commit_evals(self, evals: int, n: int) -> abi.CommitmentC:
+        """Commitment of the polynomial with these n evaluations on the order-n
+        subgroup, against the resident key in the Lagrange basis."""
+        out = abi.CommitmentC()
+        check(self.lib.pnp_commit_evals(self.h, C.c_void_p(evals), n, C.byref(out)), "pnp_commit_evals")
         return out
 
     def poly_eval(self, addr: int, n: int, x_limbs):
