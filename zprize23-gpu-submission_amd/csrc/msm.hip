@@ -1034,7 +1034,12 @@ static void msm_local_batch(MsmWork &wk, const uint64_t *d_points, const uint64_
     // Two-stream pipelining measured 3% SLOWER per proof on MI355X (the sort
     // and tree kernels steal issue slots from the VALU-bound accumulation and
     // slow down themselves): one group unless PNP_MSM_PIPE=1 (experiments).
-    static const bool no_pipe = getenv("PNP_MSM_PIPE") == nullptr;
+    // PNP_MSM_PIPE=B: pipeline batches of at least B MSMs only (experiments)
+    static const int pipe_min_b = [] {
+        const char *e = getenv("PNP_MSM_PIPE");
+        return e ? std::max(1, atoi(e)) : 0;
+    }();
+    const bool no_pipe = pipe_min_b == 0 || B < pipe_min_b;
     if (!folded) {
         kr.vstride = 1, kr.off = 0, kr.rows = 1, kr.id_row0 = 0, kr.id_mul = 0;
         gp[0] = {kr, B * g.W};
