@@ -727,9 +727,10 @@ namespace {
 // HEIGHT=15), so a caller may rewrite its key buffers in place between calls.
 // The v1 symbol keeps that contract by default: every call uploads the whole
 // prover key and commit key (pnp_load_*), and the proof reads only what this
-// call uploaded.  The one expensive derived object, the folded MSM table of
-// the SRS, is kept when the uploaded SRS equals the resident one byte for byte
-// (compared on the device, pnp_load_commit_key).
+// call uploaded.  The expensive objects derived from the SRS (the folded MSM
+// tables, the Lagrange basis of lagrange.hip) are kept when the uploaded SRS
+// equals the resident one byte for byte (compared on the device,
+// pnp_load_commit_key).
 // PNP_V1_REUSE=1 (opt-in, for callers that never mutate their keys, like
 // merkle-tree's main.rs and pnp_bench.rs): the resident copy made by an
 // earlier call is reused while the key's fingerprint (every field pointer, the

@@ -252,20 +252,29 @@ int prove_impl(pnp_ctx *ctx, const CircuitC *cs, int device_ptrs, ProofC *out, c
     }
 
     // ---------------- round 1: witness polynomials (gen_proof.cuh:25-50)
-    for (int j = 0; j < 4; j++) ntt_run(nt, wpoly[j], lg, true, false, s, wsc[j]);
-    tm.mark("r1_intt");
+    // With the Lagrange-basis key the commitments are taken from the padded
+    // evaluations (the same points; zero rows drop out of the MSM,
+    // lagrange.hip), and the coefficients feed only the round-4 LDEs and
+    // round 5: the wires' iNTTs move to the side stream with the LDEs, off
+    // the commitments' path.
+    const bool lag = lagrange_table(ctx, n) != nullptr;
     uint64_t *w8buf[4];
     for (int j = 0; j < 4; j++) w8buf[j] = ctx->buf("w8_" + std::to_string(j), NB);
-    fork();
-    for (int j = 0; j < 4; j++) lde_on(s_lo, wpoly[j], w8buf[j]);
-    if (overlap) PNP_HIP(hipEventRecord(ctx->ev_w8, s_lo));
     CommitmentC *wc[4] = {&out->a_comm, &out->b_comm, &out->c_comm, &out->d_comm};
-    if (lagrange_table(ctx, n)) {
-        // from the padded evaluations over the Lagrange-basis key: the same
-        // commitments, the zero rows drop out of the MSM (lagrange.hip)
+    if (lag) {
+        fork();
+        for (int j = 0; j < 4; j++) ntt_run(nt, wpoly[j], lg, true, false, s_lo, wsc[j]);
+        for (int j = 0; j < 4; j++) lde_on(s_lo, wpoly[j], w8buf[j]);
+        if (overlap) PNP_HIP(hipEventRecord(ctx->ev_w8, s_lo));
+        tm.mark("r1_intt");
         const uint64_t *sc[4] = {wsc[0], wsc[1], wsc[2], wsc[3]};
         commit_evals_batch(ctx, sc, 4, n, wc);
     } else {
+        for (int j = 0; j < 4; j++) ntt_run(nt, wpoly[j], lg, true, false, s, wsc[j]);
+        tm.mark("r1_intt");
+        fork();
+        for (int j = 0; j < 4; j++) lde_on(s_lo, wpoly[j], w8buf[j]);
+        if (overlap) PNP_HIP(hipEventRecord(ctx->ev_w8, s_lo));
         const uint64_t *sc[4] = {wpoly[0], wpoly[1], wpoly[2], wpoly[3]};
         commit_affine_batch(ctx, sc, 4, n, wc);
     }
@@ -362,13 +371,24 @@ int prove_impl(pnp_ctx *ctx, const CircuitC *cs, int device_ptrs, ProofC *out, c
     k_batch_inverse(den, n, ctx->scratch_a, s);
     k_mul_inplace(num, den, n, s);
     k_prefix_product(num, n, ctx->scratch_a, s);
-    ntt_run(nt, z_poly, lg, true, false, s, num);
-    tm.mark("r3_z");
     uint64_t *z8 = ctx->buf("z8", NB);
-    fork();
-    lde_on(s_lo, z_poly, z8);
-    if (overlap) PNP_HIP(hipEventRecord(ctx->ev_z8, s_lo));
-    commit_affine(ctx, z_poly, n, &out->z_comm);
+    if (lag) {  // z from its evaluations; its iNTT joins its LDE on the side stream
+        fork();
+        ntt_run(nt, z_poly, lg, true, false, s_lo, num);
+        lde_on(s_lo, z_poly, z8);
+        if (overlap) PNP_HIP(hipEventRecord(ctx->ev_z8, s_lo));
+        tm.mark("r3_z");
+        const uint64_t *sc[1] = {num};
+        CommitmentC *oc[1] = {&out->z_comm};
+        commit_evals_batch(ctx, sc, 1, n, oc);
+    } else {
+        ntt_run(nt, z_poly, lg, true, false, s, num);
+        tm.mark("r3_z");
+        fork();
+        lde_on(s_lo, z_poly, z8);
+        if (overlap) PNP_HIP(hipEventRecord(ctx->ev_z8, s_lo));
+        commit_affine(ctx, z_poly, n, &out->z_comm);
+    }
     append_comm(tr, "z", out->z_comm);
     // lookup grand product (permutation/mod.rs:754-822)
     uint64_t *z2_poly = ctx->buf("z2_poly", n);
@@ -382,6 +402,8 @@ int prove_impl(pnp_ctx *ctx, const CircuitC *cs, int device_ptrs, ProofC *out, c
         PNP_HIP(hipMemcpyAsync(z2_poly, one, 32, hipMemcpyHostToDevice, s));
         PNP_HIP(hipStreamSynchronize(s));
     } else {
+        // num is rewritten: the side stream's z iNTT must have read it
+        if (lag && overlap) PNP_HIP(hipStreamWaitEvent(s, ctx->ev_z8, 0));
         k_lookup_nd(num, den, fc, tc, h1, h2, delta, eps, n, s);
         k_batch_inverse(den, n, ctx->scratch_a, s);
         k_mul_inplace(num, den, n, s);
