@@ -44,9 +44,11 @@ namespace pnp {
 
 // ---------------------------------------------------------------- 1. digits
 constexpr uint32_t KEY_ZERO = 0xFFFFFFFFu;
-__global__ void k_digits(const uint64_t *scalars, uint64_t n, int c, int W, uint32_t *keys) {
-    uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
-    if (i >= n) return;
+// the W signed c-bit digits of scalar i as keys (magnitude - 1 | sign << 31,
+// KEY_ZERO for a zero digit), row w of keys at keys[w n + i]; fn(key) per digit
+template <class F>
+__device__ __forceinline__ void scalar_digits(const uint64_t *scalars, uint64_t i, uint64_t n, int c, int W,
+                                              uint32_t *keys, F fn) {
     Fr s = from_mont(load_fr(scalars, i));
     const uint32_t NB = 1u << (c - 1);
     uint32_t carry = 0;
@@ -74,7 +76,13 @@ __global__ void k_digits(const uint64_t *scalars, uint64_t n, int c, int W, uint
         }
         // the top window never carries: W c >= 255 + 1 for the configured c (scalars < 2^255)
         keys[(uint64_t)w * n + i] = key;
+        fn(key);
     }
+}
+__global__ void k_digits(const uint64_t *scalars, uint64_t n, int c, int W, uint32_t *keys) {
+    uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    scalar_digits(scalars, i, n, c, W, keys, [](uint32_t) {});
 }
 
 // Virtual window v reads `rows` key rows starting at row v*vstride + off of
@@ -147,6 +155,30 @@ __global__ __launch_bounds__(1024) void k_coarse_hist(const uint32_t *keys, KeyR
     for (int b = threadIdx.x; b < NBc; b += blockDim.x) counts[cidx(v, gridDim.y, b, NBc, wmaj, ch, nch)] = hist[b];
 }
 
+// k_digits + k_coarse_hist in one pass for the standard folded layout (every
+// window of MSM v = blockIdx.y, keys of MSM v at keys + v W n): the keys are
+// counted as they are made instead of being read back
+struct ScalarPtrs {
+    static constexpr int MAX = 16;
+    const uint64_t *p[MAX];
+};
+__global__ __launch_bounds__(1024) void k_digits_hist(ScalarPtrs sp, uint64_t n, int c, int W, int fb, int NBc,
+                                                      uint64_t chunk, int nch, uint32_t *keys, uint32_t *counts,
+                                                      int wmaj = 1) {
+    __shared__ uint32_t hist[1 << SORT_CB];
+    const int v = blockIdx.y, ch = blockIdx.x;
+    for (int b = threadIdx.x; b < NBc; b += blockDim.x) hist[b] = 0;
+    __syncthreads();
+    const uint64_t lo = (uint64_t)ch * chunk, hi = lo + chunk < n ? lo + chunk : n;
+    uint32_t *kv = keys + (uint64_t)v * W * n;
+    for (uint64_t i = lo + threadIdx.x; i < hi; i += blockDim.x)
+        scalar_digits(sp.p[v], i, n, c, W, kv, [&](uint32_t key) {
+            if (key != KEY_ZERO) atomicAdd(&hist[(key & 0x7FFFFFFFu) >> fb], 1u);
+        });
+    __syncthreads();
+    for (int b = threadIdx.x; b < NBc; b += blockDim.x) counts[cidx(v, gridDim.y, b, NBc, wmaj, ch, nch)] = hist[b];
+}
+
 // ---------------------------------------------------------------- 3. scan
 // exclusive scan of u32 in place, three phases over 1024-element tiles
 __global__ __launch_bounds__(256) void k_scan_tiles(uint32_t *d, uint64_t n, uint32_t *tile_sums) {
@@ -212,9 +244,17 @@ static void scan_u32(uint32_t *d, uint64_t n, DevBuf &scratch, hipStream_t s) {
 
 // ---------------------------------------------------------------- 4. scatters
 // pass A: entry (table index | sign << 31) and its fine key, grouped by coarse
-// bin.  Tiles of 4096 keys are counting-sorted in LDS first, so each bin's
-// entries of a tile leave as one contiguous run (coalesced stores).
-constexpr int TILE_K = 4096;
+// bin.  Tiles of 16384 keys are counting-sorted in LDS first, so each bin's
+// entries of a tile leave as one contiguous run (coalesced stores: ~32
+// entries per bin and tile; 4096-key tiles left ~8-entry runs, and pass A took
+// 3.9 instead of 3.3 ms per proof, A/B 0.1437 -> 0.1425 s per proof,
+// profiles/r03_ab_sort_tiles.txt; one workgroup per CU with 134 KB of LDS).
+#ifndef PNP_TILE_K
+#define PNP_TILE_K 16384
+#endif
+constexpr int TILE_K = PNP_TILE_K;
+constexpr int KPT = TILE_K / 1024;  // keys per lane per tile
+static_assert(TILE_K % 4096 == 0 && TILE_K <= 16384, "PNP_TILE_K: a multiple of 4096 up to 16384");
 __device__ __forceinline__ void tile_scan(uint32_t *lh, uint32_t *lofs, int nb) {
     // exclusive scan of lh[0..nb) into lofs by wave 0
     if (threadIdx.x < 64) {
@@ -258,26 +298,31 @@ __global__ __launch_bounds__(1024) void k_coarse_scatter(const uint32_t *keys, K
         const uint32_t *k = kb + (uint64_t)r * n;
         const uint32_t idb = (uint32_t)((kr.id_row0 + r) * kr.id_mul + kr.id_base);
         for (uint64_t tb = lo; tb < hi; tb += TILE_K) {
-            const uint64_t i0 = tb + 4 * threadIdx.x;
-            uint32_t key[4], rank[4];
-            if (vec && i0 + 4 <= hi) {
-                uint4 q = *reinterpret_cast<const uint4 *>(k + i0);
-                key[0] = q.x; key[1] = q.y; key[2] = q.z; key[3] = q.w;
-            } else {
+            // KPT keys per lane, in groups of four consecutive points (16-byte loads)
+            uint32_t key[KPT], rank[KPT];
 #pragma unroll
-                for (int j = 0; j < 4; j++) key[j] = i0 + j < hi ? k[i0 + j] : KEY_ZERO;
+            for (int g = 0; g < KPT / 4; g++) {
+                const uint64_t i0 = tb + 4 * (threadIdx.x + 1024 * g);
+                if (vec && i0 + 4 <= hi) {
+                    uint4 q = *reinterpret_cast<const uint4 *>(k + i0);
+                    key[4 * g] = q.x; key[4 * g + 1] = q.y; key[4 * g + 2] = q.z; key[4 * g + 3] = q.w;
+                } else {
+#pragma unroll
+                    for (int j = 0; j < 4; j++) key[4 * g + j] = i0 + j < hi ? k[i0 + j] : KEY_ZERO;
+                }
             }
 #pragma unroll
-            for (int j = 0; j < 4; j++)
+            for (int j = 0; j < KPT; j++)
                 if (key[j] != KEY_ZERO) rank[j] = atomicAdd(&lh[(key[j] & 0x7FFFFFFFu) >> fb], 1u);
             __syncthreads();
             tile_scan(lh, lofs, NBc);
             __syncthreads();
 #pragma unroll
-            for (int j = 0; j < 4; j++) {
+            for (int j = 0; j < KPT; j++) {
                 if (key[j] == KEY_ZERO) continue;
+                const uint64_t i = tb + 4 * (threadIdx.x + 1024 * (j / 4)) + (j & 3);
                 uint32_t mag = key[j] & 0x7FFFFFFFu, at = lofs[mag >> fb] + rank[j];
-                st_e[at] = (idb + (uint32_t)(i0 + j)) | (key[j] & 0x80000000u);
+                st_e[at] = (idb + (uint32_t)i) | (key[j] & 0x80000000u);
                 st_m[at] = mag;
             }
             __syncthreads();
@@ -846,8 +891,10 @@ struct GroupPlan {
     int nv;  // virtual windows (bucket sets)
 };
 
+// scalars != nullptr: the keys are not made yet; k_digits_hist makes them
+// (standard folded layout: gp.kr covers every window of MSMs 0 .. nv-1)
 static void sort_group(MsmWork &wk, MsmGroup &gb, const uint32_t *keys, const GroupPlan &gp,
-                       const MsmCfg &g, hipStream_t s) {
+                       const MsmCfg &g, hipStream_t s, const uint64_t *const *scalars = nullptr) {
     const int nv = gp.nv;
     const uint64_t n = gp.kr.n, WB = (uint64_t)nv * g.NB;
     // points per coarse-pass workgroup: ~512 workgroups in all, >= 1024 points each
@@ -870,7 +917,14 @@ static void sort_group(MsmWork &wk, MsmGroup &gb, const uint32_t *keys, const Gr
     uint32_t *counts = static_cast<uint32_t *>(gb.counts.p);
     uint32_t *bstart = static_cast<uint32_t *>(gb.offsets.p);
     dim3 grid((uint32_t)nch, (uint32_t)nv);
-    hipLaunchKernelGGL(k_coarse_hist, grid, dim3(1024), 0, s, keys, gp.kr, fb, NBc, chunk, nch, counts);
+    if (scalars) {
+        ScalarPtrs sp{};
+        for (int v = 0; v < nv; v++) sp.p[v] = scalars[v];
+        hipLaunchKernelGGL(k_digits_hist, grid, dim3(1024), 0, s, sp, n, g.c, g.W, fb, NBc, chunk, nch,
+                           const_cast<uint32_t *>(keys), counts, 1);
+    } else {
+        hipLaunchKernelGGL(k_coarse_hist, grid, dim3(1024), 0, s, keys, gp.kr, fb, NBc, chunk, nch, counts);
+    }
     PNP_HIP(hipGetLastError());
     const uint64_t ncount = nbins * nch;
     PNP_HIP(hipMemsetAsync(counts + ncount, 0, 4, s));
@@ -1008,6 +1062,15 @@ static hipEvent_t ev_get(MsmWork &wk, int i) {
 // n_table / id_base: a folded table built over n_table points of which this
 // call's points are [id_base, id_base + n) (bucket-range mode keeps the full
 // table; a point-range batch then indexes into it); 0 = the table is this range
+static int pipe_min_b() {
+    static const int v = [] {
+        const char *e = getenv("PNP_MSM_PIPE");
+        return e ? std::max(1, atoi(e)) : 0;
+    }();
+    return v;
+}
+static bool pipe_off() { return pipe_min_b() == 0; }
+
 static void msm_local_batch(MsmWork &wk, const uint64_t *d_points, const uint64_t *const *d_scalars,
                             int B, uint64_t n, uint64_t *h_xyzz, hipStream_t s,
                             const uint64_t *table, uint64_t n_table = 0, uint64_t id_base = 0) {
@@ -1021,10 +1084,20 @@ static void msm_local_batch(MsmWork &wk, const uint64_t *d_points, const uint64_
     auto need = [](DevBuf &b, size_t bytes) { if (b.bytes < bytes) b.alloc(bytes); };
     need(wk.digits, (uint64_t)g.W * B * n * 4);
     uint32_t *keys = static_cast<uint32_t *>(wk.digits.p);
-    for (int b = 0; b < B; b++) {
-        hipLaunchKernelGGL(k_digits, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, s, d_scalars[b], n,
-                           g.c, g.W, keys + (uint64_t)b * g.W * n);
-        PNP_HIP(hipGetLastError());
+    // PNP_MSM_FUSE_DIGITS=0: separate digit and histogram passes (A/B)
+    static const bool fuse_env = [] {
+        const char *e = getenv("PNP_MSM_FUSE_DIGITS");
+        return !e || atoi(e) != 0;
+    }();
+    const bool no_pipe = pipe_off() || B < pipe_min_b();
+    // the fused pass makes the keys of the single standard folded group
+    const bool fuse = fuse_env && folded && B <= ScalarPtrs::MAX && no_pipe;
+    if (!fuse) {
+        for (int b = 0; b < B; b++) {
+            hipLaunchKernelGGL(k_digits, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, s, d_scalars[b], n,
+                               g.c, g.W, keys + (uint64_t)b * g.W * n);
+            PNP_HIP(hipGetLastError());
+        }
     }
     // groups: (plan, first MSM of its results)
     GroupPlan gp[2];
@@ -1035,11 +1108,6 @@ static void msm_local_batch(MsmWork &wk, const uint64_t *d_points, const uint64_
     // and tree kernels steal issue slots from the VALU-bound accumulation and
     // slow down themselves): one group unless PNP_MSM_PIPE=1 (experiments).
     // PNP_MSM_PIPE=B: pipeline batches of at least B MSMs only (experiments)
-    static const int pipe_min_b = [] {
-        const char *e = getenv("PNP_MSM_PIPE");
-        return e ? std::max(1, atoi(e)) : 0;
-    }();
-    const bool no_pipe = pipe_min_b == 0 || B < pipe_min_b;
     if (!folded) {
         kr.vstride = 1, kr.off = 0, kr.rows = 1, kr.id_row0 = 0, kr.id_mul = 0;
         gp[0] = {kr, B * g.W};
@@ -1069,7 +1137,7 @@ static void msm_local_batch(MsmWork &wk, const uint64_t *d_points, const uint64_
     const uint64_t *pts = folded ? table : d_points;
     const uint64_t *res[2] = {nullptr, nullptr};
     if (ng == 1) {
-        sort_group(wk, wk.grp[0], keys, gp[0], g, s);
+        sort_group(wk, wk.grp[0], keys, gp[0], g, s, fuse ? d_scalars : nullptr);
         accumulate_group(wk, wk.grp[0], gp[0], g, pts, table, s);
         res[0] = reduce_group(wk.grp[0], gp[0], g, s, folded);
     } else {
