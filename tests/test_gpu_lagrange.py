@@ -119,3 +119,35 @@ def test_commit_evals_degenerate_key_refused():
             ctx.commit_evals(d.data_ptr(), n)
     finally:
         ctx.close()
+
+
+def test_prover_coefficient_commitments_same_proof():
+    """gen_proof with the Lagrange basis switched off (PNP_LAGRANGE=0: the
+    path a degenerate key takes) returns the same bytes as the oracle, like
+    the default path does (test_gpu_merkle.py); run in a child process, the
+    switch is read once per process."""
+    import os
+    import subprocess
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    code = (
+        "import sys; sys.path[:0] = [%r, %r]\n"
+        "import merkle_circuit as mc\n"
+        "from test_general import pis_of\n"
+        "from pnp import abi\n"
+        "import pnp\n"
+        "cp, _ = mc.merkle_circuit(4, seed=11)\n"
+        "inp = cp.build()\n"
+        "exp = inp.oracle_proof()\n"
+        "ctx = pnp.Context(0)\n"
+        "ctx.load_prover_key(inp.pk, inp.n, device_ptrs=False)\n"
+        "ctx.load_commit_key(inp.ck, inp.n, device_ptrs=False)\n"
+        "got = ctx.prove_ex(inp.circuit, False, pis_of(inp))\n"
+        "ctx.close()\n"
+        "assert abi.proof_to_bytes(got) == abi.proof_to_bytes(exp)\n"
+        "print('SAME')\n"
+    ) % (here, os.path.join(os.path.dirname(here), "zprize23-gpu-submission_amd"))
+    env = dict(os.environ, PNP_LAGRANGE="0")
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert "SAME" in r.stdout

@@ -1253,7 +1253,8 @@ static bool msm_bucket_batch(MsmWork &wk, const uint64_t *const *sc, int B, uint
     // 1. digits of this rank's points
     need(wk.digits, (uint64_t)g.W * B * std::max<uint64_t>(n, 1) * 4);
     uint32_t *keys = static_cast<uint32_t *>(wk.digits.p);
-    for (int b = 0; b < B && n; b++) {
+    const bool fuse = B <= ScalarPtrs::MAX;  // digits made by the histogram pass
+    for (int b = 0; b < B && n && !fuse; b++) {
         hipLaunchKernelGGL(k_digits, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, s, sc[b], n, g.c, g.W,
                            keys + (uint64_t)b * g.W * n);
         PNP_HIP(hipGetLastError());
@@ -1269,7 +1270,13 @@ static bool msm_bucket_batch(MsmWork &wk, const uint64_t *const *sc, int B, uint
     uint32_t *counts = static_cast<uint32_t *>(gb.counts.p);
     PNP_HIP(hipMemsetAsync(counts, 0, (ncount + 1) * 4, s));
     const dim3 grid((uint32_t)nch, (uint32_t)B);
-    if (n) {
+    if (n && fuse) {
+        ScalarPtrs sp{};
+        for (int b = 0; b < B; b++) sp.p[b] = sc[b];
+        hipLaunchKernelGGL(k_digits_hist, grid, dim3(1024), 0, s, sp, n, g.c, g.W, fb, NBc, chunk, nch, keys, counts,
+                           W);
+        PNP_HIP(hipGetLastError());
+    } else if (n) {
         hipLaunchKernelGGL(k_coarse_hist, grid, dim3(1024), 0, s, keys, kr, fb, NBc, chunk, nch, counts, W);
         PNP_HIP(hipGetLastError());
     }
