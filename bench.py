@@ -511,7 +511,8 @@ def main():
         mad_rate = SIMDS * CLOCK_HZ * 64 / mad_cycles()          # v_mad_u64_u32 / s
         fq_peak = mad_rate / MADS_PER_FQ_PRODUCT                 # Fq products / s
         fq_achieved = madds_per_s * FQ_PRODUCTS_PER_MADD
-        traffic = pmc_traffic()
+        # the PMC traffic was measured on the default single-GPU workload only
+        traffic = pmc_traffic() if (world == 1 and not solo and args.lg == 22 and args.circuit == "merkle") else None
         q_gbs = q_bytes / (q_ms / 1e3) / 1e9 if q_ms > 0 else 0.0
         out = {
             "metric": METRIC,
