@@ -142,6 +142,7 @@ void KernelTimer::end(const char *name, hipStream_t s, hipEvent_t e0, double byt
 void KernelTimer::collect() {
     for (auto &p : pending) {
         float ms = 0;
+        PNP_HIP(hipEventSynchronize(p.e1));  // (no-op once the stream has drained)
         PNP_HIP(hipEventElapsedTime(&ms, p.e0, p.e1));
         auto &st = stats[p.name];
         st.ms += ms;
