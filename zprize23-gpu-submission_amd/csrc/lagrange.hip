@@ -16,11 +16,11 @@
 // Cost: one EC transform per (commit key, n), at the first commitment that
 // needs it (like the folded table of the monomial key): log2(n) DIF layers of
 // n/2 butterflies (a, b) -> (a + b, w^k (a - b)), one variable-base scalar
-// multiplication per butterfly — fixed 4-bit windows over the twiddle's
-// canonical integer, the 15 multiples of the lane's point kept in a per-lane
-// scratch table, so every lane of a wave runs the same 64 x (4 doublings + 1
-// addition) whatever its twiddle (a bit-serial ladder would diverge on every
-// bit).  1/n is folded into the first layer.  Point arithmetic: the radix-2^29
+// multiplication per butterfly — GLV-split twiddle (two 128-bit halves),
+// fixed 4-bit joint windows, the 15 multiples of the lane's point kept in a
+// per-lane scratch table, so every lane of a wave runs the same 32 x (4
+// doublings + 2 additions) whatever its twiddle (a bit-serial ladder would
+// diverge on every bit).  1/n is folded into the first layer.  Point arithmetic: the radix-2^29
 // XYZZ formulas of ec29.cuh for the scalar multiplications; the butterfly's
 // sum and difference in exact 32-bit XYZZ (ec.cuh add: equal, opposite and
 // infinite operands handled).  Outputs are bit-reversed by the DIF order and
@@ -28,8 +28,9 @@
 // msm_build_table.
 //
 // Exceptional additions inside a scalar multiplication cannot occur (the
-// accumulator holds m P with 16 <= m and m + digit <= twiddle < r), so a
-// zero ZZ at the end can only come from a degenerate key (a point of small
+// accumulator holds (a + b lambda) P for prefixes a < lambda, b of the two
+// halves, a + b lambda < r, never +- a window digit or its lambda multiple),
+// so a zero ZZ at the end can only come from a degenerate key (a point of small
 // order, tau a root of unity); it is flagged and the caller keeps committing
 // from coefficients.
 #include <algorithm>
@@ -68,9 +69,53 @@ __global__ __launch_bounds__(256) void k_lag_powers(uint64_t *tw, uint64_t m, Fr
     store_fr(tw, e, acc);
 }
 
+// GLV on BLS12-381 G1: phi(x, y) = (beta x, y) = [lambda] P, with
+// lambda = z^2 - 1 (128 bits, lambda^2 + lambda + 1 = 0 mod r) and beta the
+// matching cube root of unity in Fq (the other root gives [lambda^2] P; the
+// pair was checked against the oracle's scalar multiplication, and the whole
+// basis against the oracle's MSM in tests/test_gpu_lagrange.py).  beta is in
+// the R = 2^406 form of field29.cuh.
+__device__ constexpr uint32_t GLV_LAMBDA[4] = {0xffffffffu, 0x00000000u, 0x0001a402u, 0xac45a401u};
+__device__ constexpr uint32_t GLV_BETA29[14] = {0x1195dfebu, 0x1b04e484u, 0x6026044u, 0x86070a2u, 0x1fd68858u,
+                                                0x137e9670u, 0x6871e67u, 0x1e736664u, 0x83b24f6u, 0x8a70373u,
+                                                0x2a012fdu, 0x112f94bu, 0x18a2733cu, 0x3u};
+
+// s = s1 + s2 lambda, s1 < lambda, s2 = floor(s / lambda) < 2^128 (s < r < 2^255):
+// binary long division of the 256-bit s by lambda
+__device__ __forceinline__ void glv_split(const uint32_t s[8], uint32_t s1[4], uint32_t s2[4]) {
+    uint32_t rem[5] = {0, 0, 0, 0, 0}, q[4] = {0, 0, 0, 0};
+#pragma unroll 1
+    for (int b = 255; b >= 0; b--) {
+        const uint32_t bit = (s[b >> 5] >> (b & 31)) & 1u;
+#pragma unroll
+        for (int i = 4; i > 0; i--) rem[i] = (rem[i] << 1) | (rem[i - 1] >> 31);
+        rem[0] = (rem[0] << 1) | bit;
+        uint32_t t[5], br = 0;
+#pragma unroll
+        for (int i = 0; i < 5; i++) {
+            const uint64_t d = (uint64_t)rem[i] - (i < 4 ? GLV_LAMBDA[i] : 0u) - br;
+            t[i] = (uint32_t)d;
+            br = (uint32_t)(d >> 63);
+        }
+        if (!br) {
+#pragma unroll
+            for (int i = 0; i < 5; i++) rem[i] = t[i];
+            if (b < 128) q[b >> 5] |= 1u << (b & 31);  // the quotient is < 2^128
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        s1[i] = rem[i];
+        s2[i] = q[i];
+    }
+}
+
 // s P for a canonical scalar s (8 x 32-bit limbs, s < r), P not infinity;
-// tab: this lane's 15-point scratch table.  *bad set when the result is
-// degenerate (ZZ = 0 mod q).
+// tab: this lane's 15-point scratch table (j P, j = 1..15).  GLV: s = s1 +
+// s2 lambda, both < 2^128, so 32 joint windows of 4 bits: 4 doublings, then
+// s1's digit times P and s2's digit times phi(P) (the table entry with X times
+// beta) — ~2.4k instead of ~3.4k Fq products per multiplication.  *bad set
+// when the result is degenerate (ZZ = 0 mod q).
 __device__ __forceinline__ Xyzz29 lag_smul(const Xyzz29 &P, const uint32_t *s, uint32_t *tab, uint32_t *bad) {
     {
         Xyzz29 T = P;
@@ -83,20 +128,26 @@ __device__ __forceinline__ Xyzz29 lag_smul(const Xyzz29 &P, const uint32_t *s, u
             store_xyzz29(tab + LAG_PT * (k - 1), T);
         }
     }
+    uint32_t s1[4], s2[4];
+    glv_split(s, s1, s2);
     Xyzz29 acc = P;
     bool started = false;
 #pragma unroll 1
-    for (int w = 256 / LAG_WIN - 1; w >= 0; w--) {
+    for (int w = 128 / LAG_WIN - 1; w >= 0; w--) {
         if (started) {
 #pragma unroll 1
             for (int d = 0; d < LAG_WIN; d++) acc = xdbl29(acc);
         }
         const int bit = w * LAG_WIN;
-        const uint32_t dig = (s[bit >> 5] >> (bit & 31)) & LAG_TAB;
-        if (dig) {
-            const Xyzz29 Q = load_xyzz29(tab + LAG_PT * (dig - 1));
-            acc = started ? xadd29(acc, Q) : Q;
-            started = true;
+#pragma unroll 1
+        for (int j = 0; j < 2; j++) {  // one addition site: s1's digit, then s2's
+            const uint32_t dig = ((j ? s2 : s1)[bit >> 5] >> (bit & 31)) & LAG_TAB;
+            if (dig) {
+                Xyzz29 Q = load_xyzz29(tab + LAG_PT * (dig - 1));
+                if (j) Q.x = mul29(Q.x, const29(GLV_BETA29));
+                acc = started ? xadd29(acc, Q) : Q;
+                started = true;
+            }
         }
     }
     if (!started || zero29(acc.zz)) *bad = 1u;
