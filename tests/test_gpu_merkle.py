@@ -111,3 +111,65 @@ def test_synth_merkle_matches_builder(pc, height):
             assert np.array_equal(from_dev(sig[j]), inp.sigma_evals[j]), name
     finally:
         ctx.close()
+
+
+def _prove_v2_counters(inp, names, env=None):
+    import pnp
+    ctx = pnp.Context(0)
+    try:
+        ctx.load_prover_key(inp.pk, inp.n, device_ptrs=False)
+        ctx.load_commit_key(inp.ck, inp.n, device_ptrs=False)
+        ctx.kernel_timing(True)
+        got = ctx.prove_ex(inp.circuit, False, pis_of(inp))
+        return got, {k: ctx.kernel_bytes(k) for k in names}
+    finally:
+        ctx.close()
+
+
+def test_merkle_wire_groups_used(pc):
+    """Round 1 commits wires a, b, d over the copy-constraint groups of the
+    Merkle circuit (csrc/wires.hip: each Poseidon state value sits in three
+    consecutive rows of those wires): the grouped path runs and the proof is
+    the oracle's byte for byte."""
+    cp, _ = mc.merkle_circuit(6, seed=5, pc=pc)
+    inp = cp.build()
+    exp = inp.oracle_proof()
+    got, c = _prove_v2_counters(inp, ["wire_groups_used", "wire_group_fallback"])
+    assert abi.proof_to_bytes(got) == abi.proof_to_bytes(exp)
+    assert c == {"wire_groups_used": 1, "wire_group_fallback": 0}
+
+
+def test_merkle_broken_copy_constraint_falls_back(pc):
+    """A witness that breaks a copy constraint (one row of a 3-row Poseidon
+    state group changed in wire a): the grouped commitment would differ, so
+    the per-proof check sends round 1 back to the row-by-row commitment — the
+    proof still equals the oracle's (which commits every row)."""
+    cp, _ = mc.merkle_circuit(6, seed=5, pc=pc)
+    inp = cp.build()
+    va = [r[1][0] for r in cp.rows]
+    row = next(i for i in range(1, len(va) - 1) if va[i] == va[i - 1] == va[i + 1] and cp.vals[va[i]])
+    w = inp.arrays["w_l"]
+    w[row, 0] ^= 1  # still < r: a different field element, in place (the structs point here)
+    exp = inp.oracle_proof()
+    got, c = _prove_v2_counters(inp, ["wire_groups_used", "wire_group_fallback"])
+    assert abi.proof_to_bytes(got) == abi.proof_to_bytes(exp)
+    assert c == {"wire_groups_used": 0, "wire_group_fallback": 1}
+
+
+def test_merkle_wire_groups_off_same_proof(pc, monkeypatch):
+    """PNP_WIRE_GROUPS=0 (row-by-row commitments from the evaluations) gives
+    the same bytes — checked in a child process, the switch is read once."""
+    import subprocess
+    import sys
+    import os
+    code = ("import sys; sys.path[:0] = sys.argv[1:3];"
+            "import merkle_circuit as mc, test_gpu_merkle as t; from pnp import abi;"
+            "cp, _ = mc.merkle_circuit(5, seed=6); inp = cp.build();"
+            "got, c = t._prove_v2_counters(inp, ['wire_groups_used']);"
+            "assert c['wire_groups_used'] == 0, c;"
+            "assert abi.proof_to_bytes(got) == abi.proof_to_bytes(inp.oracle_proof()); print('ok')")
+    here = os.path.dirname(os.path.abspath(__file__))
+    pkg = os.path.join(os.path.dirname(here), "zprize23-gpu-submission_amd")
+    r = subprocess.run([sys.executable, "-c", code, here, pkg], env=dict(os.environ, PNP_WIRE_GROUPS="0"),
+                       capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0 and "ok" in r.stdout, r.stdout[-2000:] + r.stderr[-2000:]

@@ -62,6 +62,7 @@ void ck_derived_reset(pnp_ctx *ctx) {
     ctx->lag_points.release();
     ctx->lag_table_n = 0;
     ctx->lag_table.release();
+    wire_bases_reset(ctx);
 }
 
 const uint64_t *lagrange_table(pnp_ctx *ctx, uint64_t n) {
@@ -466,6 +467,7 @@ int pnp_load_prover_key(pnp_ctx *ctx, const ProverKeyC *pk, uint64_t D, int devi
     PNP_TRY({
         PNP_HIP(hipSetDevice(ctx->device));
         ctx->pk_loaded = false;
+        ctx->pk_gen++;  // derived groups (wires.hip) re-check sigma
         ctx->pk_owned.clear();
         ProverKeyC dev{};
         uint64_t *const *src = reinterpret_cast<uint64_t *const *>(pk);

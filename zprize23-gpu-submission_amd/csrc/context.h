@@ -57,6 +57,24 @@ struct pnp_ctx {
     pnp::DevBuf lag_points, lag_table;
     uint64_t lag_n = 0, lag_table_n = 0, lag_table_p0 = 0, lag_table_p1 = 0;
     bool lag_ok = false;
+    // wire commitments over copy-constraint groups (wires.hip): the rows of
+    // one wire that hold one variable (a cycle of sigma restricted to the
+    // wire) share the base sum_i L_i, so a wire commits with one scalar per
+    // group; built from sigma and the Lagrange points on the first proof that
+    // needs them, kept while both are unchanged
+    struct WireBases {
+        bool built = false, ok = false;
+        uint64_t n = 0, total = 0, m = 0, len = 0;  // domain, bases, largest group count, MSM length
+        uint64_t g[4] = {}, off[4] = {};
+        bool ident[4] = {};             // ungrouped wire: its scalars are its evaluations
+        pnp::DevBuf grp[4], rep[4];     // row -> group, group -> representative row
+        pnp::DevBuf scal[4];            // per-proof group scalars (m each, zero from g)
+        pnp::DevBuf table;              // folded table over the `total` bases
+        pnp::DevBuf sigma;              // the sigma evaluations the groups came from
+        pnp::DevBuf flag;
+        uint64_t pk_gen = 0;            // prover-key load the sigma check last covered
+    } wb;
+    uint64_t pk_gen = 0;                // incremented by every pnp_load_prover_key
 
     // ---- per-proof working set (sized on first use, reused) ----
     std::map<std::string, pnp::DevBuf> work;
@@ -84,6 +102,13 @@ const uint64_t *lagrange_table(pnp_ctx *ctx, uint64_t n);
 // lagrange_table(ctx, n) != nullptr
 void commit_evals_batch(pnp_ctx *ctx, const uint64_t *const *d_evals, int B, uint64_t n, CommitmentC *const *out);
 void commit_affine(pnp_ctx *ctx, const uint64_t *d_scalars, uint64_t n, CommitmentC *out);
+// the four wire commitments from their n padded evaluations over the
+// copy-constraint-grouped bases (wires.hip); false (nothing written) when the
+// groups are unavailable or the witness differs inside a group, and the caller
+// commits with commit_evals_batch
+bool commit_wires_grouped(pnp_ctx *ctx, const uint64_t *const *d_evals, uint64_t n, CommitmentC *const *out);
+// drop the wire groups (a new commit key or Lagrange basis)
+void wire_bases_reset(pnp_ctx *ctx);
 // B commitments over the resident SRS in one batched MSM
 // local: on a multi-GPU run the scalars hold only this rank's point range
 void commit_affine_batch(pnp_ctx *ctx, const uint64_t *const *d_scalars, int B, uint64_t n,

@@ -89,12 +89,18 @@ __global__ void k_digits(const uint64_t *scalars, uint64_t n, int c, int W, uint
 // the key matrix (row r = keys[r*n .. r*n + n)); the entry of point i in its
 // row j is  i + (id_row0 + j) * id_mul  (id_mul = 0: the point index itself;
 // id_mul = n: the index into the folded table).
+constexpr int MSM_BATCH_MAX = 16;  // MSMs per batch with per-MSM pointers / offsets
 struct KeyRows {
     uint64_t n;
     int vstride, off, rows;
     uint32_t id_row0;
     uint64_t id_mul;
     uint64_t id_base = 0;  // added to every entry id (a rank's first point in the full folded table)
+    // folded tables holding several point sets (MsmSegs): MSM v < nseg starts
+    // at seg_off[v] of every table row (nseg = 0: one point set; the
+    // per-window layout has more virtual windows than slots here)
+    int nseg = 0;
+    uint64_t seg_off[MSM_BATCH_MAX] = {};
 };
 
 // ---------------------------------------------------------------- 2. coarse pass
@@ -159,7 +165,7 @@ __global__ __launch_bounds__(1024) void k_coarse_hist(const uint32_t *keys, KeyR
 // window of MSM v = blockIdx.y, keys of MSM v at keys + v W n): the keys are
 // counted as they are made instead of being read back
 struct ScalarPtrs {
-    static constexpr int MAX = 16;
+    static constexpr int MAX = MSM_BATCH_MAX;
     const uint64_t *p[MAX];
 };
 __global__ __launch_bounds__(1024) void k_digits_hist(ScalarPtrs sp, uint64_t n, int c, int W, int fb, int NBc,
@@ -296,7 +302,8 @@ __global__ __launch_bounds__(1024) void k_coarse_scatter(const uint32_t *keys, K
     const bool vec = ((n | chunk) & 3) == 0;
     for (int r = 0; r < kr.rows; r++) {
         const uint32_t *k = kb + (uint64_t)r * n;
-        const uint32_t idb = (uint32_t)((kr.id_row0 + r) * kr.id_mul + kr.id_base);
+        const uint64_t so = v < kr.nseg ? kr.seg_off[v] : 0;
+        const uint32_t idb = (uint32_t)((kr.id_row0 + r) * kr.id_mul + kr.id_base + so);
         for (uint64_t tb = lo; tb < hi; tb += TILE_K) {
             // KPT keys per lane, in groups of four consecutive points (16-byte loads)
             uint32_t key[KPT], rank[KPT];
@@ -1073,7 +1080,8 @@ static bool pipe_off() { return pipe_min_b() == 0; }
 
 static void msm_local_batch(MsmWork &wk, const uint64_t *d_points, const uint64_t *const *d_scalars,
                             int B, uint64_t n, uint64_t *h_xyzz, hipStream_t s,
-                            const uint64_t *table, uint64_t n_table = 0, uint64_t id_base = 0) {
+                            const uint64_t *table, uint64_t n_table = 0, uint64_t id_base = 0,
+                            const uint64_t *seg_off = nullptr) {
     if (n == 0 || B == 0) {
         for (int b = 0; b < B; b++) put_xyzz(Xyzz::inf(), h_xyzz + 24 * b);
         return;
@@ -1133,6 +1141,12 @@ static void msm_local_batch(MsmWork &wk, const uint64_t *d_points, const uint64_
     } else {
         kr.vstride = g.W, kr.off = 0, kr.rows = g.W, kr.id_row0 = 0, kr.id_mul = n_table, kr.id_base = id_base;
         gp[0] = {kr, 1};
+    }
+    if (seg_off) {  // MSM first[k] + v of group k starts at seg_off[first[k] + v] (window split: MSM 0)
+        for (int k = 0; k < ng; k++) {
+            gp[k].kr.nseg = gp[k].nv;
+            for (int v = 0; v < gp[k].nv; v++) gp[k].kr.seg_off[v] = seg_off[B == 1 ? 0 : first[k] + v];
+        }
     }
     const uint64_t *pts = folded ? table : d_points;
     const uint64_t *res[2] = {nullptr, nullptr};
@@ -1228,7 +1242,8 @@ static Xyzz mul_small(const Xyzz &p, uint64_t k) {
 // counts) when the records would overflow the exchange buffers: the caller
 // then takes point ranges.
 static bool msm_bucket_batch(MsmWork &wk, const uint64_t *const *sc, int B, uint64_t n_full, uint64_t p0,
-                             uint64_t p1, uint64_t *part, hipStream_t s, const uint64_t *table) {
+                             uint64_t p1, uint64_t *part, hipStream_t s, const uint64_t *table,
+                             const uint64_t *seg_off = nullptr) {
     const int W = wk.world;
     // Bucket ranges pay from 4 ranks on (solo-rank times per proof at n = 2^22,
     // points vs buckets: 2 ranks 91.1 vs 94.0 ms, 4 ranks 56.0 vs 55.3, 8 ranks
@@ -1262,6 +1277,10 @@ static bool msm_bucket_batch(MsmWork &wk, const uint64_t *const *sc, int B, uint
     // 2. pass A, destination-major (chunks as sort_group: ~512 workgroups)
     KeyRows kr;
     kr.n = n, kr.vstride = g.W, kr.off = 0, kr.rows = g.W, kr.id_row0 = 0, kr.id_mul = n_full, kr.id_base = p0;
+    if (seg_off) {
+        kr.nseg = B;
+        for (int b = 0; b < B; b++) kr.seg_off[b] = seg_off[b];
+    }
     const int nch0 = std::max(1, 512 / B);
     const uint64_t chunk = std::max<uint64_t>(1024, (n + nch0 - 1) / nch0);
     const int nch = (int)std::max<uint64_t>(1, (n + chunk - 1) / chunk);
@@ -1431,9 +1450,16 @@ void msm_point_range(uint64_t n, int rank, int world, uint64_t &p0, uint64_t &p1
 // meet in one all-gather of B XYZZ points per rank and are added on the host.
 void msm_run_batch(MsmWork &wk, const uint64_t *d_points, const uint64_t *const *d_scalars, int B,
                    uint64_t n, uint64_t *h_xyzz, hipStream_t s, const uint64_t *table,
-                   bool scalars_local) {
+                   bool scalars_local, const MsmSegs *segs) {
+    if (segs && (!table || B > MSM_BATCH_MAX)) {
+        set_error("msm: point segments need a folded table and at most %d MSMs", MSM_BATCH_MAX);
+        throw Error(PNP_E_ARG);
+    }
     if (wk.world == 1) {
-        msm_local_batch(wk, d_points, d_scalars, B, n, h_xyzz, s, table);
+        if (segs)
+            msm_local_batch(wk, nullptr, d_scalars, B, n, h_xyzz, s, table, segs->n_table, 0, segs->off);
+        else
+            msm_local_batch(wk, d_points, d_scalars, B, n, h_xyzz, s, table);
         return;
     }
     uint64_t p0, p1;
@@ -1441,11 +1467,14 @@ void msm_run_batch(MsmWork &wk, const uint64_t *d_points, const uint64_t *const 
     std::vector<const uint64_t *> sc(B);
     for (int b = 0; b < B; b++) sc[b] = scalars_local ? d_scalars[b] : d_scalars[b] + 4 * p0;
     std::vector<uint64_t> part((size_t)B * 24);
-    // bucket ranges (the folded table covers all n points) or point ranges
-    const bool full = table && wk.full_table();
-    if (!(full && msm_bucket_batch(wk, sc.data(), B, n, p0, p1, part.data(), s, table)))
-        msm_local_batch(wk, d_points + 12 * p0, sc.data(), B, p1 - p0, part.data(), s, table, full ? n : 0,
-                        full ? p0 : 0);
+    // bucket ranges (the folded table covers all n points) or point ranges;
+    // a segmented table always covers every point of its sets
+    const bool full = table && (wk.full_table() || segs);
+    const uint64_t n_tab = segs ? segs->n_table : n;
+    const uint64_t *off = segs ? segs->off : nullptr;
+    if (!(table && wk.full_table() && msm_bucket_batch(wk, sc.data(), B, n_tab, p0, p1, part.data(), s, table, off)))
+        msm_local_batch(wk, d_points ? d_points + 12 * p0 : nullptr, sc.data(), B, p1 - p0, part.data(), s, table,
+                        full ? n_tab : 0, full ? p0 : 0, off);
     const uint64_t slot = (uint64_t)B * 24 * 8;
     if (wk.xbuf_bytes < slot * wk.world) {
         set_error("msm shard: exchange buffer %llu B < %llu B", (unsigned long long)wk.xbuf_bytes,

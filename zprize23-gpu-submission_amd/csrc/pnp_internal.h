@@ -163,10 +163,18 @@ struct MsmWork {
 // `table` (optional): msm_build_table(d_points, n) — the folded layout
 void msm_run(MsmWork &w, const uint64_t *d_points, const uint64_t *d_scalars_mont, uint64_t n,
              uint64_t *h_xyzz, hipStream_t s, const uint64_t *table = nullptr);
+// A folded table built over n_table points holding several point sets: MSM b
+// of a batch sums over points off[b] .. off[b] + n - 1 of it (wires.hip: the
+// four wires' grouped bases in one table)
+struct MsmSegs {
+    uint64_t n_table = 0;
+    uint64_t off[16] = {};
+};
 // scalars_local: multi-GPU, d_scalars[b] hold only this rank's point range
+// segs: `table` is segmented as above (d_points unused)
 void msm_run_batch(MsmWork &w, const uint64_t *d_points, const uint64_t *const *d_scalars, int B,
                    uint64_t n, uint64_t *h_xyzz, hipStream_t s, const uint64_t *table = nullptr,
-                   bool scalars_local = false);
+                   bool scalars_local = false, const MsmSegs *segs = nullptr);
 // multi-GPU MSMs: the points [p0, p1) rank `rank` of `world` takes
 void msm_point_range(uint64_t n, int rank, int world, uint64_t &p0, uint64_t &p1);
 // T[k*n + i] = 2^(c*k) P_i, k < W (msm_cfg(n)), affine, in the radix-2^29

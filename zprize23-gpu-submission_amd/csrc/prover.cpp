@@ -267,8 +267,10 @@ int prove_impl(pnp_ctx *ctx, const CircuitC *cs, int device_ptrs, ProofC *out, c
         for (int j = 0; j < 4; j++) lde_on(s_lo, wpoly[j], w8buf[j]);
         if (overlap) PNP_HIP(hipEventRecord(ctx->ev_w8, s_lo));
         tm.mark("r1_intt");
+        // over the copy-constraint groups when the key has them and the
+        // witness keeps them (wires.hip), else row by row
         const uint64_t *sc[4] = {wsc[0], wsc[1], wsc[2], wsc[3]};
-        commit_evals_batch(ctx, sc, 4, n, wc);
+        if (!commit_wires_grouped(ctx, sc, n, wc)) commit_evals_batch(ctx, sc, 4, n, wc);
     } else {
         for (int j = 0; j < 4; j++) ntt_run(nt, wpoly[j], lg, true, false, s, wsc[j]);
         tm.mark("r1_intt");
