@@ -248,3 +248,131 @@ def test_unit_levels_bounds():
     vals = [rng.randrange(R) for _ in range(256)]
     out = dif_pass(vals, tw29, 8, unit_last=True)
     assert [out[_brev(k, 8)] for k in range(256)] == _ref_dft(vals, g)
+
+
+# ---------------------------------------------------------------- k_quotient29
+def mul2(a, b, c, d):  # r29_mul2: (a b + c d) 2^-261, one reduction
+    p = C["R29_P"]
+    m, out, acc = [0] * 9, [], 0
+    for k in range(17):
+        for i in range(max(0, k - 8), min(k, 8) + 1):
+            acc += a[i] * b[k - i] + c[i] * d[k - i]
+            assert acc < U64
+        for i in range(max(0, k - 8), min(k, 9)):
+            acc += m[i] * p[k - i]
+            assert acc < U64
+        if k < 9:
+            m[k] = (-acc) & M
+            acc += m[k]
+            assert acc % (1 << L) == 0 and acc < U64
+        else:
+            out.append(acc & M)
+        acc >>= L
+    out.append(acc)
+    assert acc < U32
+    assert val(out) % R == (val(a) * val(b) + val(c) * val(d)) * pow(2, -261, R) % R
+    return out
+
+
+def _mul_in(a, b):  # a product's inputs stay below 2^261 (normalised top limb)
+    assert val(a) < 2**261 and val(b) < 2**261 and norm_ok(a) and norm_ok(b)
+    return mul(a, b)
+
+
+def quotient29(x, consts, qm=True, pinv=True):
+    """csrc/protocol.hip k_quotient29_ on one point, limb for limb: x = the
+    loaded 32-byte values (2^261 form, except vh_inv / l1v / pinv in the
+    2^256 form), consts = the 2^261-form constants.  Returns the stored
+    (canonical, 2^256-form) value."""
+    ld = {k: from_fr(v) for k, v in x.items()}
+    cst = {k: limbs(v) for k, v in consts.items()}
+    a, b, c, d = ld["a"], ld["b"], ld["c"], ld["d"]
+
+    def pow5(v):
+        v2 = _mul_in(v, v)
+        return _mul_in(_mul_in(v2, v2), v)
+
+    acc = mul2(a, ld["q_l"], b, ld["q_r"])
+    if qm:
+        acc = add(acc, _mul_in(_mul_in(a, b), ld["q_m"]))
+    acc = add(acc, mul2(c, ld["q_o"], d, ld["q_4"]))
+    acc = add(acc, mul2(pow5(a), ld["q_hl"], pow5(b), ld["q_hr"]))
+    acc = add(acc, _mul_in(pow5(d), ld["q_h4"]))
+    acc = add(acc, ld["q_c"])
+    num = _mul_in(acc, ld["q_arith"])
+    beta, gamma = cst["beta"], cst["gamma"]
+    xb = _mul_in(ld["lin"], beta)
+    x2 = add(xb, xb)
+    x4 = add(x2, x2)
+    x8 = add(x4, x4)
+    xb7 = sub(x8, xb, C["KDIF"][0])
+    xb13 = add(add(x8, x4), xb)
+    xb17 = add(add(x8, x8), xb)
+    pa = _mul_in(add(add(xb, a), gamma), add(add(xb7, b), gamma))
+    pa = _mul_in(pa, add(add(xb13, c), gamma))
+    pa = _mul_in(pa, add(add(xb17, d), gamma))
+    f = [add(add(_mul_in(ld[f"sig{j}"], beta), w), gamma) for j, w in enumerate((a, b, c, d))]
+    pb = _mul_in(_mul_in(_mul_in(f[0], f[1]), f[2]), f[3])
+    zi, zn = ld["zi"], ld["zn"]
+    nzn = sub([0] * 9, zn, C["KDIF"][0])
+    assert val(pa) < 2**261 and val(pb) < 2**261 and val(nzn) < 2**261
+    num = add(num, _mul_in(mul2(pa, zi, pb, nzn), cst["alpha"]))
+    l1t = _mul_in(sub(zi, cst["one"], C["KDIF"][0]), cst["alpha2"])
+    assert val(num) < 2**261 and val(l1t) < 2**261
+    r = mul2(num, ld["vh_inv"], l1t, ld["l1v"])
+    if pinv:
+        r = add(r, _mul_in(cst["c_pi"], ld["pinv"]))
+    assert val(r) < 2**264
+    return val(canon(r))
+
+
+def _quotient_ref(v, k, qm=True, pinv=True):
+    """The same numerator in plain field arithmetic (protocol.hip k_quotient_)."""
+    a, b, c, d = v["a"], v["b"], v["c"], v["d"]
+    gate = (a * v["q_l"] + b * v["q_r"] + (a * b * v["q_m"] if qm else 0) + c * v["q_o"] + d * v["q_4"]
+            + pow(a, 5, R) * v["q_hl"] + pow(b, 5, R) * v["q_hr"] + pow(d, 5, R) * v["q_h4"] + v["q_c"])
+    num = gate * v["q_arith"]
+    x, beta, gamma = v["lin"], k["beta"], k["gamma"]
+    pa = (x * beta + a + gamma) * (7 * x * beta + b + gamma) * (13 * x * beta + c + gamma) * \
+        (17 * x * beta + d + gamma)
+    pb = 1
+    for j, w in enumerate((a, b, c, d)):
+        pb *= v[f"sig{j}"] * beta + w + gamma
+    num += (pa * v["zi"] - pb * v["zn"]) * k["alpha"]
+    l1t = (v["zi"] - 1) * k["alpha2"]
+    r = num * v["vh_inv"] + l1t * v["l1v"] + (k["c_pi"] * v["pinv"] if pinv else 0)
+    return r % R
+
+
+ARRAYS29 = ("a", "b", "c", "d", "q_l", "q_r", "q_m", "q_o", "q_4", "q_hl", "q_hr", "q_h4", "q_c", "q_arith",
+            "lin", "sig0", "sig1", "sig2", "sig3", "zi", "zn")
+ARRAYS256 = ("vh_inv", "l1v", "pinv")
+CONSTS29 = ("beta", "gamma", "alpha", "alpha2", "one", "c_pi")
+
+
+@pytest.mark.parametrize("case", ["random", "worst", "qm_off"])
+def test_quotient29_model(case):
+    """k_quotient29's limb-level model equals the field formula of k_quotient_
+    (values in the 2^261 form in, the 2^256 form out), with every column sum
+    < 2^64 and every product input < 2^261 asserted; 'worst' takes every
+    loaded value and constant r - 1 (the bounds only)."""
+    rng = random.Random(11)
+    for trial in range(4 if case != "worst" else 1):
+        if case == "worst":
+            v = {k: R - 1 for k in ARRAYS29 + ARRAYS256}
+            kc = {k: R - 1 for k in CONSTS29 if k != "one"}
+        else:
+            v = {k: rng.randrange(R) for k in ARRAYS29 + ARRAYS256}
+            kc = {k: rng.randrange(R) for k in CONSTS29 if k != "one"}
+        kc["one"] = 1
+        # stored forms: 2^261 for ARRAYS29 and the constants, 2^256 for the final multipliers
+        x = {k: v[k] * 2**261 % R for k in ARRAYS29}
+        x.update({k: v[k] * 2**256 % R for k in ARRAYS256})
+        consts = {k: kc[k] * 2**261 % R for k in CONSTS29}
+        if case == "worst":  # the largest stored words everywhere
+            x = {k: R - 1 for k in x}
+            consts = {k: R - 1 for k in consts}
+        qm = case != "qm_off"
+        got = quotient29(x, consts, qm=qm)
+        if case != "worst":
+            assert got == _quotient_ref(v, kc, qm=qm) * 2**256 % R

@@ -129,14 +129,17 @@ def _prove_v2_counters(inp, names, env=None):
 def test_merkle_wire_groups_used(pc):
     """Round 1 commits wires a, b, d over the copy-constraint groups of the
     Merkle circuit (csrc/wires.hip: each Poseidon state value sits in three
-    consecutive rows of those wires): the grouped path runs and the proof is
-    the oracle's byte for byte."""
+    consecutive rows of those wires) and round 3 commits z over its runs (z
+    is constant over the rows sigma fixes): both grouped paths run and the
+    proof is the oracle's byte for byte."""
     cp, _ = mc.merkle_circuit(6, seed=5, pc=pc)
     inp = cp.build()
     exp = inp.oracle_proof()
-    got, c = _prove_v2_counters(inp, ["wire_groups_used", "wire_group_fallback"])
+    got, c = _prove_v2_counters(inp, ["wire_groups_used", "wire_group_fallback", "z_groups_used",
+                                      "z_group_fallback"])
     assert abi.proof_to_bytes(got) == abi.proof_to_bytes(exp)
-    assert c == {"wire_groups_used": 1, "wire_group_fallback": 0}
+    # z too: constant over the padding rows (sigma fixes them), one scalar per run
+    assert c == {"wire_groups_used": 1, "wire_group_fallback": 0, "z_groups_used": 1, "z_group_fallback": 0}
 
 
 def test_merkle_broken_copy_constraint_falls_back(pc):

@@ -586,6 +586,33 @@ int pnp_load_prover_key(pnp_ctx *ctx, const ProverKeyC *pk, uint64_t D, int devi
         blk("lin", dev.linear_evaluations);
         blk("vh_inv", vh_inv.u64());
         if (ctx->pk_std_coset) blk("l1v", l1v.u64());
+        // k_quotient29's copies (2^261 form) for keys of its class: no custom
+        // gate, no lookup selector or table, the standard coset
+        ctx->pk_blk29.clear();
+        ctx->pk_q29 = false;
+        {
+            static const bool q29_on = [] {
+                const char *e = getenv("PNP_QUOT29");
+                return !e || atoi(e) != 0;
+            }();
+            bool ok = q29_on && ctx->pk_std_coset && ctx->pk_qlookup_zero && !ctx->pk_custom_nz[0] &&
+                      !ctx->pk_custom_nz[1] && !ctx->pk_custom_nz[2] && !ctx->pk_custom_nz[3];
+            const uint64_t *tabs[4] = {dev.table1, dev.table2, dev.table3, dev.table4};
+            for (int k = 0; k < 4 && ok; k++)
+                ok = !tabs[k] || !pnp::k_any_nonzero(tabs[k], 4 * D, ctx->scratch_b, ctx->stream);
+            if (ok) {
+                const char *names[] = {"q_m", "q_l", "q_r", "q_o", "q_4", "q_c", "q_hl", "q_hr", "q_h4", "q_arith",
+                                       "sig0", "sig1", "sig2", "sig3", "lin"};
+                for (const char *nm : names) {
+                    const uint64_t *src = ctx->blk(nm);
+                    if (!src) continue;
+                    auto &b = ctx->pk_blk29[nm];
+                    b.alloc(32 * (uint64_t)ctx->pk_nb * D);
+                    pnp::k_to_form29(src, b.u64(), (uint64_t)ctx->pk_nb * D, ctx->stream);
+                }
+                ctx->pk_q29 = true;
+            }
+        }
         ctx->pk_blk_rank = ctx->msm.rank;
         ctx->pk_blk_world = world;
         ctx->pk_pinv.release();

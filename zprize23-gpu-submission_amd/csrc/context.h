@@ -41,6 +41,14 @@ struct pnp_ctx {
         auto it = pk_blk.find(name);
         return it == pk_blk.end() ? nullptr : it->second.u64();
     }
+    // the same block arrays in the 2^261 form for k_quotient29 (protocol.h),
+    // made at key load for keys of its class (pk_q29): selectors, sigmas, lin
+    std::map<std::string, pnp::DevBuf> pk_blk29;
+    bool pk_q29 = false;
+    const uint64_t *blk29(const char *name) const {
+        auto it = pk_blk29.find(name);
+        return it == pk_blk29.end() ? nullptr : it->second.u64();
+    }
     // ---- resident commit key ----
     bool ck_loaded = false;
     uint64_t ck_points = 0;
@@ -62,13 +70,15 @@ struct pnp_ctx {
     // wire) share the base sum_i L_i, so a wire commits with one scalar per
     // group; built from sigma and the Lagrange points on the first proof that
     // needs them, kept while both are unchanged
+    // Index 4 is z (round 3): its groups are the runs of rows sigma fixes
+    // (the padding rows: z is constant there).
     struct WireBases {
-        bool built = false, ok = false;
+        bool built = false, ok = false, wires_ok = false, z_ok = false;
         uint64_t n = 0, total = 0, m = 0, len = 0;  // domain, bases, largest group count, MSM length
-        uint64_t g[4] = {}, off[4] = {};
-        bool ident[4] = {};             // ungrouped wire: its scalars are its evaluations
-        pnp::DevBuf grp[4], rep[4];     // row -> group, group -> representative row
-        pnp::DevBuf scal[4];            // per-proof group scalars (m each, zero from g)
+        uint64_t g[5] = {}, off[5] = {};
+        bool ident[5] = {};             // ungrouped wire: its scalars are its evaluations
+        pnp::DevBuf grp[5], rep[5];     // row -> group slot, slot -> representative row
+        pnp::DevBuf scal[5];            // per-proof group scalars at their slots (n each)
         pnp::DevBuf table;              // folded table over the `total` bases
         pnp::DevBuf sigma;              // the sigma evaluations the groups came from
         pnp::DevBuf flag;
@@ -107,6 +117,9 @@ void commit_affine(pnp_ctx *ctx, const uint64_t *d_scalars, uint64_t n, Commitme
 // groups are unavailable or the witness differs inside a group, and the caller
 // commits with commit_evals_batch
 bool commit_wires_grouped(pnp_ctx *ctx, const uint64_t *const *d_evals, uint64_t n, CommitmentC *const *out);
+// z (round 3) from its n evaluations over its groups, the runs of rows sigma
+// fixes (wires.hip); false when unavailable (the caller commits row by row)
+bool commit_z_grouped(pnp_ctx *ctx, const uint64_t *d_z, uint64_t n, CommitmentC *out);
 // drop the wire groups (a new commit key or Lagrange basis)
 void wire_bases_reset(pnp_ctx *ctx);
 // B commitments over the resident SRS in one batched MSM

@@ -105,6 +105,33 @@ __device__ __forceinline__ R29 r29_mul(const R29 &a, const R29 &b) {
     return r;
 }
 
+// (a b + c d) 2^-261 with one reduction (< (a b + c d) / 2^261 + r); every
+// column holds <= 27 products of normalised limbs (< 2^58 each): < 2^63
+__device__ __forceinline__ R29 r29_mul2(const R29 &a, const R29 &b, const R29 &c, const R29 &d) {
+    uint32_t m[9];
+    R29 r;
+    uint64_t acc = 0;
+#pragma unroll
+    for (int k = 0; k < 17; k++) {
+#pragma unroll
+        for (int i = (k > 8 ? k - 8 : 0); i <= (k < 8 ? k : 8); i++) {
+            acc += (uint64_t)a.l[i] * b.l[k - i];
+            acc += (uint64_t)c.l[i] * d.l[k - i];
+        }
+#pragma unroll
+        for (int i = (k > 8 ? k - 8 : 0); i < (k < 9 ? k : 9); i++) acc += (uint64_t)m[i] * R29_P[k - i];
+        if (k < 9) {
+            m[k] = (0u - (uint32_t)acc) & R29_M;
+            acc += m[k];
+        } else {
+            r.l[k - 9] = (uint32_t)acc & R29_M;
+        }
+        acc >>= 29;
+    }
+    r.l[8] = (uint32_t)acc;
+    return r;
+}
+
 // x < 2^264 -> x mod r: q = floor(l_8 MU / 2^32) <= x / r falls short of it by
 // at most 2, x - q r = x + q (2^261 - r) - q 2^261, then two conditional
 // subtractions of r (y >= r iff y + 2^261 - r reaches bit 261)

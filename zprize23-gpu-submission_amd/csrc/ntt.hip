@@ -907,6 +907,30 @@ static const uint64_t *block_twist_table(NttTables &t, uint32_t lg_n, bool inver
     return p;
 }
 
+// the forward block twists times 32: an LDE through them yields 32 f(x) in
+// the 2^256 form, i.e. f(x) in the 2^261 form of fr29.cuh (k_quotient29's
+// inputs, protocol.hip), at no cost in the transform
+__global__ void k_times32(const uint64_t *in, uint64_t *out, uint64_t N) {
+    const uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    if (i >= N) return;
+    Fr x = load_fr(in, i);
+#pragma unroll
+    for (int k = 0; k < 5; k++) x = x + x;
+    store_fr(out, i, x);
+}
+static const uint64_t *block_twist_table32(NttTables &t, uint32_t lg_n, hipStream_t s) {
+    auto it = t.blk_twist32.find(lg_n);
+    if (it != t.blk_twist32.end()) return it->second.u64();
+    const uint64_t N = 8ULL << lg_n;
+    const uint64_t *src = block_twist_table(t, lg_n, false, s);
+    DevBuf buf(N * 32);
+    hipLaunchKernelGGL(k_times32, dim3((uint32_t)((N + 255) / 256)), dim3(256), 0, s, src, buf.u64(), N);
+    PNP_HIP(hipGetLastError());
+    const uint64_t *p = buf.u64();
+    t.blk_twist32.emplace(lg_n, std::move(buf));
+    return p;
+}
+
 static void check_blocks(int m0, int nb) {
     if (m0 < 0 || nb < 1 || m0 + nb > 8) {
         set_error("coset blocks [%d, %d) outside [0, 8)", m0, m0 + nb);
@@ -936,16 +960,18 @@ void ntt_warm(NttTables &t, uint32_t lg_n, hipStream_t s) {
             block_twist_table29(t, lg_n, inv, s);
         }
     }
+    block_twist_table32(t, lg_n, s);
     ntt_prepare_coset(t, s);
 }
 
 void lde_blocks(NttTables &t, const uint64_t *in, uint64_t *out, uint32_t lg_n, int m0, int nb,
-                hipStream_t s) {
+                hipStream_t s, bool form29) {
     const uint64_t n = 1ULL << lg_n;
     PassFuse fz;
     fz.src = in;
-    fz.pre = block_twist_table(t, lg_n, false, s) + 4 * (uint64_t)m0 * n;
-    if (ntt29_enabled()) fz.pre29 = block_twist_table29(t, lg_n, false, s) + 9 * (uint64_t)m0 * n;
+    // (form29: the 32-bit passes; the experimental radix-2^29 passes have no scaled twist)
+    fz.pre = (form29 ? block_twist_table32(t, lg_n, s) : block_twist_table(t, lg_n, false, s)) + 4 * (uint64_t)m0 * n;
+    if (ntt29_enabled() && !form29) fz.pre29 = block_twist_table29(t, lg_n, false, s) + 9 * (uint64_t)m0 * n;
     fz.src_mask = n - 1;
     check_blocks(m0, nb);
     ntt_core(t, out, lg_n, false, false, s, (uint64_t)nb, fz);

@@ -61,6 +61,8 @@ struct NttTables {
     // the same twiddles / twists times 2^261 in radix 2^29 (9 u32 per entry)
     // for the radix-2^29 passes (fr29.cuh)
     std::map<uint32_t, DevBuf> fwd29, inv29, blk_twist29, blk_twist_inv29;
+    // the forward block twists times 32 (lde_blocks form29)
+    std::map<uint32_t, DevBuf> blk_twist32;
 };
 const uint64_t *ntt_twiddles(NttTables &t, uint32_t lg, bool inverse, hipStream_t s);
 void ntt_prepare_coset(NttTables &t, hipStream_t s);
@@ -76,8 +78,9 @@ void coset_lde8(NttTables &t, const uint64_t *in, uint64_t *out8, uint32_t lg_n,
 // build every NTT table of domain 2^lg_n on stream s (before forking work
 // that reads them onto another stream)
 void ntt_warm(NttTables &t, uint32_t lg_n, hipStream_t s);
+// form29: the values times 32, i.e. in the 2^261 form of fr29.cuh (k_quotient29)
 void lde_blocks(NttTables &t, const uint64_t *in, uint64_t *out, uint32_t lg_n, int m0, int nb,
-                hipStream_t s);
+                hipStream_t s, bool form29 = false);
 // per block: unscaled inverse size-n DFT then twist by w_8n^(-m u)
 void intt_blocks(NttTables &t, uint64_t *d, uint32_t lg_n, int m0, int nb, hipStream_t s);
 // 8-point inverse DFT across blocks + g^-i / (8n): coefficient chunks u in [q0, q0+len)

@@ -40,6 +40,28 @@ struct QuotArgs {
     Fr bk[4], opd, eopd, sep2, sep3;
 };
 
+// k_quotient29: the quotient of the common case (no custom gates, no lookup,
+// closed-form L1 and at most one PI: the Merkle circuit) in radix-2^29
+// arithmetic (fr29.cuh).  The arrays marked 2^261 hold values in that
+// Montgomery form (the wire / z LDEs through the scaled twist, lde_blocks
+// form29; key copies made at load); vh_inv, l1v and pinv stay in the 2^256
+// form, so the final products return the quotient to it.  Constants: nine
+// 29-bit limbs of their 2^261 forms (fr_to_r29_limbs).
+struct Quot29Args {
+    const uint64_t *w8[4], *z8;                                                  // 2^261
+    const uint64_t *q_m, *q_l, *q_r, *q_o, *q_4, *q_c, *q_hl, *q_hr, *q_h4, *q_arith;  // 2^261
+    const uint64_t *sig[4], *lin;                                                // 2^261
+    const uint64_t *vh_inv, *l1v, *pinv;                                         // 2^256
+    uint32_t c_pi[9], alpha[9], alpha2[9], beta[9], gamma[9], one[9];
+    uint64_t n;
+    uint32_t lg_n;
+};
+// the 2^261 form of a (2^256-form) Fr as nine 29-bit limbs, canonical
+void fr_to_r29_limbs(const Fr &a, uint32_t l[9]);
+void k_quotient29(const Quot29Args &q, uint64_t N8, uint64_t *out, hipStream_t s);
+// out = 32 in (mod r) elementwise: 2^256-form arrays -> their 2^261 forms
+void k_to_form29(const uint64_t *in, uint64_t *out, uint64_t n, hipStream_t s);
+
 // custom-gate quotient terms (k_widgets): block-layout arrays as QuotArgs;
 // sel = range, logic, fixed-base scalar mul, curve addition selector
 // evaluations (nullptr = zero selector), sep = their separation challenges

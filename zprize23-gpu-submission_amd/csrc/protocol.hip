@@ -17,6 +17,7 @@
 #include "pnp_internal.h"
 #include "protocol.h"
 #include "widgets.cuh"
+#include "fr29.cuh"
 #include <vector>
 
 namespace pnp {
@@ -314,6 +315,110 @@ __global__ __launch_bounds__(256) void k_quotient_(QuotArgs q, uint64_t N8, uint
 void k_quotient(const QuotArgs &q, uint64_t N8, uint64_t *out, hipStream_t s) {
     hipLaunchKernelGGL(k_quotient_, dim3(nblk(N8)), dim3(256), 0, s, q, N8, out);
     PNP_HIP(hipGetLastError());
+}
+
+// ---------------------------------------------------------------- quotient, radix 2^29
+// The same numerator as k_quotient_ for the common case (protocol.h
+// Quot29Args), every product a radix-2^29 Montgomery product (fr29.cuh: 153
+// bare multiply-adds, no carry instructions, against 128 multiply-adds + 128
+// carries in 32-bit limbs; two-product sums share one reduction).  Inputs
+// are canonical 32-byte values, unpacked into nine limbs on load.  Bounds (r
+// = 0.452 * 2^256, so r / 2^261 < 0.0142; a product of x < X r and y < Y r
+// is < (0.0142 X Y + 1) r): gate terms < 1.03 r each, their sum < 6.2 r, num
+// < 1.1 r; x beta k_j < 17.3 r, the four permutation factors < 19.4 r, pa <
+// 1.4 r, pb < 1.05 r; every product input stays far below 2^261 (70 r), the
+// limit of the 64-bit column sums.  The output (< 2.1 r) is canonicalised.
+__device__ __forceinline__ R29 ld29(const uint64_t *p, uint64_t i) {
+    const uint4 *q = reinterpret_cast<const uint4 *>(p + 4 * i);
+    const uint4 lo = q[0], hi = q[1];
+    const uint32_t w[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+    return r29_from_words(w);
+}
+__device__ __forceinline__ R29 c29(const uint32_t *c) {
+    R29 r;
+#pragma unroll
+    for (int k = 0; k < 9; k++) r.l[k] = c[k];
+    return r;
+}
+__device__ __forceinline__ R29 pow5_29(const R29 &a) {
+    const R29 a2 = r29_mul(a, a);
+    return r29_mul(r29_mul(a2, a2), a);
+}
+__device__ __forceinline__ R29 add3_29(const R29 &a, const R29 &b, const R29 &c) {
+    return r29_add(r29_add(a, b), c);
+}
+
+// (4 waves per SIMD: <= 128 VGPRs; unbounded the compiler takes 129 and 3 waves)
+__global__ __launch_bounds__(256, 4) void k_quotient29_(Quot29Args q, uint64_t N8, uint64_t *out) {
+    const uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    if (i >= N8) return;
+    const uint64_t nx = next_in_block(i, q.n, q.lg_n);
+    const R29 a = ld29(q.w8[0], i), b = ld29(q.w8[1], i), c = ld29(q.w8[2], i), d = ld29(q.w8[3], i);
+    // gate (widget/arithmetic.cu:7-45)
+    R29 acc = r29_mul2(a, ld29(q.q_l, i), b, ld29(q.q_r, i));
+    if (q.q_m) acc = r29_add(acc, r29_mul(r29_mul(a, b), ld29(q.q_m, i)));
+    acc = r29_add(acc, r29_mul2(c, ld29(q.q_o, i), d, ld29(q.q_4, i)));
+    acc = r29_add(acc, r29_mul2(pow5_29(a), ld29(q.q_hl, i), pow5_29(b), ld29(q.q_hr, i)));
+    acc = r29_add(acc, r29_mul(pow5_29(d), ld29(q.q_h4, i)));
+    acc = r29_add(acc, ld29(q.q_c, i));
+    R29 num = r29_mul(acc, ld29(q.q_arith, i));
+    // permutation (proof_system/permutation.cu:267-296), x beta k_j by doublings
+    const R29 beta = c29(q.beta), gamma = c29(q.gamma);
+    const R29 xb = r29_mul(ld29(q.lin, i), beta);
+    const R29 x2 = r29_add(xb, xb), x4 = r29_add(x2, x2), x8 = r29_add(x4, x4);
+    const R29 xb7 = r29_sub(x8, xb, R29_KDIF[0]);  // + 2 r > xb
+    const R29 xb13 = add3_29(x8, x4, xb), xb17 = add3_29(x8, x8, xb);
+    R29 pa = r29_mul(add3_29(xb, a, gamma), add3_29(xb7, b, gamma));
+    pa = r29_mul(pa, add3_29(xb13, c, gamma));
+    pa = r29_mul(pa, add3_29(xb17, d, gamma));
+    R29 pb = r29_mul(add3_29(r29_mul(ld29(q.sig[0], i), beta), a, gamma),
+                     add3_29(r29_mul(ld29(q.sig[1], i), beta), b, gamma));
+    pb = r29_mul(pb, add3_29(r29_mul(ld29(q.sig[2], i), beta), c, gamma));
+    pb = r29_mul(pb, add3_29(r29_mul(ld29(q.sig[3], i), beta), d, gamma));
+    const R29 zi = ld29(q.z8, i), zn = ld29(q.z8, nx);
+    R29 zero;
+#pragma unroll
+    for (int k = 0; k < 9; k++) zero.l[k] = 0;
+    const R29 nzn = r29_sub(zero, zn, R29_KDIF[0]);  // 2 r - zn
+    num = r29_add(num, r29_mul(r29_mul2(pa, zi, pb, nzn), c29(q.alpha)));
+    // alpha^2 L1 (z - 1) / Z_H and PI / Z_H in closed form (protocol.h QuotArgs)
+    const R29 l1t = r29_mul(r29_sub(zi, c29(q.one), R29_KDIF[0]), c29(q.alpha2));
+    R29 r = r29_mul2(num, ld29(q.vh_inv, i), l1t, ld29(q.l1v, i));  // back in the 2^256 form
+    if (q.pinv) r = r29_add(r, r29_mul(c29(q.c_pi), ld29(q.pinv, i)));
+    r = r29_canon(r);
+    uint32_t w[8];
+    r29_to_words(r, w);
+    uint4 *o = reinterpret_cast<uint4 *>(out + 4 * i);
+    o[0] = make_uint4(w[0], w[1], w[2], w[3]);
+    o[1] = make_uint4(w[4], w[5], w[6], w[7]);
+}
+void k_quotient29(const Quot29Args &q, uint64_t N8, uint64_t *out, hipStream_t s) {
+    hipLaunchKernelGGL(k_quotient29_, dim3(nblk(N8)), dim3(256), 0, s, q, N8, out);
+    PNP_HIP(hipGetLastError());
+}
+
+__global__ void k_to_form29_(const uint64_t *in, uint64_t *out, uint64_t n) {
+    const uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    Fr x = load_fr(in, i);
+#pragma unroll
+    for (int k = 0; k < 5; k++) x = x + x;
+    store_fr(out, i, x);
+}
+void k_to_form29(const uint64_t *in, uint64_t *out, uint64_t n, hipStream_t s) {
+    hipLaunchKernelGGL(k_to_form29_, dim3(nblk(n)), dim3(256), 0, s, in, out, n);
+    PNP_HIP(hipGetLastError());
+}
+
+void fr_to_r29_limbs(const Fr &a, uint32_t l[9]) {
+    Fr x = a;
+    for (int k = 0; k < 5; k++) x = x + x;  // 32 a: the 2^261 form
+    for (int j = 0; j < 9; j++) {
+        const int bit = 29 * j, w = bit >> 5, sh = bit & 31;
+        uint64_t v = x.v[w] >> sh;
+        if (w + 1 < 8) v |= (uint64_t)x.v[w + 1] << (32 - sh);
+        l[j] = j < 8 ? (uint32_t)(v & 0x1FFFFFFFu) : (uint32_t)v;
+    }
 }
 
 // custom gates (quotient_poly.rs:253-296): out += sum_g selector_g * constraints_g

@@ -219,8 +219,15 @@ int prove_impl(pnp_ctx *ctx, const CircuitC *cs, int device_ptrs, ProofC *out, c
         return v < 6 ? 6 : v > 8 ? 8 : v;
     }();
     int nbq = dist ? nb : quot_blocks;  // blocks this round-4 attempt covers
-    auto lde_on = [&](hipStream_t st, const uint64_t *coeffs, uint64_t *dst) {
-        lde_blocks(nt, coeffs, dst, lg, mb0, nbq, st);
+    // The quotient of the common case (no custom gates, no lookup, closed
+    // forms, <= 1 PI: the Merkle circuit) runs in radix 2^29 (protocol.h
+    // k_quotient29): its wire and z LDEs are taken in the 2^261 form (the
+    // scaled twist, free) and the key arrays it reads come from the copies
+    // made at key load; any other circuit keeps k_quotient_ (PNP_QUOT29=0:
+    // always)
+    const bool q29 = ctx->pk_q29 && pi_pos.size() <= 1;
+    auto lde_on = [&](hipStream_t st, const uint64_t *coeffs, uint64_t *dst, bool f29) {
+        lde_blocks(nt, coeffs, dst, lg, mb0, nbq, st, f29);
     };
     auto fork = [&]() {
         if (!overlap) return;
@@ -264,7 +271,7 @@ int prove_impl(pnp_ctx *ctx, const CircuitC *cs, int device_ptrs, ProofC *out, c
     if (lag) {
         fork();
         for (int j = 0; j < 4; j++) ntt_run(nt, wpoly[j], lg, true, false, s_lo, wsc[j]);
-        for (int j = 0; j < 4; j++) lde_on(s_lo, wpoly[j], w8buf[j]);
+        for (int j = 0; j < 4; j++) lde_on(s_lo, wpoly[j], w8buf[j], q29);
         if (overlap) PNP_HIP(hipEventRecord(ctx->ev_w8, s_lo));
         tm.mark("r1_intt");
         // over the copy-constraint groups when the key has them and the
@@ -275,7 +282,7 @@ int prove_impl(pnp_ctx *ctx, const CircuitC *cs, int device_ptrs, ProofC *out, c
         for (int j = 0; j < 4; j++) ntt_run(nt, wpoly[j], lg, true, false, s, wsc[j]);
         tm.mark("r1_intt");
         fork();
-        for (int j = 0; j < 4; j++) lde_on(s_lo, wpoly[j], w8buf[j]);
+        for (int j = 0; j < 4; j++) lde_on(s_lo, wpoly[j], w8buf[j], q29);
         if (overlap) PNP_HIP(hipEventRecord(ctx->ev_w8, s_lo));
         const uint64_t *sc[4] = {wpoly[0], wpoly[1], wpoly[2], wpoly[3]};
         commit_affine_batch(ctx, sc, 4, n, wc);
@@ -377,17 +384,19 @@ int prove_impl(pnp_ctx *ctx, const CircuitC *cs, int device_ptrs, ProofC *out, c
     if (lag) {  // z from its evaluations; its iNTT joins its LDE on the side stream
         fork();
         ntt_run(nt, z_poly, lg, true, false, s_lo, num);
-        lde_on(s_lo, z_poly, z8);
+        lde_on(s_lo, z_poly, z8, q29);
         if (overlap) PNP_HIP(hipEventRecord(ctx->ev_z8, s_lo));
         tm.mark("r3_z");
         const uint64_t *sc[1] = {num};
         CommitmentC *oc[1] = {&out->z_comm};
-        commit_evals_batch(ctx, sc, 1, n, oc);
+        // z is constant over runs of rows sigma fixes (the padding): one
+        // scalar per run (wires.hip), else row by row
+        if (!commit_z_grouped(ctx, num, n, &out->z_comm)) commit_evals_batch(ctx, sc, 1, n, oc);
     } else {
         ntt_run(nt, z_poly, lg, true, false, s, num);
         tm.mark("r3_z");
         fork();
-        lde_on(s_lo, z_poly, z8);
+        lde_on(s_lo, z_poly, z8, q29);
         if (overlap) PNP_HIP(hipEventRecord(ctx->ev_z8, s_lo));
         commit_affine(ctx, z_poly, n, &out->z_comm);
     }
@@ -466,7 +475,7 @@ int prove_impl(pnp_ctx *ctx, const CircuitC *cs, int device_ptrs, ProofC *out, c
 
         QuotArgs q;
         // coset evaluations in block layout, this rank's blocks only
-        auto lde = [&](const uint64_t *coeffs, uint64_t *dst) { lde_on(s, coeffs, dst); };
+        auto lde = [&](const uint64_t *coeffs, uint64_t *dst) { lde_on(s, coeffs, dst, false); };
         for (int j = 0; j < 4; j++) q.w8[j] = w8buf[j];
         uint64_t *z28 = ctx->buf("z28", NB);
         q.z8 = z8;
@@ -561,7 +570,41 @@ int prove_impl(pnp_ctx *ctx, const CircuitC *cs, int device_ptrs, ProofC *out, c
         uint64_t *t_blk = ctx->buf("t_blk", NB);
         hipEvent_t qe0 = nullptr;
         ctx->ktimer.begin("quotient", s, qe0);
-        k_quotient(q, NBq, t_blk, s);
+        if (q29) {
+            Quot29Args q2;
+            for (int j = 0; j < 4; j++) q2.w8[j] = q.w8[j];
+            q2.z8 = q.z8;
+            q2.q_m = ctx->blk29("q_m");
+            q2.q_l = ctx->blk29("q_l");
+            q2.q_r = ctx->blk29("q_r");
+            q2.q_o = ctx->blk29("q_o");
+            q2.q_4 = ctx->blk29("q_4");
+            q2.q_c = ctx->blk29("q_c");
+            q2.q_hl = ctx->blk29("q_hl");
+            q2.q_hr = ctx->blk29("q_hr");
+            q2.q_h4 = ctx->blk29("q_h4");
+            q2.q_arith = ctx->blk29("q_arith");
+            for (int j = 0; j < 4; j++) q2.sig[j] = ctx->blk29(("sig" + std::to_string(j)).c_str());
+            q2.lin = ctx->blk29("lin");
+            q2.vh_inv = q.vh_inv;
+            q2.l1v = q.l1v;
+            q2.pinv = q.pinv;
+            fr_to_r29_limbs(q.pinv ? q.c_pi : Fr::zero(), q2.c_pi);
+            fr_to_r29_limbs(alpha, q2.alpha);
+            fr_to_r29_limbs(alpha2, q2.alpha2);
+            fr_to_r29_limbs(beta, q2.beta);
+            fr_to_r29_limbs(gamma, q2.gamma);
+            fr_to_r29_limbs(Fr::one(), q2.one);
+            q2.n = n;
+            q2.lg_n = lg;
+            if (!q2.l1v || !q2.q_l || !q2.lin || !q2.sig[3]) {
+                set_error("quotient29: key copies missing");
+                return PNP_E_ARG;
+            }
+            k_quotient29(q2, NBq, t_blk, s);
+        } else {
+            k_quotient(q, NBq, t_blk, s);
+        }
         if (ctx->pk_custom_nz[0] || ctx->pk_custom_nz[1] || ctx->pk_custom_nz[2] || ctx->pk_custom_nz[3]) {
             WidgetArgs g;
             for (int j = 0; j < 4; j++) g.w8[j] = q.w8[j];
@@ -879,8 +922,8 @@ int prove_impl(pnp_ctx *ctx, const CircuitC *cs, int device_ptrs, ProofC *out, c
             if (!(lin_z + r0).is_zero()) {
                 ctx->ktimer.credit("quotient_all_blocks", 1);
                 const uint64_t off = 4 * (uint64_t)nbq * n;  // blocks nbq .. 7
-                for (int j = 0; j < 4; j++) lde_blocks(nt, wpoly[j], w8buf[j] + off, lg, nbq, 8 - nbq, s);
-                lde_blocks(nt, z_poly, z8 + off, lg, nbq, 8 - nbq, s);
+                for (int j = 0; j < 4; j++) lde_blocks(nt, wpoly[j], w8buf[j] + off, lg, nbq, 8 - nbq, s, q29);
+                lde_blocks(nt, z_poly, z8 + off, lg, nbq, 8 - nbq, s, q29);
                 nbq = 8;
                 tr = tr3;
                 continue;

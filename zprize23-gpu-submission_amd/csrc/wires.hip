@@ -28,7 +28,9 @@
 //      representative row; run sums of the L_i (exact XYZZ additions, chunked
 //      so large groups — the zero variable's — stay parallel) -> affine bases;
 //   4. one folded table (msm_build_table) over the bases of all four wires,
-//      MSM b reading its wire's segment (MsmSegs).
+//      MSM b reading its wire's n-slot segment (MsmSegs); group k of g sits at
+//      slot floor(k n / g), so the groups spread over the whole segment and
+//      every rank of a sharded MSM gets its share of them.
 // A wire whose groups are nearly all single rows (g > 0.9 n, the Merkle
 // circuit's wire c) keeps the plain Lagrange points as its segment: its
 // scalars are its evaluations.
@@ -112,15 +114,27 @@ __global__ void k_wb_heads(const uint32_t *slab, uint64_t n, uint32_t *head) {
     if (t < n) head[t] = (t == 0 || slab[t] != slab[t - 1]) ? 1u : 0u;
 }
 
+// group k sits at slot bitrev(k) of its wire's n-slot segment (n = 2^lg, k <
+// g <= n): any run of consecutive groups spreads evenly over the segment, so
+// every rank's point range of a sharded MSM (n / W slots) holds its share of
+// them — the groups come in label order, the Merkle wires' real variables
+// first and the padding rows' singletons last; packed at the front (or spread
+// in order) the non-zero scalars would all fall to the first ranks
+__device__ __forceinline__ uint32_t wb_slot(uint64_t k, uint64_t g, uint64_t n) {
+    (void)g;
+    const int lg = 63 - __clzll(n);
+    return lg ? (uint32_t)(__brevll(k) >> (64 - lg)) : 0u;
+}
+
 // gid: inclusive scan of the heads (group index + 1)
 __global__ void k_wb_groups(const uint32_t *srow, const uint32_t *gid, const uint32_t *head, uint64_t n,
-                            uint32_t *grp, uint32_t *rep, uint32_t *gstart) {
+                            uint64_t g_cnt, uint32_t *grp, uint32_t *rep, uint32_t *gstart) {
     const uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
     if (t >= n) return;
-    const uint32_t g = gid[t] - 1, row = srow[t];
-    grp[row] = g;
+    const uint32_t g = gid[t] - 1, row = srow[t], slot = wb_slot(g, g_cnt, n);
+    grp[row] = slot;
     if (head[t]) {
-        rep[g] = row;
+        rep[slot] = row;
         gstart[g] = (uint32_t)t;
     }
 }
@@ -161,7 +175,23 @@ __global__ __launch_bounds__(256) void k_wb_final(const uint64_t *part, const ui
         if (e >= t1) break;
     }
     if (acc.is_inf()) atomicOr(bad, 1u);
-    store_xyzz(out + 24 * g, acc);
+    store_xyzz(out + 24 * (uint64_t)wb_slot(g, g_cnt, n), acc);
+}
+
+// z's runs: z_(i+1) = z_i ratio_i and ratio_i = 1 exactly when sigma fixes
+// all four positions of row i (the numerator and denominator products are the
+// same expression), so a run of fixed rows continues z's run; a run starts at
+// row 0 and after every row that sigma moves
+__global__ void k_wb_zheads(const uint32_t *next, uint64_t n, uint32_t *head, uint32_t *row) {
+    const uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    bool cont = i > 0;
+    for (int j = 0; j < 4 && cont; j++) {
+        const uint64_t p = (uint64_t)j * n + i - 1;
+        cont = next[p] == (uint32_t)p;
+    }
+    head[i] = cont ? 0u : 1u;
+    row[i] = (uint32_t)i;
 }
 
 // Lagrange points (affine) -> XYZZ, for an ungrouped wire's segment
@@ -204,6 +234,13 @@ bool groups_enabled() {
         return !e || atoi(e) != 0;
     }();
     return v;
+}
+bool z_groups_enabled() {
+    static const bool v = [] {
+        const char *e = getenv("PNP_Z_GROUPS");
+        return !e || atoi(e) != 0;
+    }();
+    return v && groups_enabled();
 }
 
 // hipcub temporary storage, grown on demand
@@ -255,11 +292,13 @@ void build_wire_bases(pnp_ctx *ctx, uint64_t n) {
                            static_cast<const uint32_t *>(pos2.p), idv.u64(), static_cast<uint32_t *>(next.p), bad);
         PNP_HIP(hipGetLastError());
     }
-    // 2. cycle labels
+    // 2. cycle labels (the jumps run on a copy: `next` stays the successor,
+    // z's runs below read it)
     {
-        DevBuf lab2(N * 4), nx2(N * 4);
+        DevBuf lab2(N * 4), nx1(N * 4), nx2(N * 4);
+        PNP_HIP(hipMemcpyAsync(nx1.p, next.p, N * 4, hipMemcpyDeviceToDevice, s));
         uint32_t *la = static_cast<uint32_t *>(lab.p), *lb = static_cast<uint32_t *>(lab2.p);
-        uint32_t *na = static_cast<uint32_t *>(next.p), *nb = static_cast<uint32_t *>(nx2.p);
+        uint32_t *na = static_cast<uint32_t *>(nx1.p), *nb = static_cast<uint32_t *>(nx2.p);
         hipLaunchKernelGGL(k_wb_iota, dim3(nblk(N)), dim3(256), 0, s, la, N);
         PNP_HIP(hipGetLastError());
         for (uint64_t span = 1; span < N; span *= 2) {
@@ -273,13 +312,34 @@ void build_wire_bases(pnp_ctx *ctx, uint64_t n) {
     }
     // 3. per wire: groups, representatives, run sums of the Lagrange points
     const uint64_t *L = ctx->lag_points.u64();
-    std::vector<DevBuf> bx(4);
+    std::vector<DevBuf> bx(5);
     {
         DevBuf srt(n * 4), srow(n * 4), row(n * 4), head(n * 4), gid(n * 4), gstart(n * 4), part(n * 192);
         uint32_t *srt_p = static_cast<uint32_t *>(srt.p), *srow_p = static_cast<uint32_t *>(srow.p);
         uint32_t *head_p = static_cast<uint32_t *>(head.p), *gid_p = static_cast<uint32_t *>(gid.p);
         const int bits = (int)lg + 2;  // labels < 4n
         const uint32_t C = 32;
+        // groups (rows srow in group order, heads, gid = inclusive scan) ->
+        // slots, representatives and the run sums of the Lagrange points
+        auto bases = [&](int j, uint32_t g) {
+            wb.grp[j].alloc(n * 4);
+            wb.rep[j].alloc(n * 4);
+            hipLaunchKernelGGL(k_wb_groups, dim3(nblk(n)), dim3(256), 0, s, srow_p, gid_p, head_p, n, (uint64_t)g,
+                               static_cast<uint32_t *>(wb.grp[j].p), static_cast<uint32_t *>(wb.rep[j].p),
+                               static_cast<uint32_t *>(gstart.p));
+            PNP_HIP(hipGetLastError());
+            hipLaunchKernelGGL(k_wb_chunks, dim3(nblk((n + C - 1) / C)), dim3(256), 0, s, L, srow_p, gid_p, n, C,
+                               part.u64());
+            PNP_HIP(hipGetLastError());
+            // the n slots: valid points everywhere (the empty slots' are never
+            // read, their scalars stay zero), the group sums at the group slots
+            bx[j].alloc(n * 192);
+            hipLaunchKernelGGL(k_wb_lift, dim3(nblk(n)), dim3(256), 0, s, L, n, bx[j].u64());
+            PNP_HIP(hipGetLastError());
+            hipLaunchKernelGGL(k_wb_final, dim3(nblk(g)), dim3(256), 0, s, part.u64(),
+                               static_cast<const uint32_t *>(gstart.p), (uint64_t)g, n, C, bx[j].u64(), bad);
+            PNP_HIP(hipGetLastError());
+        };
         for (int j = 0; j < 4; j++) {
             const uint32_t *labj = static_cast<const uint32_t *>(lab.p) + (uint64_t)j * n;
             hipLaunchKernelGGL(k_wb_iota, dim3(nblk(n)), dim3(256), 0, s, static_cast<uint32_t *>(row.p), n);
@@ -306,46 +366,58 @@ void build_wire_bases(pnp_ctx *ctx, uint64_t n) {
                 PNP_HIP(hipGetLastError());
                 continue;
             }
-            wb.grp[j].alloc(n * 4);
-            wb.rep[j].alloc((uint64_t)g * 4);
-            hipLaunchKernelGGL(k_wb_groups, dim3(nblk(n)), dim3(256), 0, s, srow_p, gid_p, head_p, n,
-                               static_cast<uint32_t *>(wb.grp[j].p), static_cast<uint32_t *>(wb.rep[j].p),
-                               static_cast<uint32_t *>(gstart.p));
+            bases(j, g);
+        }
+        // z (segment 4): runs of rows sigma fixes, already in row order
+        {
+            hipLaunchKernelGGL(k_wb_zheads, dim3(nblk(n)), dim3(256), 0, s, static_cast<const uint32_t *>(next.p), n,
+                               head_p, srow_p);
             PNP_HIP(hipGetLastError());
-            hipLaunchKernelGGL(k_wb_chunks, dim3(nblk((n + C - 1) / C)), dim3(256), 0, s, L, srow_p, gid_p, n, C,
-                               part.u64());
-            PNP_HIP(hipGetLastError());
-            bx[j].alloc((uint64_t)g * 192);
-            hipLaunchKernelGGL(k_wb_final, dim3(nblk(g)), dim3(256), 0, s, part.u64(),
-                               static_cast<const uint32_t *>(gstart.p), (uint64_t)g, n, C, bx[j].u64(), bad);
-            PNP_HIP(hipGetLastError());
+            size_t tb = 0;
+            PNP_HIP(hipcub::DeviceScan::InclusiveSum(nullptr, tb, head_p, gid_p, (int)n, s));
+            PNP_HIP(hipcub::DeviceScan::InclusiveSum(cub_tmp(tmp, tb), tb, head_p, gid_p, (int)n, s));
+            uint32_t g = 0;
+            PNP_HIP(hipMemcpyAsync(&g, gid_p + n - 1, 4, hipMemcpyDeviceToHost, s));
+            PNP_HIP(hipStreamSynchronize(s));
+            wb.g[4] = g;
+            wb.ident[4] = (uint64_t)g * 10 > 9 * n;  // (not worth a segment: z commits from its evaluations)
+            if (!wb.ident[4]) bases(4, g);
         }
     }
     uint32_t hbad = 0;
     PNP_HIP(hipMemcpyAsync(&hbad, bad, 4, hipMemcpyDeviceToHost, s));
     PNP_HIP(hipStreamSynchronize(s));
-    // worth it only when some wire has far fewer groups than rows
+    // the wires are worth their segments only when some wire has far fewer
+    // groups than rows; z when its runs merge >= 10% of the rows
     bool gain = false;
     for (int j = 0; j < 4; j++) gain |= !wb.ident[j] && wb.g[j] * 4 < 3 * n;
-    if (hbad || !gain) {
+    wb.wires_ok = gain && !hbad;
+    wb.z_ok = !wb.ident[4] && !hbad;
+    if (!wb.wires_ok)
         for (int j = 0; j < 4; j++) {
             wb.grp[j].release();
             wb.rep[j].release();
+            bx[j].release();
         }
-        return;  // wb.ok stays false (kept with its sigma): commit from the evaluations
+    if (!wb.z_ok) {
+        wb.grp[4].release();
+        wb.rep[4].release();
+        bx[4].release();
     }
-    // 4. affine bases of the four segments, one folded table
+    if (!wb.wires_ok && !wb.z_ok) return;  // wb.ok stays false (kept with its sigma): commit from the evaluations
+    // 4. affine bases of the n-slot segments (wires a..d, z), one folded table
     wb.total = 0;
-    for (int j = 0; j < 4; j++) {
+    for (int j = 0; j < 5; j++) {
+        if (j < 4 ? !wb.wires_ok : !wb.z_ok) continue;
         wb.off[j] = wb.total;
-        wb.total += wb.g[j];
-        wb.m = std::max(wb.m, wb.g[j]);
+        wb.total += n;
     }
+    wb.m = n;
     {
         DevBuf xyzz(wb.total * 192), aff(wb.total * 96);
-        for (int j = 0; j < 4; j++) {
-            PNP_HIP(hipMemcpyAsync(xyzz.u64() + 24 * wb.off[j], bx[j].u64(), wb.g[j] * 192, hipMemcpyDeviceToDevice,
-                                   s));
+        for (int j = 0; j < 5; j++) {
+            if (!bx[j].p) continue;
+            PNP_HIP(hipMemcpyAsync(xyzz.u64() + 24 * wb.off[j], bx[j].u64(), n * 192, hipMemcpyDeviceToDevice, s));
         }
         PNP_HIP(hipStreamSynchronize(s));
         for (auto &b : bx) b.release();
@@ -353,15 +425,11 @@ void build_wire_bases(pnp_ctx *ctx, uint64_t n) {
         xyzz.release();
         msm_build_table(wb.table, aff.u64(), wb.total, ctx->msm.fold_c, s);
     }
-    // every MSM of the batch reads `len` scalars: n when a wire is ungrouped
-    // (its evaluations), else the largest group count; a grouped wire's
-    // scalars past its own count stay zero (no entries: the neighbouring
-    // segment is never read)
-    bool any_ident = false;
-    for (int j = 0; j < 4; j++) any_ident |= wb.ident[j];
-    wb.len = any_ident ? n : wb.m;
-    for (int j = 0; j < 4; j++) {
-        if (wb.ident[j]) continue;
+    // every MSM of the batch reads n scalars: an ungrouped wire's evaluations,
+    // a grouped wire's group values at their slots (zero elsewhere)
+    wb.len = n;
+    for (int j = 0; j < 5; j++) {
+        if (wb.ident[j] || !wb.grp[j].p) continue;
         wb.scal[j].alloc(wb.len * 32);
         PNP_HIP(hipMemsetAsync(wb.scal[j].p, 0, wb.len * 32, s));
     }
@@ -392,7 +460,7 @@ bool wire_bases_ready(pnp_ctx *ctx, uint64_t n) {
 void wire_bases_reset(pnp_ctx *ctx) { ctx->wb = pnp_ctx::WireBases{}; }
 
 bool commit_wires_grouped(pnp_ctx *ctx, const uint64_t *const *d_evals, uint64_t n, CommitmentC *const *out) {
-    if (!groups_enabled() || !lagrange_table(ctx, n) || !wire_bases_ready(ctx, n)) return false;
+    if (!groups_enabled() || !lagrange_table(ctx, n) || !wire_bases_ready(ctx, n) || !ctx->wb.wires_ok) return false;
     auto &wb = ctx->wb;
     hipStream_t s = ctx->stream;
     uint32_t *flag = static_cast<uint32_t *>(wb.flag.p);
@@ -430,6 +498,39 @@ bool commit_wires_grouped(pnp_ctx *ctx, const uint64_t *const *d_evals, uint64_t
         memcpy(out[b]->y, &aff[12 * b + 6], 48);
     }
     if (ctx->ktimer.enabled) ctx->ktimer.credit("wire_groups_used", 1);
+    return true;
+}
+
+bool commit_z_grouped(pnp_ctx *ctx, const uint64_t *d_z, uint64_t n, CommitmentC *out) {
+    if (!z_groups_enabled() || !lagrange_table(ctx, n) || !wire_bases_ready(ctx, n) || !ctx->wb.z_ok) return false;
+    auto &wb = ctx->wb;
+    hipStream_t s = ctx->stream;
+    uint32_t *flag = static_cast<uint32_t *>(wb.flag.p);
+    PNP_HIP(hipMemsetAsync(flag, 0, 4, s));
+    WirePtrs wp{};
+    wp.w[0] = d_z;
+    wp.grp[0] = static_cast<const uint32_t *>(wb.grp[4].p);
+    wp.rep[0] = static_cast<const uint32_t *>(wb.rep[4].p);
+    wp.scal[0] = wb.scal[4].u64();
+    hipLaunchKernelGGL(k_wb_gather, dim3(nblk(n), 1), dim3(256), 0, s, wp, n, flag);
+    PNP_HIP(hipGetLastError());
+    uint32_t hflag = 0;
+    PNP_HIP(hipMemcpyAsync(&hflag, flag, 4, hipMemcpyDeviceToHost, s));
+    PNP_HIP(hipStreamSynchronize(s));
+    if (hflag) {  // (a zero denominator: the ratio of a fixed row was not 1)
+        if (ctx->ktimer.enabled) ctx->ktimer.credit("z_group_fallback", 1);
+        return false;
+    }
+    const uint64_t *sc[1] = {wb.scal[4].u64()};
+    MsmSegs segs;
+    segs.n_table = wb.total;
+    segs.off[0] = wb.off[4];
+    uint64_t xyzz[24], aff[12];
+    msm_run_batch(ctx->msm, nullptr, sc, 1, wb.len, xyzz, s, wb.table.u64(), false, &segs);
+    xyzz_to_affine_batch_host(xyzz, 1, aff);
+    memcpy(out->x, aff, 48);
+    memcpy(out->y, aff + 6, 48);
+    if (ctx->ktimer.enabled) ctx->ktimer.credit("z_groups_used", 1);
     return true;
 }
 
