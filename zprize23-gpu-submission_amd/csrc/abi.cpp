@@ -610,6 +610,11 @@ int pnp_load_prover_key(pnp_ctx *ctx, const ProverKeyC *pk, uint64_t D, int devi
                     b.alloc(32 * (uint64_t)ctx->pk_nb * D);
                     pnp::k_to_form29(src, b.u64(), (uint64_t)ctx->pk_nb * D, ctx->stream);
                 }
+                // the 2^256-form blocks only the 32-bit quotient reads (every
+                // proof of this key takes k_quotient29); lin stays for the PI term
+                PNP_HIP(hipStreamSynchronize(ctx->stream));
+                for (const char *nm : names)
+                    if (strcmp(nm, "lin") != 0) ctx->pk_blk.erase(nm);
                 ctx->pk_q29 = true;
             }
         }

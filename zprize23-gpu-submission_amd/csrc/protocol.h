@@ -41,14 +41,14 @@ struct QuotArgs {
 };
 
 // k_quotient29: the quotient of the common case (no custom gates, no lookup,
-// closed-form L1 and at most one PI: the Merkle circuit) in radix-2^29
+// the standard coset: the Merkle circuit) in radix-2^29
 // arithmetic (fr29.cuh).  The arrays marked 2^261 hold values in that
 // Montgomery form (the wire / z LDEs through the scaled twist, lde_blocks
 // form29; key copies made at load); vh_inv, l1v and pinv stay in the 2^256
 // form, so the final products return the quotient to it.  Constants: nine
 // 29-bit limbs of their 2^261 forms (fr_to_r29_limbs).
 struct Quot29Args {
-    const uint64_t *w8[4], *z8;                                                  // 2^261
+    const uint64_t *w8[4], *z8, *pi8;  // 2^261 (pi8: several PIs, nullptr otherwise)
     const uint64_t *q_m, *q_l, *q_r, *q_o, *q_4, *q_c, *q_hl, *q_hr, *q_h4, *q_arith;  // 2^261
     const uint64_t *sig[4], *lin;                                                // 2^261
     const uint64_t *vh_inv, *l1v, *pinv;                                         // 2^256

@@ -362,6 +362,7 @@ __global__ __launch_bounds__(256, 4) void k_quotient29_(Quot29Args q, uint64_t N
     acc = r29_add(acc, r29_mul(pow5_29(d), ld29(q.q_h4, i)));
     acc = r29_add(acc, ld29(q.q_c, i));
     R29 num = r29_mul(acc, ld29(q.q_arith, i));
+    if (q.pi8) num = r29_add(num, ld29(q.pi8, i));  // several PIs: their LDE (one PI: closed form below)
     // permutation (proof_system/permutation.cu:267-296), x beta k_j by doublings
     const R29 beta = c29(q.beta), gamma = c29(q.gamma);
     const R29 xb = r29_mul(ld29(q.lin, i), beta);

@@ -219,13 +219,13 @@ int prove_impl(pnp_ctx *ctx, const CircuitC *cs, int device_ptrs, ProofC *out, c
         return v < 6 ? 6 : v > 8 ? 8 : v;
     }();
     int nbq = dist ? nb : quot_blocks;  // blocks this round-4 attempt covers
-    // The quotient of the common case (no custom gates, no lookup, closed
-    // forms, <= 1 PI: the Merkle circuit) runs in radix 2^29 (protocol.h
-    // k_quotient29): its wire and z LDEs are taken in the 2^261 form (the
-    // scaled twist, free) and the key arrays it reads come from the copies
-    // made at key load; any other circuit keeps k_quotient_ (PNP_QUOT29=0:
-    // always)
-    const bool q29 = ctx->pk_q29 && pi_pos.size() <= 1;
+    // The quotient of the common case (no custom gates, no lookup, the
+    // standard coset: the Merkle circuit) runs in radix 2^29 (protocol.h
+    // k_quotient29): its wire, z (and multi-PI) LDEs are taken in the 2^261
+    // form (the scaled twist, free) and the key arrays it reads are the
+    // 2^261-form copies made at key load; any other key keeps k_quotient_
+    // (PNP_QUOT29=0: every key)
+    const bool q29 = ctx->pk_q29;
     auto lde_on = [&](hipStream_t st, const uint64_t *coeffs, uint64_t *dst, bool f29) {
         lde_blocks(nt, coeffs, dst, lg, mb0, nbq, st, f29);
     };
@@ -487,7 +487,7 @@ int prove_impl(pnp_ctx *ctx, const CircuitC *cs, int device_ptrs, ProofC *out, c
             q.c_pi = pi_val[0] * pow_u64(root_of_unity(lg), pi_pos[0]) * n_inv;
         } else if (pi_poly) {
             uint64_t *pi8 = ctx->buf("pi8", NB);
-            lde(pi_poly, pi8);
+            lde_on(s, pi_poly, pi8, q29);
             q.pi8 = pi8;
         }
         q.z28 = nullptr;  // z2 = 1: its quotient terms cancel (protocol.h)
@@ -574,6 +574,7 @@ int prove_impl(pnp_ctx *ctx, const CircuitC *cs, int device_ptrs, ProofC *out, c
             Quot29Args q2;
             for (int j = 0; j < 4; j++) q2.w8[j] = q.w8[j];
             q2.z8 = q.z8;
+            q2.pi8 = q.pi8;
             q2.q_m = ctx->blk29("q_m");
             q2.q_l = ctx->blk29("q_l");
             q2.q_r = ctx->blk29("q_r");
@@ -602,6 +603,10 @@ int prove_impl(pnp_ctx *ctx, const CircuitC *cs, int device_ptrs, ProofC *out, c
                 return PNP_E_ARG;
             }
             k_quotient29(q2, NBq, t_blk, s);
+            // (the byte accounting below counts the arrays this kernel read)
+            q.q_m = q2.q_m, q.q_l = q2.q_l, q.q_r = q2.q_r, q.q_o = q2.q_o, q.q_4 = q2.q_4, q.q_c = q2.q_c;
+            q.q_hl = q2.q_hl, q.q_hr = q2.q_hr, q.q_h4 = q2.q_h4, q.q_arith = q2.q_arith, q.lin = q2.lin;
+            for (int j = 0; j < 4; j++) q.sig[j] = q2.sig[j];
         } else {
             k_quotient(q, NBq, t_blk, s);
         }
