@@ -4,6 +4,7 @@
 // plonk-core/src/lib.rs:237-239): structs by value, ProofC by value,
 // synchronous, device 0, print-and-exit on device errors (caffe/common.hpp:
 // 23-30).  v2 functions return PNP_* codes and never exit.
+#include <algorithm>
 #include <stdarg.h>
 #include <stdlib.h>
 #include <string.h>
@@ -468,7 +469,10 @@ int pnp_load_prover_key(pnp_ctx *ctx, const ProverKeyC *pk, uint64_t D, int devi
         PNP_HIP(hipSetDevice(ctx->device));
         ctx->pk_loaded = false;
         ctx->pk_gen++;  // derived groups (wires.hip) re-check sigma
-        ctx->pk_owned.clear();
+        // device copies are kept across loads and reused when a field's size is
+        // unchanged (the v1 symbol reloads every call: no hipMalloc / hipFree of
+        // ~20 GiB per call)
+        ctx->pk_owned.resize(44);
         ProverKeyC dev{};
         uint64_t *const *src = reinterpret_cast<uint64_t *const *>(pk);
         uint64_t **dst = reinterpret_cast<uint64_t **>(&dev);
@@ -488,19 +492,23 @@ int pnp_load_prover_key(pnp_ctx *ctx, const ProverKeyC *pk, uint64_t D, int devi
         for (int f = 0; f < 44; f++) {
             FieldKind k = kPkKinds[f];
             dst[f] = nullptr;
-            if (k == kSkip || ((k == kSelEvals8 || k == kSelCoeffs) && !sel_nz[f])) continue;
+            if (k == kSkip || ((k == kSelEvals8 || k == kSelCoeffs) && !sel_nz[f])) {
+                ctx->pk_owned[f].release();
+                continue;
+            }
             uint64_t elems = (k == kEvals8 || k == kSelEvals8) ? 8 * D : D;
             if (!src[f]) {
                 set_error("prover key field %d is null", f);
                 throw Error(PNP_E_ARG);
             }
             if (device_ptrs) {
+                ctx->pk_owned[f].release();
                 dst[f] = src[f];
             } else {
-                ctx->pk_owned.emplace_back(elems * 32);
-                PNP_HIP(hipMemcpyAsync(ctx->pk_owned.back().p, src[f], elems * 32,
-                                       hipMemcpyHostToDevice, ctx->stream));
-                dst[f] = ctx->pk_owned.back().u64();
+                auto &o = ctx->pk_owned[f];
+                if (o.bytes != elems * 32) o.alloc(elems * 32);
+                PNP_HIP(hipMemcpyAsync(o.p, src[f], elems * 32, hipMemcpyHostToDevice, ctx->stream));
+                dst[f] = o.u64();
             }
         }
         // key-derived constants, computed once per key instead of per proof:
@@ -529,18 +537,21 @@ int pnp_load_prover_key(pnp_ctx *ctx, const ProverKeyC *pk, uint64_t D, int devi
         // reference's preprocessing), the L1 and PI coset evaluations have the
         // closed forms of protocol.h and need no LDE per proof
         const uint64_t N8 = 8 * D;
-        pnp::DevBuf vh_inv(32 * N8), l1v;
+        auto tmp = [&](int k) -> pnp::DevBuf & {  // per-load scratch, kept for the next load
+            if (ctx->pk_tmp[k].bytes != 32 * N8) ctx->pk_tmp[k].alloc(32 * N8);
+            return ctx->pk_tmp[k];
+        };
+        pnp::DevBuf &vh_inv = tmp(0), &l1v = tmp(1);
         PNP_HIP(hipMemcpyAsync(vh_inv.p, dev.v_h_coset_8n, 32 * N8, hipMemcpyDeviceToDevice,
                                ctx->stream));
         pnp::k_batch_inverse(vh_inv.u64(), N8, ctx->scratch_a, ctx->stream);
         {
-            pnp::DevBuf vh(32 * N8), x(32 * N8);
+            pnp::DevBuf &vh = tmp(2), &x = tmp(3);
             pnp::k_coset_consts(vh.u64(), x.u64(), lg, ctx->stream);
             ctx->pk_std_coset =
                 !pnp::k_any_diff(vh.u64(), dev.v_h_coset_8n, 4 * N8, ctx->scratch_b, ctx->stream) &&
                 !pnp::k_any_diff(x.u64(), dev.linear_evaluations, 4 * N8, ctx->scratch_b, ctx->stream);
             if (ctx->pk_std_coset) {
-                l1v.alloc(32 * N8);
                 pnp::k_affine(l1v.u64(), x.u64(), Fr::one(), pnp::neg(Fr::one()), N8, ctx->stream);
                 pnp::k_batch_inverse(l1v.u64(), N8, ctx->scratch_a, ctx->stream);
                 Fr nf = Fr::zero();
@@ -558,11 +569,39 @@ int pnp_load_prover_key(pnp_ctx *ctx, const ProverKeyC *pk, uint64_t D, int devi
         const bool split = world > 1 && 8 % world == 0 && ctx->msm.alltoall;
         ctx->pk_nb = split ? 8 / world : 8;
         ctx->pk_mb0 = split ? ctx->msm.rank * ctx->pk_nb : 0;
-        ctx->pk_blk.clear();
-        auto blk = [&](const char *name, const uint64_t *src) {
-            auto &b = ctx->pk_blk[name];
-            b.alloc(32 * (uint64_t)ctx->pk_nb * D);
+        // k_quotient29's keys (protocol.h): no custom gate, no lookup selector
+        // or table, the standard coset; their selector / sigma / lin blocks are
+        // kept in the 2^261 form (pk_blk29) and, but lin (the PI term), not in
+        // the 2^256 form at all
+        bool q29 = false;
+        {
+            static const bool q29_on = [] {
+                const char *e = getenv("PNP_QUOT29");
+                return !e || atoi(e) != 0;
+            }();
+            q29 = q29_on && ctx->pk_std_coset && ctx->pk_qlookup_zero && !ctx->pk_custom_nz[0] &&
+                  !ctx->pk_custom_nz[1] && !ctx->pk_custom_nz[2] && !ctx->pk_custom_nz[3];
+            const uint64_t *tabs[4] = {dev.table1, dev.table2, dev.table3, dev.table4};
+            for (int k = 0; k < 4 && q29; k++)
+                q29 = !tabs[k] || !pnp::k_any_nonzero(tabs[k], 4 * D, ctx->scratch_b, ctx->stream);
+        }
+        std::vector<std::string> used, used29;
+        const uint64_t blk_elems = (uint64_t)ctx->pk_nb * D;
+        auto put = [&](std::map<std::string, pnp::DevBuf> &m, std::vector<std::string> &u, const char *name,
+                       const uint64_t *src, bool form29) {
+            auto &b = m[name];
+            if (b.bytes != 32 * blk_elems) b.alloc(32 * blk_elems);
             pnp::to_blocks(src, b.u64(), lg, ctx->pk_mb0, ctx->pk_nb, ctx->stream);
+            if (form29) pnp::k_to_form29(b.u64(), b.u64(), blk_elems, ctx->stream);  // elementwise, in place
+            u.push_back(name);
+        };
+        auto blk = [&](const char *name, const uint64_t *src) {
+            static const char *const names29[] = {"q_m", "q_l", "q_r", "q_o", "q_4", "q_c", "q_hl", "q_hr",
+                                                  "q_h4", "q_arith", "sig0", "sig1", "sig2", "sig3", "lin"};
+            bool in29 = false;
+            for (const char *nm : names29) in29 |= strcmp(nm, name) == 0;
+            if (q29 && in29) put(ctx->pk_blk29, used29, name, src, true);
+            if (!(q29 && in29) || strcmp(name, "lin") == 0) put(ctx->pk_blk, used, name, src, false);
         };
         if (!ctx->pk_qm_zero) blk("q_m", dev.q_m_evals);
         if (!ctx->pk_qlookup_zero) blk("q_lookup", dev.q_lookup_evals);
@@ -586,38 +625,14 @@ int pnp_load_prover_key(pnp_ctx *ctx, const ProverKeyC *pk, uint64_t D, int devi
         blk("lin", dev.linear_evaluations);
         blk("vh_inv", vh_inv.u64());
         if (ctx->pk_std_coset) blk("l1v", l1v.u64());
-        // k_quotient29's copies (2^261 form) for keys of its class: no custom
-        // gate, no lookup selector or table, the standard coset
-        ctx->pk_blk29.clear();
-        ctx->pk_q29 = false;
-        {
-            static const bool q29_on = [] {
-                const char *e = getenv("PNP_QUOT29");
-                return !e || atoi(e) != 0;
-            }();
-            bool ok = q29_on && ctx->pk_std_coset && ctx->pk_qlookup_zero && !ctx->pk_custom_nz[0] &&
-                      !ctx->pk_custom_nz[1] && !ctx->pk_custom_nz[2] && !ctx->pk_custom_nz[3];
-            const uint64_t *tabs[4] = {dev.table1, dev.table2, dev.table3, dev.table4};
-            for (int k = 0; k < 4 && ok; k++)
-                ok = !tabs[k] || !pnp::k_any_nonzero(tabs[k], 4 * D, ctx->scratch_b, ctx->stream);
-            if (ok) {
-                const char *names[] = {"q_m", "q_l", "q_r", "q_o", "q_4", "q_c", "q_hl", "q_hr", "q_h4", "q_arith",
-                                       "sig0", "sig1", "sig2", "sig3", "lin"};
-                for (const char *nm : names) {
-                    const uint64_t *src = ctx->blk(nm);
-                    if (!src) continue;
-                    auto &b = ctx->pk_blk29[nm];
-                    b.alloc(32 * (uint64_t)ctx->pk_nb * D);
-                    pnp::k_to_form29(src, b.u64(), (uint64_t)ctx->pk_nb * D, ctx->stream);
-                }
-                // the 2^256-form blocks only the 32-bit quotient reads (every
-                // proof of this key takes k_quotient29); lin stays for the PI term
-                PNP_HIP(hipStreamSynchronize(ctx->stream));
-                for (const char *nm : names)
-                    if (strcmp(nm, "lin") != 0) ctx->pk_blk.erase(nm);
-                ctx->pk_q29 = true;
-            }
-        }
+        // blocks of an earlier key this one does not have
+        auto prune = [](std::map<std::string, pnp::DevBuf> &m, const std::vector<std::string> &u) {
+            for (auto it = m.begin(); it != m.end();)
+                it = std::find(u.begin(), u.end(), it->first) == u.end() ? m.erase(it) : std::next(it);
+        };
+        prune(ctx->pk_blk, used);
+        prune(ctx->pk_blk29, used29);
+        ctx->pk_q29 = q29;
         ctx->pk_blk_rank = ctx->msm.rank;
         ctx->pk_blk_world = world;
         ctx->pk_pinv.release();

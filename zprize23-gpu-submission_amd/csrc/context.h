@@ -21,11 +21,12 @@ struct pnp_ctx {
     // ---- resident prover key (ProverKeyC mirrored in HBM) ----
     bool pk_loaded = false;
     uint64_t pk_n = 0;                     // domain size D
-    std::vector<pnp::DevBuf> pk_owned;     // copies (device_ptrs == 0)
+    std::vector<pnp::DevBuf> pk_owned;     // copies (device_ptrs == 0), by ProverKeyC field
     ProverKeyC pk_dev{};                   // HBM pointers for every field
     bool pk_qm_zero = false, pk_qlookup_zero = false;  // all-zero 8n selector evaluations
     bool pk_custom_nz[4] = {};  // range, logic, fixed-base, curve-add selectors non-zero
     pnp::DevBuf pk_sigma_n[4];             // sigma evaluations on the n-domain
+    pnp::DevBuf pk_tmp[4];                 // key-load scratch (8n Fr each), kept for the next load
     // The quotient's 8n-point arrays in block layout (ntt.hip: point 8j + m
     // -> block m, index j), blocks pk_mb0 .. pk_mb0 + pk_nb - 1 only:
     // q_* selectors, sig0..3, lin (coset points) and the proof-independent
