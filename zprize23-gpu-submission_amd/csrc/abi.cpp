@@ -633,6 +633,14 @@ int pnp_load_prover_key(pnp_ctx *ctx, const ProverKeyC *pk, uint64_t D, int devi
         prune(ctx->pk_blk, used);
         prune(ctx->pk_blk29, used29);
         ctx->pk_q29 = q29;
+        // the coset-constant scratch (4 x 8n Fr) is kept only for callers that
+        // load keys from host memory again and again (the v1 symbol); a
+        // device-resident key is loaded once (and ranks sharing a GPU need the
+        // HBM)
+        if (device_ptrs) {
+            PNP_HIP(hipStreamSynchronize(ctx->stream));
+            for (auto &b : ctx->pk_tmp) b.release();
+        }
         ctx->pk_blk_rank = ctx->msm.rank;
         ctx->pk_blk_world = world;
         ctx->pk_pinv.release();
