@@ -167,6 +167,7 @@ class Synthetic:
 # product spends 392).  The issue-model ceiling (tools/isa_model.py: 19,761
 # SIMD cycles per 64 additions of the compiled code) is kept as a secondary.
 FQ_PRODUCTS_PER_MADD = 10
+ALG_BYTES_PER_ENTRY = 96 + 4
 MADS_PER_FQ_PRODUCT = 288
 MADD_ISSUE_CYCLES = 19761
 SIMDS, CLOCK_HZ = 256 * 4, 2.4e9
@@ -200,21 +201,6 @@ def pmc_traffic():
         return None
 
 
-CPU_SCALING_FILE = os.path.join(REPO, "profiles", "r03_cpu_scaling_box.json")
-
-
-def cpu_scaling():
-    """The CPU restatement's gen_proof on the Merkle circuit measured on a GPU
-    box's host (tools/cpu_scaling.py --circuit merkle on the box: 2^16 .. 2^20
-    and the full 2^22 instance): the fitted exponent b of t = a n^b and the
-    measured 2^22 time, or None."""
-    try:
-        with open(CPU_SCALING_FILE) as f:
-            return json.load(f)
-    except (OSError, ValueError):
-        return None
-
-
 def host_copy(syn):
     """(CircuitC, ProverKeyC, CommitKeyC) over host copies of bench.Synthetic's
     device arrays, as the Rust caller hands them over (prover.rs:727-901), +
@@ -243,44 +229,82 @@ def host_copy(syn):
     return cs_h, pk_h, ck_h, host
 
 
-def cpu_baseline(ctx, lg: int, circuit: str):
-    """Time the CPU restatement (oracle/, test infrastructure; OpenMP on all
-    host threads) on one bounded gen_proof of the bench's own circuit at
-    n = 2^lg: the instance is bench.Synthetic's (generated on the GPU, copied to
-    host memory, generation not timed); its proof must equal the GPU's.  Rank 0
-    at N = 1 only, after the timed region."""
+def host_cpu():
+    """The host's CPU model and the CPUs this process may run on."""
+    model = ""
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        usable = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        usable = os.cpu_count()
+    return {"model": model, "nproc": os.cpu_count(), "usable": usable,
+            "omp_num_threads": os.environ.get("OMP_NUM_THREADS")}
+
+
+def cpu_baseline(ctx, lg: int, circuit: str, syn=None, gpu_proof=None):
+    """Time the CPU restatement (oracle/, test infrastructure; OpenMP on the
+    host threads OMP_NUM_THREADS allows) on one gen_proof of the bench's own
+    circuit at n = 2^lg, in the same run as the GPU measurement.
+    At the bench's own size (the default, HEIGHT = 15) it proves the SAME
+    instance the GPU just proved (`syn`, copied to host memory, not timed) and
+    its proof must equal the GPU's timed proof; a smaller lg generates a
+    smaller instance of the same circuit.  Rank 0 at N = 1 only, after the
+    timed region."""
     sys.path.insert(0, os.path.join(REPO, "tests"))
     import torch
     from pnp import abi
     from pnp_testlib import oracle
     lib = oracle()
-    syn = Synthetic(ctx, lg, int(HEIGHT15_GATES / (1 << 22) * (1 << lg)), seed=1, circuit=circuit)
+    own = syn is None or syn.lg_n != lg
+    if own:
+        syn = Synthetic(ctx, lg, int(HEIGHT15_GATES / (1 << 22) * (1 << lg)), seed=1, circuit=circuit)
+        gpu_proof = prove_resident(ctx, syn)
     cs_h, pk_h, ck_h, keep = host_copy(syn)
-    gpu = prove_resident(ctx, syn)
-    out = abi.ProofC()
-    t0 = time.perf_counter()
-    rc = lib.or_gen_proof(C.byref(cs_h), C.byref(pk_h), C.byref(ck_h), C.byref(out))
-    dt = time.perf_counter() - t0
-    del keep, syn
+    if own:
+        del syn
     torch.cuda.empty_cache()
-    res = {"value": round(dt, 3), "unit": f"s per gen_proof at n=2^{lg}",
-           "cores": int(lib.or_num_threads()), "kind": "port",
-           "sample": (f"one gen_proof of the bench's {circuit} circuit at n=2^{lg}"
-                      + (f" (HEIGHT={lg - 7} Poseidon Merkle tree)" if circuit == "merkle" else "")
-                      + " with the C restatement (oracle/, OpenMP); instance generated on the GPU and "
-                        "copied to host memory (not timed)"),
-           "equals_gpu_proof": rc == 0 and abi.proof_to_bytes(out) == abi.proof_to_bytes(gpu)}
-    sc = cpu_scaling()
-    if sc and sc.get("circuit") == circuit:
-        b = float(sc["fit"]["exponent"])
-        res["extrapolated_full_s"] = round(dt * (2.0 ** ((22 - lg) * b)), 1)
-        res["extrapolation"] = (f"t ~ n^{b:.3f} fitted on the box's host over "
-                                f"{[p['lg'] for p in sc['points']]} ({os.path.relpath(CPU_SCALING_FILE, REPO)})")
-        full = [p for p in sc["points"] if p["lg"] == 22]
-        if full:
-            res["measured_full_s"] = full[0]["seconds"]
-            res["measured_full_cores"] = sc.get("threads")
-    return res
+    out = abi.ProofC()
+    res = {}
+
+    def run():  # ctypes releases the GIL: the main thread reports progress
+        t = time.perf_counter()
+        res["rc"] = lib.or_gen_proof(C.byref(cs_h), C.byref(pk_h), C.byref(ck_h), C.byref(out))
+        res["dt"] = time.perf_counter() - t
+
+    import threading
+    th = threading.Thread(target=run)
+    t0 = time.perf_counter()
+    th.start()
+    while th.is_alive():
+        th.join(30)
+        if th.is_alive():
+            log(f"cpu baseline: {time.perf_counter() - t0:.0f} s")
+    rc, dt = res.get("rc", -1), res.get("dt", 0.0)
+    del keep
+    cpu = host_cpu()
+    return {"value": round(dt, 3), "unit": f"s per gen_proof at n=2^{lg}",
+            "cores": int(lib.or_num_threads()), "kind": "port",
+            "host": cpu,
+            "sample": (f"one gen_proof of the bench's {circuit} circuit at n=2^{lg}"
+                       + (f" (HEIGHT={lg - 7} Poseidon Merkle tree, {syn_gates(lg, circuit)} gates)"
+                          if circuit == "merkle" else "")
+                       + (", the same instance as the timed GPU proofs" if not own else
+                          ", a smaller instance of the same circuit")
+                       + "; C restatement of the ZK-Garage prover (oracle/, OpenMP, "
+                         f"{int(lib.or_num_threads())} threads on {cpu['model'] or 'the host CPU'}); "
+                         "inputs copied to host memory before timing"),
+            "equals_gpu_proof": rc == 0 and abi.proof_to_bytes(out) == abi.proof_to_bytes(gpu_proof)}
+
+
+def syn_gates(lg: int, circuit: str) -> int:
+    return 193 * ((1 << (lg - 8)) - 1) + 5 if circuit == "merkle" else int(HEIGHT15_GATES / (1 << 22) * (1 << lg))
 
 
 def prove_resident(ctx, syn):
@@ -407,7 +431,9 @@ def main():
     ap.add_argument("--circuit", default="merkle", choices=("merkle", "arith"),
                     help="merkle: the reference's Poseidon Merkle circuit (HEIGHT = lg - 7); "
                          "arith: a random satisfying arithmetic circuit of --gates gates")
-    ap.add_argument("--cpu-lg", type=int, default=18, help="CPU baseline sample size; 0 = skip")
+    ap.add_argument("--cpu-lg", type=int, default=22,
+                    help="CPU baseline size (default: the bench's own HEIGHT=15 instance, ~150 s on 16 "
+                         "host threads); 0 = skip")
     ap.add_argument("--no-verify", action="store_true", help="skip the proof check after the timed region")
     ap.add_argument("--solo", default="", metavar="R/W",
                     help="time rank R's share of a W-GPU proof alone on this GPU (loopback exchanges, "
@@ -476,16 +502,24 @@ def main():
     torch.cuda.synchronize()
     ctx.sync()
     t0 = time.perf_counter()
+    proofs = []
     for _ in range(args.steps):
-        proof = ctx.prove(syn.cs, device_ptrs=True)
+        proofs.append(ctx.prove(syn.cs, device_ptrs=True))
     ctx.sync()
     torch.cuda.synchronize()
     barrier()
     elapsed = time.perf_counter() - t0
     stages = ctx.stage_times()
+    from pnp import abi
+    proof = proofs[-1]
+    # every timed proof must be the same (the reference harness checks each
+    # proof it times, benches/pnp_bench.rs:124-135; the instance is fixed and
+    # the prover deterministic, so all equal the first, which is verified below)
+    all_equal = all(abi.proof_to_bytes(p) == abi.proof_to_bytes(proofs[0]) for p in proofs)
     acc_ms, acc_n = ctx.kernel_stats("msm_accumulate")
-    acc_bytes = ctx.kernel_bytes("msm_accumulate")
-    entries = ctx.kernel_bytes("msm_entries")
+    entries = ctx.kernel_bytes("msm_entries")          # real sorted entries, counted on the device
+    madds = ctx.kernel_bytes("msm_madds")              # real mixed additions (entries - fresh pieces)
+    dense = ctx.kernel_bytes("msm_entries_dense")      # the dense bound (MSMs x windows x points)
     q_ms, q_n = ctx.kernel_stats("quotient")
     q_bytes = ctx.kernel_bytes("quotient")
     redo_lanes = ctx.kernel_bytes("msm_redo_lanes")
@@ -502,18 +536,27 @@ def main():
             f"quotient: {q_n} launches, {q_ms / max(q_n, 1):.3f} ms avg")
     if rank == 0:
         acc_avg_s = acc_ms / max(acc_n, 1) / 1e3
-        # algorithmic bytes per launch (library-credited: points x windows the
-        # launch swept x 128 B) / average launch duration
-        achieved = acc_bytes / (acc_ms / 1e3) / 1e9 if acc_ms > 0 else 0.0
-        # mixed additions = sorted (point, window) entries, counted by the library
-        madds_per_s = entries / (acc_ms / 1e3) if acc_ms > 0 else 0.0
+        acc_s = acc_ms / 1e3
+        # the dominant kernel's real work: mixed additions counted on the device
+        # from the bucket starts of every timed launch (k_count_pieces), per
+        # second of its launches (HIP events on the library stream)
+        madds_per_s = madds / acc_s if acc_s > 0 else 0.0
         valu_peak = SIMDS * CLOCK_HZ * 64 / MADD_ISSUE_CYCLES
         mad_rate = SIMDS * CLOCK_HZ * 64 / mad_cycles()          # v_mad_u64_u32 / s
         fq_peak = mad_rate / MADS_PER_FQ_PRODUCT                 # Fq products / s
         fq_achieved = madds_per_s * FQ_PRODUCTS_PER_MADD
+        # algorithmic bytes: each sorted entry gathers one affine point (96 B)
+        # and reads its 4-B index (the reference's per-entry model,
+        # pippenger.cuh:147-223)
+        alg_per_launch = entries * ALG_BYTES_PER_ENTRY / max(acc_n, 1)
+        achieved = entries * ALG_BYTES_PER_ENTRY / acc_s / 1e9 if acc_s > 0 else 0.0
         # the PMC traffic was measured on the default single-GPU workload only
         traffic = pmc_traffic() if (world == 1 and not solo and args.lg == 22 and args.circuit == "merkle") else None
         q_gbs = q_bytes / (q_ms / 1e3) / 1e9 if q_ms > 0 else 0.0
+        held = madds_per_s / (valu_peak * HELD_CLOCK_GHZ * 1e9 / CLOCK_HZ)
+        if held > 1.0:
+            log(f"bench: WARNING k_accumulate29 at {held:.3f} of its issue ceiling at the held clock: "
+                "the work count is too high")
         out = {
             "metric": METRIC,
             "value": round(per_proof, 4),
@@ -538,34 +581,47 @@ def main():
                                        if world > 1 else
                                        f"solo rank {solo.rank} of {solo.world} (loopback exchanges, "
                                        f"proof discarded)" if solo else "single")},
+            "timed_proofs_identical": all_equal,
             "roofline": {"bound": "valu", "kernel": "k_accumulate29 (MSM bucket accumulation)",
                          "achieved": round(fq_achieved / 1e9, 2), "peak": round(fq_peak / 1e9, 2),
                          "unit": "G Fq-mul/s", "frac": round(fq_achieved / fq_peak, 4),
                          "traffic": traffic,
-                         "traffic_over_algorithmic": (round(traffic / (acc_bytes / max(acc_n, 1)), 2)
-                                                      if traffic and acc_bytes else None),
-                         "work": "library-counted mixed additions x 10 Fq products (8M+2S) / "
-                                 "average launch duration (HIP events on the library stream)",
+                         "traffic_over_algorithmic": (round(traffic / alg_per_launch, 3)
+                                                      if traffic and alg_per_launch else None),
+                         "work": "mixed additions counted on the device per timed launch (sorted entries "
+                                 "minus the pieces lanes start fresh, k_count_pieces) x 10 Fq products "
+                                 "(8M+2S) / summed launch duration (HIP events on the library stream)",
                          "peak_basis": f"{mad_cycles():.2f} cycles per wave64 v_mad_u64_u32 per "
                                        f"SIMD (profiles/r02_ubench_ops.txt) x 1024 SIMDs x 2.4 GHz "
                                        f"/ {MADS_PER_FQ_PRODUCT} mads per Fq product",
+                         "launches": acc_n,
                          "launch_ms": round(acc_avg_s * 1e3, 3),
-                         "bytes_per_launch": round(acc_bytes / max(acc_n, 1)),
+                         "entries_per_launch": round(entries / max(acc_n, 1)),
+                         "madds_per_launch": round(madds / max(acc_n, 1)),
+                         "madds_per_proof": round(madds / args.steps),
                          "madds_per_s": round(madds_per_s / 1e9, 3),
                          "issue_model": {"peak_gmadd_s": round(valu_peak / 1e9, 3),
                                          "frac": round(madds_per_s / valu_peak, 4),
                                          "basis": "tools/isa_model.py: 19,761 SIMD cycles per 64 "
                                                   "mixed additions of the compiled kernel",
                                          "held_clock_ghz": HELD_CLOCK_GHZ,
-                                         "frac_at_held_clock": round(
-                                             madds_per_s / (valu_peak * HELD_CLOCK_GHZ * 1e9 / CLOCK_HZ), 4),
+                                         "frac_at_held_clock": round(held, 4),
+                                         "exceeds_ceiling": held > 1.0,
                                          "held_clock_basis": "GRBM_GUI_ACTIVE / 8 XCDs / kernel time "
                                                              "(profiles/r02_pmc_clock.txt)"},
+                         "dense_equivalent": {
+                             "entries_per_launch": round(dense / max(acc_n, 1)),
+                             "gmadd_s": round(dense / acc_s / 1e9, 3) if acc_s > 0 else 0.0,
+                             "note": "MSMs x windows x points per launch: the work a dense Pippenger "
+                                     "over the same MSMs does (zero digits, copy groups and padding "
+                                     "rows drop out of the real count); not the kernel's work"},
                          "redo_lanes_per_proof": round(redo_lanes / args.steps, 2),
                          "exact_fallbacks_per_proof": round(exact_fallbacks / args.steps, 2),
                          "hbm": {"achieved_gbs": round(achieved, 1), "peak_gbs": HBM_PEAK_GBS,
                                  "frac": round(achieved / HBM_PEAK_GBS, 5),
-                                 "basis": "algorithmic bytes n*(96+32) per window sweep"},
+                                 "algorithmic_bytes_per_launch": round(alg_per_launch),
+                                 "basis": f"{ALG_BYTES_PER_ENTRY} B per sorted entry (one 96-B affine "
+                                          "point + its 4-B index) x real entries"},
                          "quotient": {"bound": "hbm", "achieved": round(q_gbs, 1),
                                       "peak": HBM_PEAK_GBS, "frac": round(q_gbs / HBM_PEAK_GBS, 4),
                                       "launch_ms": round(q_ms / max(q_n, 1), 3)}},
@@ -583,17 +639,14 @@ def main():
                                    "(their xGMI time is not included)"}
         if not args.no_verify:
             chk = check_proof(syn, proof, args.circuit)
-            out["verified"] = chk.pop("verified")
+            out["verified"] = chk.pop("verified") and all_equal
             out["verification"] = chk
             log(f"proof check: {out['verified']} {chk}")
         if args.drop_in and world == 1:
             out["drop_in"] = drop_in(ctx, syn, args.steps, v1=args.drop_in == "v1")
         if args.cpu_lg and world == 1:  # the CPU baseline: rank 0 at N = 1 only
-            del syn
-            import torch
-            torch.cuda.empty_cache()
             try:
-                out["cpu_baseline"] = cpu_baseline(ctx, args.cpu_lg, args.circuit)
+                out["cpu_baseline"] = cpu_baseline(ctx, args.cpu_lg, args.circuit, syn, proofs[0])
             except Exception as e:  # the CPU leg must never hide the GPU number
                 out["cpu_baseline"] = {"error": repr(e)}
         print(json.dumps(out), flush=True)

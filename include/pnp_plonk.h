@@ -381,6 +381,16 @@ int pnp_commit_ck(pnp_ctx *ctx, const uint64_t *d_scalars, uint64_t n, Commitmen
  * PNP_E_ARG when the basis is unavailable (PNP_LAGRANGE=0, degenerate key).  */
 int pnp_commit_evals(pnp_ctx *ctx, const uint64_t *d_evals, uint64_t n, CommitmentC *out);
 
+/* Extension (operator form of gen_proof's copy-group commitments, wires.hip):
+ * B <= 16 MSMs over sub-ranges of ONE base set — out[b] = sum_{i<n}
+ * s_b[i] P[seg_off[b] + i] over the n_points affine points d_points (12 u64
+ * each, Montgomery) — through one folded table built over all n_points (the
+ * segmented batch of the round-1 wire commitments; each MSM's entries carry its
+ * segment offset).  seg_off[b] + n <= n_points.  Single GPU.  Synchronous.  */
+int pnp_commit_segments(pnp_ctx *ctx, const uint64_t *d_points, uint64_t n_points, int B,
+                        const uint64_t *seg_off, const uint64_t *const *d_scalars, uint64_t n,
+                        CommitmentC *out);
+
 /* evaluate (function.cu:162-173): sum_i c_i x^i; x and result Montgomery,
  * host-side scalars.  Synchronous. */
 int pnp_poly_eval(pnp_ctx *ctx, const uint64_t *d_coeffs, uint64_t n,

@@ -342,3 +342,70 @@ def test_proof_infinity_mask_of_gpu_proof():
         assert not flags["f_comm"] and not flags["h_1_comm"] and not flags["h_2_comm"]
     finally:
         ctx.close()
+
+
+# ---- small-n matrix: every MSM entry point at the sizes
+# where the per-window layout has more virtual windows (B W = 64 at n = 1,
+# c = 4) than the 16 per-MSM segment slots of KeyRows — the r03v illegal
+# memory access ("Fault record") — and the segmented copy-group
+# batch at B = 1 and B = 4, all against the oracle's Pippenger (oracle/g1.c).
+def _srs_host(n, seed):
+    rng = np.random.default_rng(seed)
+    tau = rand_fr_mont_arr(rng, 1)
+    pts = np.zeros((n, 12), dtype=np.uint64)
+    oracle().or_srs(vp(pts), n, vp(tau))
+    return pts
+
+
+def _oracle_commit(pts, sc):
+    exp = np.zeros(12, dtype=np.uint64)
+    oracle().or_commit(vp(np.ascontiguousarray(pts)), vp(np.ascontiguousarray(sc)), len(sc), vp(exp))
+    return exp
+
+
+@pytest.mark.parametrize("n", [1, 2, 3, 17])
+def test_msm_small_n_matrix(ctx, n):
+    rng = np.random.default_rng(1000 + n)
+    pts = _srs_host(4 * n + 7, n)
+    sc = rand_fr_mont_arr(rng, n)
+    if n > 2:
+        sc[1] = 0
+    exp = _oracle_commit(pts[:n], sc)
+    assert (_commit_dev(ctx, pts[:n].copy(), sc) == exp).all(), "pnp_commit (per-window layout)"
+    assert (_commit_ck(ctx, pts[:n].copy(), sc) == exp).all(), "pnp_commit_ck (folded layout)"
+    # the segmented batch: B = 1, then B = 4 sub-ranges of one base set
+    dp = to_dev(pts)
+    for offs in ([3], [0, n, 2 * n + 1, 3 * n + 7]):
+        scs = [rand_fr_mont_arr(rng, n) for _ in offs]
+        ds = [to_dev(s) for s in scs]
+        got = ctx.commit_segments(dp.data_ptr(), len(pts), offs, [d.data_ptr() for d in ds], n)
+        for b, o in enumerate(offs):
+            e = _oracle_commit(pts[o:o + n], scs[b])
+            assert (np.array(list(got[b].x) + list(got[b].y), dtype=np.uint64) == e).all(), (offs, b)
+
+
+@pytest.mark.parametrize("n", [2, 4, 16])
+def test_commit_evals_small_n(ctx, n):
+    from pnp import abi
+    rng = np.random.default_rng(77 + n)
+    lg = n.bit_length() - 1
+    pts = _srs_host(n + 1, 500 + n)
+    dp = to_dev(pts)
+    ctx.load_commit_key(abi.CommitKeyC(powers_of_g=abi.ptr(dp.data_ptr()), powers_of_gamma_g=abi.ptr(dp.data_ptr())),
+                        n + 1, device_ptrs=True)
+    ev = rand_fr_mont_arr(rng, n)
+    ev[n // 2] = 0
+    coeffs = ev.copy()
+    oracle().or_ntt(vp(coeffs), lg, 1, 0)
+    exp = _oracle_commit(pts[:n], coeffs)
+    c = ctx.commit_evals(to_dev(ev).data_ptr(), n)
+    assert (np.array(list(c.x) + list(c.y), dtype=np.uint64) == exp).all()
+
+
+def test_commit_segments_refuses_out_of_range(ctx):
+    import pnp
+    pts = _srs_host(10, 3)
+    dp = to_dev(pts)
+    ds = to_dev(rand_fr_mont_arr(np.random.default_rng(3), 4))
+    with pytest.raises(pnp.PnpError, match="PNP_E_ARG"):
+        ctx.commit_segments(dp.data_ptr(), 10, [7], [ds.data_ptr()], 4)

@@ -1,4 +1,4 @@
-"""Summarise rocprofv3 --pmc CSVs (tools/pmc_run.sh) per kernel and grid size:
+"""Summarise rocprofv3 --pmc CSVs (tools/gpu.sh pmc / traffic steps) per kernel and grid size:
     python tools/pmc_summary.py gpurun_out/<tag> > profiles/<name>.txt
 FETCH_SIZE / WRITE_SIZE are in KB as reported (gfx950: FETCH_SIZE counts wide
 coalesced streaming reads at half their bytes, MI355X_MICROARCH.md HBM)."""
@@ -28,3 +28,26 @@ for key in sorted(acc, key=lambda k: -sum(acc[k]["_dur_ns"])):
           f"{mean('SQ_INSTS_VALU') / max(mean('SQ_WAVES'), 1):9.0f} "
           f"{100 * mean('SQ_ACTIVE_INST_ANY') / wc:7.1f} {100 * mean('SQ_WAIT_ANY') / wc:6.1f} "
           f"{100 * mean('SQ_WAIT_INST_ANY') / wc:9.1f}")
+
+# k_accumulate29: the mixed additions the counters allow per launch.  Every
+# lane-addition issues ~5,154 VALU wave-instructions per 64 lanes
+# (tools/isa_model.py); SQ_INSTS_VALU also counts the non-addition work (the
+# binary search, staging, stores), so this is an upper bound on the real count
+# the bench credits (roofline.madds_per_launch).
+VALU_PER_MADD = 5154
+rows = [(k, acc[k]) for k in acc if k[0].endswith("k_accumulate29") and acc[k].get("SQ_INSTS_VALU")]
+if rows:
+    tot_m = tot_ns = tot_n = 0
+    print()
+    print(f"{'k_accumulate29 grid':>20s} {'n':>3s} {'dur_us':>9s} {'VALU_G/launch':>13s} {'madds_le_M':>11s}")
+    for k, d in sorted(rows, key=lambda r: -r[0][1]):
+        v = [x for x in d["SQ_INSTS_VALU"]]
+        n = len(v)
+        m = sum(v) / n * 64 / VALU_PER_MADD
+        dur = sum(d["_dur_ns"]) / len(d["_dur_ns"])
+        tot_m += m * n
+        tot_ns += dur * n
+        tot_n += n
+        print(f"{k[1]:20d} {n:3d} {dur / 1e3:9.1f} {sum(v) / n / 1e9:13.3f} {m / 1e6:11.2f}")
+    print(f"all launches: {tot_n}, madds <= {tot_m / 1e6:.1f} M, {tot_m / (tot_ns / 1e9) / 1e9:.3f} G madd/s "
+          f"over their summed duration")

@@ -1,4 +1,4 @@
-"""FETCH_SIZE + WRITE_SIZE per k_accumulate29 launch from a tools/pmc_run.sh
+"""FETCH_SIZE + WRITE_SIZE per k_accumulate29 launch from a tools/gpu.sh traffic
 output directory -> the JSON bench.py reads for roofline.traffic:
     python tools/pmc_traffic.py gpurun_out/<tag> > profiles/r02_accumulate_traffic.json
 FETCH_SIZE is scaled by the calibration of the gather pattern measured with
@@ -29,7 +29,7 @@ json.dump({
     "write_bytes_per_launch": write,
     "bytes_per_launch": fetch + write,
     "note": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE, separate passes over one bench proof "
-            "(tools/pmc_run.sh); FETCH_SIZE x the calibration of the same gather pattern on a known byte "
+            "(tools/gpu.sh pmc / traffic steps); FETCH_SIZE x the calibration of the same gather pattern on a known byte "
             "count (tools/ubench_gather.hip, MI355X_MICROARCH.md HBM: other access widths are "
             "uncalibrated); expected: one 128-B table line per (point, window) plus the sorted indices",
 }, sys.stdout, indent=1)

@@ -5,6 +5,7 @@
 // synchronous, device 0, print-and-exit on device errors (caffe/common.hpp:
 // 23-30).  v2 functions return PNP_* codes and never exit.
 #include <algorithm>
+#include <atomic>
 #include <stdarg.h>
 #include <stdlib.h>
 #include <string.h>
@@ -23,19 +24,31 @@ void set_error(const char *fmt, ...) {
     va_end(ap);
 }
 
+// device bytes held by every DevBuf of the process (pnp_hbm_usage)
+std::atomic<uint64_t> g_dev_live{0}, g_dev_peak{0};
+
 void DevBuf::alloc(size_t b) {
     release();
     if (b == 0) b = 16;
     hipError_t e = hipMalloc(&p, b);
     if (e != hipSuccess) {
         p = nullptr;
-        set_error("hipMalloc(%zu) failed: %s", b, hipGetErrorString(e));
+        (void)hipGetLastError();  // clear the sticky out-of-memory status
+        set_error("hipMalloc(%zu) failed: %s (%.2f GiB held by this library)", b, hipGetErrorString(e),
+                  g_dev_live.load() / 1073741824.0);
         throw Error(PNP_E_NOMEM);
     }
     bytes = b;
+    const uint64_t now = g_dev_live.fetch_add(b) + b;
+    uint64_t pk = g_dev_peak.load();
+    while (now > pk && !g_dev_peak.compare_exchange_weak(pk, now)) {
+    }
 }
 void DevBuf::release() {
-    if (p) (void)hipFree(p);
+    if (p) {
+        (void)hipFree(p);
+        g_dev_live.fetch_sub(bytes);
+    }
     p = nullptr;
     bytes = 0;
 }
@@ -357,6 +370,39 @@ int pnp_commit_evals(pnp_ctx *ctx, const uint64_t *d_evals, uint64_t n, Commitme
         CommitmentC *o[1] = {out};
         const uint64_t *e[1] = {d_evals};
         commit_evals_batch(ctx, e, 1, n, o);
+    });
+}
+
+int pnp_commit_segments(pnp_ctx *ctx, const uint64_t *d_points, uint64_t n_points, int B, const uint64_t *seg_off,
+                        const uint64_t *const *d_scalars, uint64_t n, CommitmentC *out) {
+    if (!ctx || !out || !seg_off || !d_scalars || B < 1 || B > 16 || (n_points && !d_points)) return PNP_E_ARG;
+    for (int b = 0; b < B; b++) {
+        if ((n && !d_scalars[b]) || seg_off[b] > n_points || n > n_points - seg_off[b]) {
+            set_error("commit segments: MSM %d covers points [%llu, %llu) of %llu", b,
+                      (unsigned long long)seg_off[b], (unsigned long long)(seg_off[b] + n),
+                      (unsigned long long)n_points);
+            return PNP_E_ARG;
+        }
+    }
+    if (ctx->msm.world > 1) {
+        set_error("commit segments: single-GPU operator");
+        return PNP_E_ARG;
+    }
+    PNP_TRY({
+        std::vector<uint64_t> xyzz((size_t)B * 24), aff((size_t)B * 12);
+        if (n != 0) {  // n = 0: every sum is infinity (ZZ = 0)
+            DevBuf tab;
+            msm_build_table(tab, d_points, n_points, ctx->msm.fold_c, ctx->stream);
+            MsmSegs segs;
+            segs.n_table = n_points;
+            for (int b = 0; b < B; b++) segs.off[b] = seg_off[b];
+            msm_run_batch(ctx->msm, nullptr, d_scalars, B, n, xyzz.data(), ctx->stream, tab.u64(), false, &segs);
+        }
+        xyzz_to_affine_batch_host(xyzz.data(), B, aff.data());
+        for (int b = 0; b < B; b++) {
+            memcpy(out[b].x, &aff[12 * b], 48);
+            memcpy(out[b].y, &aff[12 * b + 6], 48);
+        }
     });
 }
 

@@ -756,6 +756,28 @@ __global__ __launch_bounds__(256, PNP_ACC_WAVES) void k_accumulate29(const uint3
     if (!ok) redo[atomicAdd(nredo, 1u)] = (uint32_t)t;
 }
 
+// Work of one k_accumulate29 launch (timed runs only, pnp_kernel_timing): the
+// sorted entries E = offs[WB] and the pieces the lanes start fresh — one per
+// lane with entries (ceil(E / S)) plus one per non-empty bucket whose first
+// entry is not a lane's first (offs[b] % S != 0).  Every other entry is one
+// mixed addition: madds = E - pieces.  ctr[0] += E, ctr[1] += pieces.
+__global__ __launch_bounds__(256) void k_count_pieces(const uint32_t *offs, uint64_t WB, uint32_t S,
+                                                      unsigned long long *ctr) {
+    const uint64_t b = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    bool fresh = false;
+    if (b < WB) {
+        const uint32_t o = offs[b];
+        fresh = offs[b + 1] > o && (o % S) != 0;
+    }
+    const unsigned long long m = __ballot(fresh);
+    if ((threadIdx.x & 63) == 0 && m) atomicAdd(&ctr[1], (unsigned long long)__popcll(m));
+    if (b == 0) {
+        const unsigned long long tot = offs[WB];
+        atomicAdd(&ctr[0], tot);
+        atomicAdd(&ctr[1], (tot + S - 1) / S);
+    }
+}
+
 // exact 32-bit recomputation of the segments k_accumulate29 flagged
 __global__ __launch_bounds__(64) void k_accumulate_redo(const uint32_t *pts29, const uint32_t *sorted,
                                                         const uint32_t *offs, uint64_t U, uint32_t S,
@@ -1030,8 +1052,30 @@ static void accumulate_group(MsmWork &wk, MsmGroup &gb, const GroupPlan &gp, con
     // once per window sweep
     if (wk.timer) {
         wk.timer->end("msm_accumulate", s, ev0, alg_bytes);
-        wk.timer->credit("msm_entries", (double)nent);  // ~ mixed additions (zero digits drop out)
+        // the dense bound nv x rows x n (zero digits drop out of the real count)
+        wk.timer->credit("msm_entries_dense", (double)nent);
+        if (table) {  // the real work, counted on the device (k_count_pieces)
+            need(gb.wctr, 16);
+            PNP_HIP(hipMemsetAsync(gb.wctr.p, 0, 16, s));
+            hipLaunchKernelGGL(k_count_pieces, dim3((uint32_t)((WB + 255) / 256)), dim3(256), 0, s, bstart, WB, S,
+                               static_cast<unsigned long long *>(gb.wctr.p));
+            PNP_HIP(hipGetLastError());
+            gb.wctr_live = true;
+        }
     }
+}
+
+// queue the D2H copy of a timed launch's work counters (before the caller's
+// stream synchronisation) / credit them to the timer after it
+static void wctr_fetch(MsmGroup &gb, hipStream_t s) {
+    if (gb.wctr_live) PNP_HIP(hipMemcpyAsync(gb.wctr_h, gb.wctr.p, 16, hipMemcpyDeviceToHost, s));
+}
+static void wctr_credit(MsmWork &wk, MsmGroup &gb) {
+    if (!gb.wctr_live) return;
+    gb.wctr_live = false;
+    if (!wk.timer) return;
+    wk.timer->credit("msm_entries", (double)gb.wctr_h[0]);
+    wk.timer->credit("msm_madds", (double)(gb.wctr_h[0] - gb.wctr_h[1]));
 }
 
 static const uint64_t *reduce_group(MsmGroup &gb, const GroupPlan &gp, const MsmCfg &g, hipStream_t s,
@@ -1184,9 +1228,11 @@ static void msm_local_batch(MsmWork &wk, const uint64_t *d_points, const uint64_
         if (folded) {
             PNP_HIP(hipMemcpyAsync(&exc[k], wk.grp[k].exc.p, 4, hipMemcpyDeviceToHost, s));
             PNP_HIP(hipMemcpyAsync(&nredo[k], wk.grp[k].redo.p, 4, hipMemcpyDeviceToHost, s));
+            wctr_fetch(wk.grp[k], s);
         }
     }
     PNP_HIP(hipStreamSynchronize(s));
+    for (int k = 0; k < ng; k++) wctr_credit(wk, wk.grp[k]);
     // accumulation lanes recomputed exactly (a degenerate step in a piece)
     if (wk.timer) wk.timer->credit("msm_redo_lanes", (double)nredo[0] + nredo[1]);
     for (int k = 0; k < ng; k++) {
@@ -1425,7 +1471,9 @@ static bool msm_bucket_batch(MsmWork &wk, const uint64_t *const *sc, int B, uint
         PNP_HIP(hipMemcpyAsync(ts.data(), res, ts.size() * 8, hipMemcpyDeviceToHost, s));
         PNP_HIP(hipMemcpyAsync(&exc, gb.exc.p, 4, hipMemcpyDeviceToHost, s));
         PNP_HIP(hipMemcpyAsync(&nredo, gb.redo.p, 4, hipMemcpyDeviceToHost, s));
+        wctr_fetch(gb, s);
         PNP_HIP(hipStreamSynchronize(s));
+        wctr_credit(wk, gb);
         if (wk.timer) wk.timer->credit("msm_redo_lanes", (double)nredo);
         if (exc) {
             if (wk.timer) wk.timer->credit("msm_exact_fallback", 1);

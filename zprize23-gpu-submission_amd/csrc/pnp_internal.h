@@ -131,6 +131,12 @@ struct MsmGroup {
     DevBuf heavy;  // folded: the merge's queue of buckets with many pieces
     uint32_t S = 0, pieces = 0;  // folded: accumulate segment length, pieces per bucket
     uint64_t nthr = 0;           // folded: accumulate lanes (head / tail slots)
+    // timed runs only (KernelTimer enabled): what the last k_accumulate29 launch
+    // really did, counted on the device from the bucket starts — {sorted
+    // entries, pieces started fresh}; mixed additions = entries - pieces
+    DevBuf wctr;
+    unsigned long long wctr_h[2] = {0, 0};
+    bool wctr_live = false;
 };
 struct MsmWork {
     DevBuf digits;  // u32 keys of every (MSM, window, point)

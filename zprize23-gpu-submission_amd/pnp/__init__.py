@@ -35,7 +35,7 @@ SYMBOLS = ("gen_proof", "pnp_last_error", "pnp_ctx_create", "pnp_ctx_destroy",
            "pnp_poly_div_linear", "pnp_prefix_product", "pnp_batch_inverse",
            "pnp_synth_random_fr", "pnp_synth_srs", "pnp_synth_coset_consts", "pnp_synth_circuit",
            "pnp_synth_merkle", "pnp_load_commit_key_strided", "pnp_proof_infinity_mask",
-           "pnp_set_exchange_v")
+           "pnp_set_exchange_v", "pnp_commit_segments")
 
 
 # int allgather(void *user, uint64_t bytes_per_rank) — pnp_set_msm_shard
@@ -91,6 +91,8 @@ def load(path: str = LIB_PATH):
     lib.pnp_commit.argtypes = [vp, vp, vp, u64, C.POINTER(abi.CommitmentC)]
     lib.pnp_commit_ck.argtypes = [vp, vp, u64, C.POINTER(abi.CommitmentC)]
     lib.pnp_commit_evals.argtypes = [vp, vp, u64, C.POINTER(abi.CommitmentC)]
+    lib.pnp_commit_segments.argtypes = [vp, vp, u64, i32, C.POINTER(u64), C.POINTER(vp), u64,
+                                        C.POINTER(abi.CommitmentC)]
     lib.pnp_poly_eval.argtypes = [vp, vp, u64, vp, vp]
     lib.pnp_poly_div_linear.argtypes = [vp, vp, u64, vp]
     lib.pnp_prefix_product.argtypes = [vp, vp, u64]
@@ -221,7 +223,7 @@ class Context:
             cb3 = exchange.c_alltoallv()
             check(self.lib.pnp_set_exchange_v(self.h, cb3, None, exchange.vsend.data_ptr(),
                                               exchange.vrecv.data_ptr(), exchange.vsend.numel() * 8),
-                  "pnp_set_exchange_v")
+                  "pnp_set_exchange_v", "pnp_commit_segments")
             keep.append(cb3)
         self._exchange = keep  # keep the callbacks alive
 
@@ -259,6 +261,17 @@ class Context:
         out = abi.CommitmentC()
         check(self.lib.pnp_commit_evals(self.h, C.c_void_p(evals), n, C.byref(out)), "pnp_commit_evals")
         return out
+
+    def commit_segments(self, points: int, n_points: int, seg_off, scalars, n: int):
+        """B MSMs over sub-ranges [seg_off[b], seg_off[b] + n) of one base set
+        (pnp_commit_segments: one folded table over all n_points)."""
+        B = len(seg_off)
+        offs = (C.c_uint64 * B)(*seg_off)
+        sc = (C.c_void_p * B)(*scalars)
+        out = (abi.CommitmentC * B)()
+        check(self.lib.pnp_commit_segments(self.h, C.c_void_p(points), n_points, B, offs, sc, n, out),
+              "pnp_commit_segments")
+        return list(out)
 
     def poly_eval(self, addr: int, n: int, x_limbs):
         x = (C.c_uint64 * 4)(*x_limbs)
