@@ -320,6 +320,17 @@ int pnp_kernel_bytes(pnp_ctx *ctx, const char *name, double *bytes);
  * must leave the slot rank s sent to this rank at
  * d_a2a + (world + s) * bytes_per_peer. */
 typedef int (*pnp_allgather_fn)(void *user, uint64_t bytes_per_rank);
+/* Every all-gather slot ends with one tag word naming the exchange (the last
+ * 8 bytes of each rank's bytes_per_rank): an exchange harness can tell the
+ * messages apart without inferring them from sizes, and the library refuses
+ * (PNP_E_DEVICE, "out of step") a result in which a peer's tag differs. */
+#define PNP_EX_TAG_COUNTS    0xB0C4E7C0ULL  /* bucket-range MSMs: entry bytes per destination */
+#define PNP_EX_TAG_MSM_SUMS  0x5EC7A111ULL  /* point-range MSMs: B partial sums (XYZZ)       */
+#define PNP_EX_TAG_T_FLAGS   0x7F1A6500ULL  /* round 4: non-zero quotient chunks (8 words)   */
+#define PNP_EX_TAG_DIV_CARRY 0xD1FC0001ULL  /* split division by (X - z): slice values      */
+#define PNP_EX_TAG_EVALS     0xE7A15000ULL  /* round 5: partial evaluations (18 x 4 words)  */
+#define PNP_EX_TAG_STATUS    0x57A7A500ULL  /* key load / derived tables: per-rank status   */
+#define PNP_EX_TAG_DEVICE    0xDE71CE00ULL  /* key load: which GPU each rank runs on        */
 typedef int (*pnp_alltoall_fn)(void *user, uint64_t bytes_per_peer);
 /* pnp_set_exchange_v (optional, before the first commitment; world must
  * divide the bucket count): the folded MSMs shard BUCKET ranges instead of
@@ -336,6 +347,17 @@ typedef int (*pnp_alltoall_fn)(void *user, uint64_t bytes_per_peer);
  * bucket range) falls back to point ranges.  The commit key's folded table then
  * covers all n points on every rank (6.5 GiB at n = 2^22). */
 typedef int (*pnp_alltoallv_fn)(void *user, const uint64_t *send_bytes, const uint64_t *recv_bytes);
+/* The library's HIP stream (a hipStream_t): every kernel and copy of a proof
+ * runs on it in order.  An exchange that enqueues its collectives on this
+ * stream (RCCL: libpnp_rccl.so, include/pnp_rccl.h) declares itself with
+ * pnp_set_exchange_ordered(ctx, 1): the library then calls the callbacks
+ * without synchronising the stream first, and a callback returns once its
+ * collective is enqueued (the library's next copies and kernels are ordered
+ * behind it).  Default 0: the stream is synchronised before every callback,
+ * which must return with the data visible to the device (host-memory
+ * exchanges, other streams). */
+int pnp_ctx_stream(pnp_ctx *ctx, void **stream);
+int pnp_set_exchange_ordered(pnp_ctx *ctx, int ordered);
 int pnp_set_msm_shard(pnp_ctx *ctx, int rank, int world, pnp_allgather_fn allgather,
                       void *user, uint64_t *d_xbuf, uint64_t xbuf_bytes);
 int pnp_set_exchange_a2a(pnp_ctx *ctx, pnp_alltoall_fn alltoall, void *user, uint64_t *d_a2a,
@@ -380,6 +402,19 @@ int pnp_commit_ck(pnp_ctx *ctx, const uint64_t *d_scalars, uint64_t n, Commitmen
  * kept; zero evaluations cost nothing).  n a power of two <= the key's points.
  * PNP_E_ARG when the basis is unavailable (PNP_LAGRANGE=0, degenerate key).  */
 int pnp_commit_evals(pnp_ctx *ctx, const uint64_t *d_evals, uint64_t n, CommitmentC *out);
+
+/* HBM accounting (extension): out[0] = device bytes this library holds now
+ * (every context of the process), out[1] = their peak since the previous
+ * pnp_hbm_usage call (which restarts it), and for the loaded
+ * prover key the upper bounds pnp_load_prover_key budgets a proof with, still
+ * to be allocated on this rank: out[2] mandatory (per-proof buffers, NTT
+ * tables, the commit key's folded table, MSM work), out[3] the Lagrange-basis
+ * key + table, out[4] the copy-constraint groups + table, out[5] the largest
+ * build scratch.  pnp_load_prover_key fails with PNP_E_NOMEM (every rank of a
+ * multi-GPU run, naming the short one) when out[2] + out[5] exceeds the rank's
+ * share of its GPU's free HBM, and switches the optional tables off (same
+ * proof bytes) when they do not fit. */
+int pnp_hbm_usage(pnp_ctx *ctx, uint64_t out[6]);
 
 /* Extension (operator form of gen_proof's copy-group commitments, wires.hip):
  * B <= 16 MSMs over sub-ranges of ONE base set — out[b] = sum_{i<n}

@@ -3,6 +3,7 @@
     RANK=r WORLD_SIZE=N MASTER_ADDR=127.0.0.1 MASTER_PORT=p \
         python shard_worker.py {cpu|gpu} OUT_PREFIX [lg seed]
         python shard_worker.py full OUT_PREFIX lg gates seed
+        python shard_worker.py hbm OUT_PREFIX lg seed   (PNP_TEST_SHORT_RANK)
 
 cpu: exercises pnp.shard.WindowExchange over gloo with host tensors.
 gpu: every rank proves the same seeded instance on cuda:0 with point-range
@@ -72,6 +73,30 @@ def main():
         assert cb(None, 1 << 20) == 1 and ex.error is not None  # oversize slot -> error code
         with open(f"{out}.{rank}", "w") as f:
             f.write("ok")
+    elif mode == "hbm":
+        # one rank short of HBM (PNP_TEST_SHORT_RANK): every rank's key load
+        # must fail with PNP_E_NOMEM naming that rank (abi.cpp hbm_budget)
+        short = int(os.environ["PNP_TEST_SHORT_RANK"])
+        if rank == short:
+            os.environ["PNP_HBM_LIMIT"] = "1"
+        lg, seed = int(sys.argv[3]), int(sys.argv[4])
+        import pnp
+        from pnp_testlib import Inputs
+        from pnp.shard import a2a_bytes_for
+        inp = Inputs(lg, seed)
+        ctx = pnp.Context(0)
+        ex = WindowExchange(rank, world, device="cuda", a2a_bytes=a2a_bytes_for(lg, world),
+                            v_bytes=_v_bytes(lg, world))
+        ctx.set_msm_shard(ex)
+        try:
+            ctx.load_prover_key(inp.pk, inp.n, device_ptrs=False)
+            msg = "loaded"
+        except pnp.PnpError as e:
+            msg = str(e)
+        assert "PNP_E_NOMEM" in msg and f"rank {short} of {world}" in msg, msg
+        with open(f"{out}.{rank}", "w") as f:
+            f.write("ok")
+        ctx.close()
     elif mode == "full":
         # bench.Synthetic (the HEIGHT=15 instance, GPU-generated) at full size
         lg, gates, seed = int(sys.argv[3]), int(sys.argv[4]), int(sys.argv[5])
@@ -95,11 +120,18 @@ def main():
             del syn.keep[k]
         torch.cuda.synchronize()
         torch.cuda.empty_cache()
+        groups = os.environ.get("PNP_EXPECT_GROUPS") == "1"
+        if groups:
+            ctx.kernel_timing(True)
         try:
             proof = ctx.prove(syn.cs, device_ptrs=True)
         except Exception:
             print(f"rank {rank}: exchange error: {ex.error!r}", flush=True)
             raise
+        if groups:  # the wires and z were committed over their groups
+            assert ctx.kernel_bytes("wire_groups_used") == 1, ctx.kernel_bytes("wire_groups_used")
+            assert ctx.kernel_bytes("z_groups_used") == 1, ctx.kernel_bytes("z_groups_used")
+            ctx.kernel_timing(False)
         assert ex.calls > 0
         assert (ex.a2a_calls > 0) == (8 % world == 0)
         if os.environ.get("PNP_EXPECT_BUCKETS"):

@@ -62,3 +62,22 @@ def test_ark_g1_affine_layout_shape():
     L = abi.ARK_G1_AFFINE
     assert C.sizeof(abi.AffineLayout) == 32
     assert (L.stride, L.x_off, L.y_off, L.inf_off) == (104, 0, 48, 96)
+
+
+def test_rccl_library_exports_header_symbols():
+    """libpnp_rccl.so exports every function include/pnp_rccl.h declares.
+    Checked in a child process that never imports torch (the library maps
+    /opt/rocm's RCCL; a torch process keeps its own)."""
+    import subprocess
+    import sys
+    src = open(os.path.join(REPO, "include", "pnp_rccl.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    declared = sorted(set(re.findall(r"\b(pnp_rccl_\w+)\s*\(", src)))
+    assert len(declared) == 8, declared
+    lib = os.path.join(REPO, "zprize23-gpu-submission_amd", "lib", "libpnp_rccl.so")
+    code = ("import ctypes, sys; l = ctypes.CDLL(sys.argv[1]); "
+            "print(' '.join(s for s in sys.argv[2:] if not hasattr(l, s)))")
+    out = subprocess.run([sys.executable, "-c", code, lib] + declared, capture_output=True, text=True,
+                         timeout=60)
+    assert out.returncode == 0, out.stderr
+    assert out.stdout.strip() == "", f"missing: {out.stdout}"

@@ -1,0 +1,109 @@
+"""HBM budget of a proof (abi.cpp hbm_plan / hbm_budget, pnp_hbm_usage):
+
+  * the plan pnp_load_prover_key budgets with is an upper bound of what the
+    first proof really allocates (the library's own allocation counter), and
+    not a wild one;
+  * a budget without room for the optional tables (PNP_HBM_LIMIT) switches the
+    copy-constraint groups / the Lagrange-basis key off and the proof bytes do
+    not change;
+  * a budget without room for the proof fails the key load with PNP_E_NOMEM
+    and a message naming the bytes — on every rank of a multi-rank run, even
+    when only one rank is short (tests/test_shard.py
+    test_hbm_short_rank_fails_every_load)."""
+import os
+import sys
+
+import pytest
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.dirname(HERE))
+
+pytestmark = pytest.mark.gpu
+
+GiB = 1 << 30
+
+
+def _instance(ctx, lg):
+    from bench import Synthetic
+    return Synthetic(ctx, lg, 0, seed=2, circuit="merkle")
+
+
+def _load(ctx, syn):
+    ctx.load_prover_key(syn.pk, syn.n, device_ptrs=True)
+    ctx.load_commit_key(syn.ck, syn.n, device_ptrs=True)
+
+
+@pytest.mark.parametrize("lg", [16, 20])
+def test_plan_bounds_the_first_proof(lg):
+    import pnp
+    ctx = pnp.Context(0)
+    try:
+        syn = _instance(ctx, lg)
+        _load(ctx, syn)
+        u0 = ctx.hbm_usage()
+        plan = u0["mandatory"] + u0["lagrange"] + u0["groups"] + u0["transient"]
+        ctx.kernel_timing(True)
+        ctx.prove(syn.cs, device_ptrs=True)
+        used = ctx.kernel_bytes("wire_groups_used")
+        ctx.kernel_timing(False)
+        u1 = ctx.hbm_usage()
+        grew = u1["peak"] - u0["live"]
+        print(f"2^{lg}: plan {plan / GiB:.3f} GiB (mandatory {u0['mandatory'] / GiB:.3f}, lagrange "
+              f"{u0['lagrange'] / GiB:.3f}, groups {u0['groups'] / GiB:.3f}, transient {u0['transient'] / GiB:.3f}); "
+              f"first proof peak +{grew / GiB:.3f} GiB, held after {u1['live'] / GiB:.3f} GiB")
+        assert used == 1  # the groups were built and used, so the plan covered them
+        assert grew <= plan, (grew, plan)
+        assert plan <= 3 * grew + (256 << 20), (grew, plan)
+        # a second proof allocates nothing new
+        ctx.prove(syn.cs, device_ptrs=True)
+        assert ctx.hbm_usage()["peak"] <= u1["live"] + (64 << 20)
+    finally:
+        ctx.close()
+
+
+def test_budget_switches_optional_tables_off(monkeypatch):
+    import pnp
+    from pnp import abi
+    lg = 16
+    ctx = pnp.Context(0)
+    try:
+        syn = _instance(ctx, lg)
+        _load(ctx, syn)
+        ref = abi.proof_to_bytes(ctx.prove(syn.cs, device_ptrs=True))
+    finally:
+        ctx.close()
+    for keep_lag in (True, False):
+        ctx = pnp.Context(0)
+        try:
+            syn = _instance(ctx, lg)
+            _load(ctx, syn)  # (plans with nothing built yet)
+            u = ctx.hbm_usage()
+            room = u["live"] + u["mandatory"] + u["transient"] + (u["lagrange"] if keep_lag else 0) + (1 << 20)
+            monkeypatch.setenv("PNP_HBM_LIMIT", str(room))
+            ctx.load_prover_key(syn.pk, syn.n, device_ptrs=True)
+            monkeypatch.delenv("PNP_HBM_LIMIT")
+            ctx.kernel_timing(True)
+            got = abi.proof_to_bytes(ctx.prove(syn.cs, device_ptrs=True))
+            groups = ctx.kernel_bytes("wire_groups_used")
+            ctx.kernel_timing(False)
+            assert got == ref, keep_lag
+            assert groups == 0, keep_lag
+        finally:
+            ctx.close()
+
+
+def test_budget_refuses_a_key_that_cannot_prove(monkeypatch):
+    import pnp
+    ctx = pnp.Context(0)
+    try:
+        syn = _instance(ctx, 16)
+        monkeypatch.setenv("PNP_HBM_LIMIT", "1")
+        with pytest.raises(pnp.PnpError, match="PNP_E_NOMEM.*HBM budget"):
+            ctx.load_prover_key(syn.pk, syn.n, device_ptrs=True)
+        monkeypatch.delenv("PNP_HBM_LIMIT")
+        with pytest.raises(pnp.PnpError, match="PNP_E_NOKEY"):
+            ctx.prove(syn.cs, device_ptrs=True)
+        _load(ctx, syn)  # room again: loads and proves
+        ctx.prove(syn.cs, device_ptrs=True)
+    finally:
+        ctx.close()

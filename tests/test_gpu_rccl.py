@@ -77,3 +77,16 @@ def test_rccl_exchange_world1(tmp_path):
     out = log.read_text(errors="replace")
     assert p.returncode == 0, out[-3000:]
     assert "rccl world-1 exchange ok" in out
+
+
+@pytest.mark.gpu
+def test_native_rccl_world1(tmp_path):
+    """libpnp_rccl.so (include/pnp_rccl.h) in a process that never imports
+    torch: tests/rccl_native_worker.py."""
+    log = tmp_path / "native.log"
+    with open(log, "wb") as f:
+        p = subprocess.run([sys.executable, os.path.join(HERE, "rccl_native_worker.py")], stdout=f,
+                           stderr=subprocess.STDOUT, timeout=110)
+    out = log.read_text(errors="replace")
+    assert p.returncode == 0, out[-3000:]
+    assert "native rccl world-1 exchange ok" in out

@@ -108,15 +108,42 @@ def test_sharded_full_size_matches_golden(tmp_path, golden, world, shard):
         torch.cuda.synchronize()
         torch.cuda.empty_cache()
     prefix = str(tmp_path / "full")
-    # 4 and 8 ranks on one GPU: no copy-constraint wire groups (their folded
-    # table, ~17 GB per rank at 2^22 plus as much while it is built, would not
-    # fit this GPU's HBM next to the ranks' other tables; one rank per GPU has
-    # room — the 2-rank cases and test_sharded_merkle_circuit cover the
-    # grouped wires sharded)
+    # 4 and 8 ranks on one GPU at 2^22: no copy-constraint wire groups (in
+    # bucket-range mode every rank holds their full folded table, 5 segments x
+    # n x 13 windows x 128 B = 35 GB at 2^22, plus its build scratch: 8 ranks
+    # would need ~300 GB of this one GPU's 288; one rank per GPU has room) —
+    # test_sharded_merkle_h13_groups_on runs the production default with the
+    # groups at 4 and 8 ranks at 2^20
     extra = {"PNP_WIRE_GROUPS": "0"} if world >= 4 else {}
     _launch(world, ["full", prefix, str(g["lg"]), str(g["gates"]), str(g["seed"]), g.get("circuit", "arith")],
             tmp_path, 900, PNP_TEST_MSM_SHARD=shard, PNP_EXPECT_BUCKETS="1" if shard == "buckets" else "0",
             PNP_MSM_BUCKETS_MIN_WORLD="2", **extra)
+    for r in range(world):
+        assert open(f"{prefix}.{r}", "rb").read().hex() == g["proof_hex"], f"rank {r}"
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world,shard", [(4, "buckets"), (8, "buckets"), (2, "points"), (4, "points")])
+def test_sharded_merkle_h13_groups_on(tmp_path, world, shard):
+    """The production default at a size where every rank fits one shared GPU:
+    the HEIGHT=13 Merkle circuit (n = 2^20, bench.Synthetic seed 1) with the
+    copy-constraint wire groups and z's runs ON, proved by `world` ranks —
+    bucket ranges (every rank holds the full grouped table) or point ranges
+    (each rank's slice of it) — equals the CPU restatement's golden proof
+    (tests/golden/merkle_h13_seed1.json, make_golden_full.py --lg 20 --circuit
+    merkle), and every rank really committed over the groups."""
+    import json
+    path = os.path.join(HERE, "golden", "merkle_h13_seed1.json")
+    with open(path) as f:
+        g = json.load(f)
+    import torch
+    if torch.cuda.is_initialized():
+        torch.cuda.synchronize()
+        torch.cuda.empty_cache()
+    prefix = str(tmp_path / "h13")
+    _launch(world, ["full", prefix, str(g["lg"]), str(g["gates"]), str(g["seed"]), "merkle"], tmp_path, 900,
+            PNP_TEST_MSM_SHARD=shard, PNP_EXPECT_BUCKETS="1" if shard == "buckets" else "0",
+            PNP_MSM_BUCKETS_MIN_WORLD="2", PNP_EXPECT_GROUPS="1")
     for r in range(world):
         assert open(f"{prefix}.{r}", "rb").read().hex() == g["proof_hex"], f"rank {r}"
 
@@ -136,3 +163,17 @@ def test_sharded_merkle_circuit(tmp_path, world):
     _launch(world, ["full", prefix, str(lg), "0", str(seed), "merkle"], tmp_path, 600)
     for r in range(world):
         assert open(f"{prefix}.{r}", "rb").read() == exp, f"rank {r}"
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 4])
+def test_hbm_short_rank_fails_every_load(tmp_path, world):
+    """One rank whose HBM budget cannot hold a proof (PNP_HBM_LIMIT=1 on rank
+    world - 1): pnp_load_prover_key fails with PNP_E_NOMEM on EVERY rank, the
+    message naming the short rank — no rank runs into an exchange its peer
+    left (an 8-rank run that ran out of HBM surfaced as "count
+    all-gather failed" on the other ranks)."""
+    prefix = str(tmp_path / "hbm")
+    _launch(world, ["hbm", prefix, "10", "5"], tmp_path, 300, PNP_TEST_SHORT_RANK=str(world - 1))
+    for r in range(world):
+        assert open(f"{prefix}.{r}").read() == "ok", f"rank {r}"

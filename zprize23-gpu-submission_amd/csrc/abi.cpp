@@ -79,34 +79,195 @@ void ck_derived_reset(pnp_ctx *ctx) {
     wire_bases_reset(ctx);
 }
 
-const uint64_t *lagrange_table(pnp_ctx *ctx, uint64_t n) {
+// every rank's verdict on a step that may fail on some rank only (an optional
+// table that did not fit its HBM): true when it succeeded on all of them
+bool all_ranks_ok(pnp_ctx *ctx, bool mine) {
+    if (ctx->msm.world <= 1 || !ctx->msm.allgather) return mine;
+    const uint64_t w = mine ? 1 : 0;
+    for (uint64_t v : rank_allgather(ctx->msm, ctx->stream, &w, 1, PNP_EX_TAG_STATUS))
+        if (!v) return false;
+    return true;
+}
+
+bool lagrange_enabled() {
     static const bool enabled = [] {
         const char *e = getenv("PNP_LAGRANGE");
         return !e || atoi(e) != 0;
     }();
-    if (!enabled || n < 2 || (n & (n - 1)) || n > ctx->ck_points) return nullptr;
-    if (ctx->lag_n != n) {
-        ctx->lag_table_n = 0;
-        ctx->lag_table.release();
-        ctx->lag_points.alloc(n * 96);
-        uint32_t lg = 0;
-        while ((1ULL << lg) < n) lg++;
-        ctx->lag_ok = srs_lagrange(ctx->ck_dev, n, inverse(root_of_unity(lg)), inverse(fr_from_u64(n)),
-                                   ctx->lag_points.u64(), ctx->stream);
-        ctx->lag_n = n;
-        if (!ctx->lag_ok) ctx->lag_points.release();
-    }
-    if (!ctx->lag_ok) return nullptr;
+    return enabled;
+}
+
+const uint64_t *lagrange_table(pnp_ctx *ctx, uint64_t n) {
+    if (!lagrange_enabled() || ctx->hbm_lag_off || n < 2 || (n & (n - 1)) || n > ctx->ck_points) return nullptr;
     uint64_t p0 = 0, p1 = n;
     if (!ctx->msm.full_table()) msm_point_range(n, ctx->msm.rank, ctx->msm.world, p0, p1);
-    if (ctx->lag_table_n != n || ctx->lag_table_p0 != p0 || ctx->lag_table_p1 != p1) {
-        ctx->lag_table_n = 0;
-        msm_build_table(ctx->lag_table, ctx->lag_points.u64() + 12 * p0, p1 - p0, ctx->msm.fold_c, ctx->stream);
-        ctx->lag_table_n = n;
-        ctx->lag_table_p0 = p0;
-        ctx->lag_table_p1 = p1;
+    // (re)built on the same call on every rank (same key and call sequence):
+    // a rank whose HBM could not hold it makes every rank go without
+    bool built = false, fits = true;
+    try {
+        if (ctx->lag_n != n) {
+            built = true;
+            ctx->lag_table_n = 0;
+            ctx->lag_table.release();
+            ctx->lag_n = 0;
+            ctx->lag_points.alloc(n * 96);
+            uint32_t lg = 0;
+            while ((1ULL << lg) < n) lg++;
+            ctx->lag_ok = srs_lagrange(ctx->ck_dev, n, inverse(root_of_unity(lg)), inverse(fr_from_u64(n)),
+                                       ctx->lag_points.u64(), ctx->stream);
+            ctx->lag_n = n;
+            if (!ctx->lag_ok) ctx->lag_points.release();
+        }
+        if (ctx->lag_ok && (ctx->lag_table_n != n || ctx->lag_table_p0 != p0 || ctx->lag_table_p1 != p1)) {
+            built = true;
+            ctx->lag_table_n = 0;
+            msm_build_table(ctx->lag_table, ctx->lag_points.u64() + 12 * p0, p1 - p0, ctx->msm.fold_c, ctx->stream);
+            ctx->lag_table_n = n;
+            ctx->lag_table_p0 = p0;
+            ctx->lag_table_p1 = p1;
+        }
+    } catch (const Error &e) {
+        if (e.code != PNP_E_NOMEM) throw;
+        fits = false;
     }
+    if (built && !all_ranks_ok(ctx, fits)) fits = false;
+    if (!fits) {  // commit from coefficients (prover.cpp), on every rank
+        ctx->lag_points.release();
+        ctx->lag_table.release();
+        ctx->lag_table_n = 0;
+        ctx->lag_n = n;
+        ctx->lag_ok = false;
+        ctx->hbm_lag_off = true;
+        return nullptr;
+    }
+    if (!ctx->lag_ok) return nullptr;
     return ctx->lag_table.u64();
+}
+
+// ---- HBM budget (key load) ----
+// Upper bounds of what a proof at domain n allocates on this rank, by part:
+// the mandatory working set (per-proof buffers, NTT tables, the commit key's
+// folded table and its build, the MSM work of the largest batch) and the two
+// optional derived tables (the Lagrange basis with its table; the
+// copy-constraint groups with theirs), each minus what is already held.
+// Checked against the measured peak by tests/test_gpu_hbm.py.
+static uint64_t map_bytes(const std::map<std::string, DevBuf> &m) {
+    uint64_t b = 0;
+    for (const auto &kv : m) b += kv.second.bytes;
+    return b;
+}
+static uint64_t map_bytes(const std::map<uint32_t, DevBuf> &m) {
+    uint64_t b = 0;
+    for (const auto &kv : m) b += kv.second.bytes;
+    return b;
+}
+HbmPlan hbm_plan(pnp_ctx *ctx, uint64_t n) {
+    HbmPlan p;
+    const MsmWork &wk = ctx->msm;
+    const int world = wk.world;
+    const bool full = wk.full_table();
+    const uint64_t per = (n + world - 1) / world;  // this rank's point range (at most)
+    const uint64_t n_tab = full ? n : per;
+    const bool dist = ctx->pk_nb < 8;
+    const uint64_t len = dist ? per : n, NB = (uint64_t)ctx->pk_nb * n, N8 = 8 * n;
+    const bool lookups = !ctx->pk_qlookup_zero;
+    // per-proof buffers (prover.cpp ctx->buf), the division / scan scratch and
+    // the PI term's 1 / (x - w^pos)
+    const uint64_t work = 32 * (25 * n + 11 * len + NB * (7 + (lookups ? 5 : 0) + (ctx->pk_std_coset ? 1 : 3))) +
+                          32 * 4 * std::max(n, NB);
+    const uint64_t work_held = map_bytes(ctx->work) + ctx->scratch_a.bytes + ctx->scratch_b.bytes + ctx->pk_pinv.bytes;
+    // NTT tables: twiddles of n and 8n (both directions, 2^256 and 2^261
+    // forms), the block twists (forward, inverse, x32, 2^261 forms)
+    const uint64_t ntt = 32 * 2 * (n + N8) + 36 * 2 * (n + N8) + 32 * 4 * N8 + 36 * 2 * N8;
+    const uint64_t ntt_held = map_bytes(ctx->ntt.fwd) + map_bytes(ctx->ntt.inv) + map_bytes(ctx->ntt.lde_twist) +
+                              map_bytes(ctx->ntt.blk_twist) + map_bytes(ctx->ntt.blk_twist_inv) +
+                              map_bytes(ctx->ntt.fwd29) + map_bytes(ctx->ntt.inv29) +
+                              map_bytes(ctx->ntt.blk_twist29) + map_bytes(ctx->ntt.blk_twist_inv29) +
+                              map_bytes(ctx->ntt.blk_twist32);
+    const uint64_t ck_tab = msm_table_bytes(n_tab, n, wk.fold_c);
+    const uint64_t msm = msm_work_bytes(per, n, wk.fold_c, 9, wk.v_bytes);
+    const uint64_t held = work_held + ntt_held + ctx->ck_table.bytes + msm_work_held(wk);
+    const uint64_t total = work + ntt + ck_tab + msm;
+    p.mandatory = total > held ? total - held : 0;
+    p.transient = ctx->ck_table.bytes ? 0 : msm_table_build_bytes(n_tab);
+    // the Lagrange basis (n affine points) + its folded table; its build:
+    // the radix-2^29 layer array, the window tables, the XYZZ output
+    const uint64_t lag = n * 96 + msm_table_bytes(n_tab, n, wk.fold_c);
+    const uint64_t lag_held = ctx->lag_points.bytes + ctx->lag_table.bytes;
+    p.lag = lag > lag_held ? lag - lag_held : 0;
+    if (p.lag)
+        p.transient = std::max<uint64_t>(p.transient, n * (224 + 16 + 192 + 48) +
+                                                          std::min<uint64_t>(n / 2, 1ULL << 18) * 15 * 224);
+    // the copy-constraint groups: 5 segments of n slots (this rank's slice in
+    // point-range mode), their folded table, the group maps and scalars, the
+    // sigma copy; the build: sort keys and labels, XYZZ bases, affine points
+    const uint64_t seg = full ? n : (world > 1 ? per : n);
+    const uint64_t grp = msm_table_bytes(5 * seg, n, wk.fold_c) + 5 * n * (4 + 4 + 32) + 4 * n * 32;
+    const uint64_t grp_held = ctx->wb.table.bytes + ctx->wb.sigma.bytes;
+    p.groups = grp > grp_held ? grp - grp_held : 0;
+    if (p.groups)
+        p.transient = std::max<uint64_t>(p.transient, 4 * n * (32 + 8 + 8 + 4 + 4 + 4 + 4 + 4 + 4) + 5 * n * 192 +
+                                                          5 * seg * (192 + 96) + msm_table_build_bytes(5 * seg));
+    return p;
+}
+
+// The key-load budget: the rank's share of its GPU's free HBM (ranks on one
+// device split it) against hbm_plan.  The optional tables that do not fit are
+// switched off on every rank (the proof bytes do not change); when even the
+// mandatory part does not fit, every rank's load fails with PNP_E_NOMEM and a
+// message naming the rank and the bytes, instead of one rank running out of
+// memory mid-proof and its peers failing in an exchange.  PNP_HBM_LIMIT
+// (bytes) caps the budget (tests).
+static uint64_t device_key(int dev) {
+    char bus[64] = {0};
+    if (hipDeviceGetPCIBusId(bus, sizeof bus, dev) != hipSuccess) snprintf(bus, sizeof bus, "dev%d", dev);
+    uint64_t h = 1469598103934665603ULL;  // FNV-1a
+    for (const char *c = bus; *c; c++) h = (h ^ (uint8_t)*c) * 1099511628211ULL;
+    return h;
+}
+void hbm_budget(pnp_ctx *ctx) {
+    MsmWork &wk = ctx->msm;
+    const int W = wk.world > 1 && wk.allgather ? wk.world : 1;
+    uint64_t share = 1;
+    if (W > 1) {  // (also the barrier after which every rank's key load has allocated)
+        const uint64_t id = device_key(ctx->device);
+        share = 0;
+        for (uint64_t v : rank_allgather(wk, ctx->stream, &id, 1, PNP_EX_TAG_DEVICE)) share += v == id;
+    }
+    size_t fr = 0, tot = 0;
+    PNP_HIP(hipMemGetInfo(&fr, &tot));
+    uint64_t budget = fr / std::max<uint64_t>(share, 1);
+    if (const char *e = getenv("PNP_HBM_LIMIT")) {
+        const uint64_t lim = strtoull(e, nullptr, 0), live = g_dev_live.load();
+        budget = std::min<uint64_t>(budget, lim > live ? lim - live : 0);
+    }
+    const HbmPlan p = hbm_plan(ctx, ctx->pk_n);
+    const uint64_t base = p.mandatory + p.transient;
+    uint64_t mine[5];
+    mine[0] = base <= budget;
+    mine[1] = lagrange_enabled() && base + p.lag <= budget;
+    mine[2] = mine[1] && wire_groups_enabled() && base + p.lag + p.groups <= budget;
+    mine[3] = base;
+    mine[4] = budget;
+    std::vector<uint64_t> all(mine, mine + 5);
+    if (W > 1) all = rank_allgather(wk, ctx->stream, mine, 5, PNP_EX_TAG_STATUS);
+    bool ok = true, lag = true, groups = true;
+    int bad = -1;
+    for (int r = 0; r < W; r++) {
+        if (!all[5 * r] && bad < 0) bad = r;
+        ok &= all[5 * r] != 0;
+        lag &= all[5 * r + 1] != 0;
+        groups &= all[5 * r + 2] != 0;
+    }
+    ctx->hbm_lag_off = !lag;
+    ctx->hbm_groups_off = !groups;
+    if (!ok) {
+        ctx->pk_loaded = false;
+        set_error("HBM budget: rank %d of %d needs %.2f GiB more for a proof at n = %llu, %.2f GiB free to it "
+                  "(%llu rank(s) on this rank's GPU)", bad, W, all[5 * bad + 3] / 1073741824.0,
+                  (unsigned long long)ctx->pk_n, all[5 * bad + 4] / 1073741824.0, (unsigned long long)share);
+        throw Error(PNP_E_NOMEM);
+    }
 }
 
 void commit_evals_batch(pnp_ctx *ctx, const uint64_t *const *d_evals, int B, uint64_t n, CommitmentC *const *out) {
@@ -315,6 +476,18 @@ int pnp_set_exchange_v(pnp_ctx *ctx, pnp_alltoallv_fn alltoallv, void *user, uin
     return PNP_OK;
 }
 
+int pnp_set_exchange_ordered(pnp_ctx *ctx, int ordered) {
+    if (!ctx) return PNP_E_ARG;
+    ctx->msm.ordered = ordered != 0;
+    return PNP_OK;
+}
+
+int pnp_ctx_stream(pnp_ctx *ctx, void **stream) {
+    if (!ctx || !stream) return PNP_E_ARG;
+    *stream = ctx->stream;
+    return PNP_OK;
+}
+
 int pnp_sync(pnp_ctx *ctx) {
     PNP_TRY(PNP_HIP(hipStreamSynchronize(ctx->stream)));
 }
@@ -370,6 +543,20 @@ int pnp_commit_evals(pnp_ctx *ctx, const uint64_t *d_evals, uint64_t n, Commitme
         CommitmentC *o[1] = {out};
         const uint64_t *e[1] = {d_evals};
         commit_evals_batch(ctx, e, 1, n, o);
+    });
+}
+
+int pnp_hbm_usage(pnp_ctx *ctx, uint64_t out[6]) {
+    if (!out) return PNP_E_ARG;
+    PNP_TRY({
+        out[0] = g_dev_live.load();
+        out[1] = g_dev_peak.exchange(out[0]);  // the peak since the previous call
+        pnp::HbmPlan p;
+        if (ctx && ctx->pk_loaded) p = pnp::hbm_plan(ctx, ctx->pk_n);
+        out[2] = p.mandatory;
+        out[3] = p.lag;
+        out[4] = p.groups;
+        out[5] = p.transient;
     });
 }
 
@@ -695,6 +882,7 @@ int pnp_load_prover_key(pnp_ctx *ctx, const ProverKeyC *pk, uint64_t D, int devi
         ctx->pk_dev = dev;
         ctx->pk_n = D;
         ctx->pk_loaded = true;
+        pnp::hbm_budget(ctx);
     });
 }
 

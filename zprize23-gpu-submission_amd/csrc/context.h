@@ -75,6 +75,7 @@ struct pnp_ctx {
     // (the padding rows: z is constant there).
     struct WireBases {
         bool built = false, ok = false, wires_ok = false, z_ok = false;
+        bool sliced = false;            // the table holds this rank's point range of each segment
         uint64_t n = 0, total = 0, m = 0, len = 0;  // domain, bases, largest group count, MSM length
         uint64_t g[5] = {}, off[5] = {};
         bool ident[5] = {};             // ungrouped wire: its scalars are its evaluations
@@ -86,6 +87,9 @@ struct pnp_ctx {
         uint64_t pk_gen = 0;            // prover-key load the sigma check last covered
     } wb;
     uint64_t pk_gen = 0;                // incremented by every pnp_load_prover_key
+    // the key-load HBM budget (pnp_load_prover_key) left no room for these
+    // optional tables: the prover commits without them (same proof bytes)
+    bool hbm_lag_off = false, hbm_groups_off = false;
 
     // ---- per-proof working set (sized on first use, reused) ----
     std::map<std::string, pnp::DevBuf> work;
@@ -98,6 +102,20 @@ struct pnp_ctx {
 };
 
 namespace pnp {
+// bytes a proof at domain n still has to allocate on this rank (abi.cpp)
+struct HbmPlan {
+    uint64_t mandatory = 0;  // per-proof buffers, NTT tables, commit-key table, MSM work
+    uint64_t lag = 0;        // the Lagrange-basis key and its folded table (optional)
+    uint64_t groups = 0;     // the copy-constraint groups and their table (optional)
+    uint64_t transient = 0;  // the largest build scratch on top of them
+};
+HbmPlan hbm_plan(pnp_ctx *ctx, uint64_t n);
+// multi-GPU: AND of every rank's `mine` (one tagged all-gather); world 1: mine
+bool all_ranks_ok(pnp_ctx *ctx, bool mine);
+bool lagrange_enabled();
+// the key-load HBM budget (sets hbm_lag_off / hbm_groups_off, or throws PNP_E_NOMEM)
+void hbm_budget(pnp_ctx *ctx);
+bool wire_groups_enabled();
 Fr root_of_unity(uint32_t lg);
 Fr fr_from_u64(uint64_t x);
 // drop everything derived from the resident SRS (folded tables, Lagrange basis)

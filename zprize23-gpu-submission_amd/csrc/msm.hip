@@ -973,6 +973,29 @@ static void sort_group(MsmWork &wk, MsmGroup &gb, const uint32_t *keys, const Gr
     PNP_HIP(hipMemcpyAsync(bstart + WB, counts + ncount, 4, hipMemcpyDeviceToDevice, s));
 }
 
+// entries per accumulation lane for nent sorted entries
+static uint32_t acc_segment(uint64_t nent, bool folded) {
+    uint32_t S = (uint32_t)std::max<uint64_t>(64, (nent >> 20) & ~7ULL);
+    if (!folded) return S;
+    // whole rounds of resident waves: the lane count a multiple of the chip's
+    // wave slots (CUs x 4 SIMDs x PNP_ACC_WAVES x 64 lanes), so the last round
+    // does not run a fraction of the chip
+    static uint64_t slots = 0;
+    if (!slots) {
+        int dev = 0, cus = 0;
+        PNP_HIP(hipGetDevice(&dev));
+        PNP_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+        slots = (uint64_t)cus * 4 * PNP_ACC_WAVES * 64;
+    }
+    const uint64_t per = (nent + slots - 1) / slots;  // entries per lane in one round
+    const uint64_t rounds = std::max<uint64_t>(1, per / S);
+    // a batch smaller than one round at S = 64 (one MSM of a 2^19-point rank
+    // range: ~35 entries per lane) takes shorter segments and fills the chip
+    // instead of leaving part of it idle (more bucket pieces to merge, a few %
+    // of the additions)
+    return (uint32_t)std::max<uint64_t>(16, (per + rounds - 1) / rounds);
+}
+
 // buckets of the group (XYZZ, R384) into gb.buckets
 // nent: entries (upper bound) in the sorted list; alg_bytes: SURVEY 8(d)
 // bytes credited to the launch (0: the group's points x 128 B per window)
@@ -992,26 +1015,7 @@ static void accumulate_group(MsmWork &wk, MsmGroup &gb, const GroupPlan &gp, con
     if (wk.timer) wk.timer->begin("msm_accumulate", s, ev0);
     // balanced accumulate: S entries per thread, S >= 64 or ~2^20 lanes (every
     // bucket piece beyond the first costs an addition in msm_merge_pieces)
-    uint32_t S = (uint32_t)std::max<uint64_t>(64, (nent >> 20) & ~7ULL);
-    if (table) {
-        // whole rounds of resident waves: the lane count a multiple of the
-        // chip's wave slots (CUs x 4 SIMDs x PNP_ACC_WAVES x 64 lanes), so the
-        // last round does not run a fraction of the chip
-        static uint64_t slots = 0;
-        if (!slots) {
-            int dev = 0, cus = 0;
-            PNP_HIP(hipGetDevice(&dev));
-            PNP_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-            slots = (uint64_t)cus * 4 * PNP_ACC_WAVES * 64;
-        }
-        const uint64_t per = (nent + slots - 1) / slots;  // entries per lane in one round
-        const uint64_t rounds = std::max<uint64_t>(1, per / S);
-        // a batch smaller than one round at S = 64 (one MSM of a 2^19-point
-        // rank range: ~35 entries per lane) takes shorter segments and fills
-        // the chip instead of leaving part of it idle (more bucket pieces to
-        // merge, a few % of the additions)
-        S = (uint32_t)std::max<uint64_t>(16, (per + rounds - 1) / rounds);
-    }
+    const uint32_t S = acc_segment(nent, table != nullptr);
     const uint64_t nthr = (nent + S - 1) / S;
     if (table) {
         // raw radix-2^29 pieces: buckets inside one segment, then heads, tails
@@ -1264,6 +1268,45 @@ static void msm_local_batch(MsmWork &wk, const uint64_t *d_points, const uint64_
     }
 }
 
+// One all-gather of k words per rank through the MSM exchange buffer, every
+// slot closed by a tag word naming the exchange (pnp_plonk.h PNP_EX_TAG_*):
+// an exchange harness can tell the messages apart without guessing from their
+// sizes, and a peer whose tag differs is a rank at another point of the
+// protocol (one that failed and left, or a mismatched build) — reported as
+// such instead of as a garbled result.  Returns world x k words (rank-major,
+// tags removed).
+std::vector<uint64_t> rank_allgather(MsmWork &wk, hipStream_t s, const uint64_t *mine, int k, uint64_t tag) {
+    const int W = wk.world;
+    const uint64_t words = (uint64_t)k + 1, slot = 8 * words;
+    if (!wk.allgather || wk.xbuf_bytes < slot * W) {
+        set_error("exchange buffer %llu B < %llu B (tag %llx)", (unsigned long long)wk.xbuf_bytes,
+                  (unsigned long long)(slot * W), (unsigned long long)tag);
+        throw Error(PNP_E_ARG);
+    }
+    std::vector<uint64_t> buf(words);
+    std::copy(mine, mine + k, buf.begin());
+    buf[k] = tag;
+    PNP_HIP(hipMemcpyAsync(wk.xbuf + words * wk.rank, buf.data(), slot, hipMemcpyHostToDevice, s));
+    ex_fence(wk, s);
+    if (int rc = wk.allgather(wk.user, slot)) {
+        set_error("all-gather (tag %llx) failed (%d): a peer rank left the proof", (unsigned long long)tag, rc);
+        throw Error(PNP_E_DEVICE);
+    }
+    std::vector<uint64_t> all(words * W);
+    PNP_HIP(hipMemcpyAsync(all.data(), wk.xbuf, all.size() * 8, hipMemcpyDeviceToHost, s));
+    PNP_HIP(hipStreamSynchronize(s));
+    std::vector<uint64_t> out((size_t)k * W);
+    for (int r = 0; r < W; r++) {
+        if (all[words * r + k] != tag) {
+            set_error("all-gather tag %llx from rank %d, expected %llx: the ranks are out of step",
+                      (unsigned long long)all[words * r + k], r, (unsigned long long)tag);
+            throw Error(PNP_E_DEVICE);
+        }
+        std::copy(all.begin() + words * r, all.begin() + words * r + k, out.begin() + (size_t)k * r);
+    }
+    return out;
+}
+
 // k * P on the host (double and add from k's top bit: the bucket-range weight
 // offsets are < 2^19, ~20 doublings, a few microseconds each in host Fq)
 static Xyzz mul_small(const Xyzz &p, uint64_t k) {
@@ -1357,27 +1400,12 @@ static bool msm_bucket_batch(MsmWork &wk, const uint64_t *const *sc, int B, uint
     // destination d starts at offs[((d B + v) nbl + l) nch]) and its record bytes
     const uint64_t per_d = (uint64_t)B * nbl;
     auto bin_off = [&](uint64_t gbin) { return offs[gbin * nch]; };
-    std::vector<uint64_t> send_b(W + 1), recv_b(W);
+    std::vector<uint64_t> send_b(W), recv_b(W);
     for (int d = 0; d < W; d++) send_b[d] = 8ULL * (bin_off((d + 1) * per_d) - bin_off(d * per_d));
-    send_b[W] = 0xB0C4E7C0u;  // tag: a slot size and content no other exchange of the proof uses
-    // 3. every rank's totals (one all-gather of W + 1 words per rank): the
+    // 3. every rank's totals (one all-gather of W words per rank): the
     // receive sizes and the common overflow verdict
-    const uint64_t slot = 8ULL * (W + 1);
-    if (wk.xbuf_bytes < slot * W) {
-        set_error("msm bucket shard: exchange buffer %llu B < %llu B", (unsigned long long)wk.xbuf_bytes,
-                  (unsigned long long)(slot * W));
-        throw Error(PNP_E_ARG);
-    }
-    PNP_HIP(hipMemcpyAsync(wk.xbuf + (uint64_t)wk.rank * (W + 1), send_b.data(), slot, hipMemcpyHostToDevice, s));
-    PNP_HIP(hipStreamSynchronize(s));
-    if (int rc = wk.allgather(wk.user, slot)) {
-        set_error("msm bucket shard: count all-gather failed (%d)", rc);
-        throw Error(PNP_E_DEVICE);
-    }
-    std::vector<uint64_t> all((size_t)W * (W + 1));
-    PNP_HIP(hipMemcpyAsync(all.data(), wk.xbuf, all.size() * 8, hipMemcpyDeviceToHost, s));
-    PNP_HIP(hipStreamSynchronize(s));
-    auto cnt = [&](int from, int to) { return all[(size_t)from * (W + 1) + to]; };
+    const std::vector<uint64_t> all = rank_allgather(wk, s, send_b.data(), W, PNP_EX_TAG_COUNTS);
+    auto cnt = [&](int from, int to) { return all[(size_t)from * W + to]; };
     const uint64_t bins_bytes = 4 * per_d * W;  // the bin-count exchange below
     bool fits = bins_bytes <= wk.v_bytes;
     for (int r = 0; r < W; r++) {
@@ -1398,7 +1426,7 @@ static bool msm_bucket_batch(MsmWork &wk, const uint64_t *const *sc, int B, uint
         std::vector<uint32_t> bc((size_t)per_d * W);
         for (uint64_t gbin = 0; gbin < per_d * W; gbin++) bc[gbin] = bin_off(gbin + 1) - bin_off(gbin);
         PNP_HIP(hipMemcpyAsync(wk.v_send, bc.data(), bc.size() * 4, hipMemcpyHostToDevice, s));
-        PNP_HIP(hipStreamSynchronize(s));
+        ex_fence(wk, s);
         std::vector<uint64_t> eq(W, 4 * per_d);
         if (int rc = wk.alltoallv(wk.v_user, eq.data(), eq.data())) {
             set_error("msm bucket shard: bin-count all-to-all failed (%d)", rc);
@@ -1491,6 +1519,37 @@ static bool msm_bucket_batch(MsmWork &wk, const uint64_t *const *sc, int B, uint
     return true;
 }
 
+// ---- HBM of the MSM machinery (upper bounds for the key-load budget,
+// abi.cpp hbm_plan; checked against the measured peak by tests/test_gpu_hbm.py)
+uint64_t msm_table_bytes(uint64_t n_points, uint64_t n_cfg, int fold_c) {
+    return (uint64_t)msm_cfg(n_cfg, fold_c, true).W * n_points * PT29 * 4;
+}
+uint64_t msm_table_build_bytes(uint64_t n_points) { return n_points * (96 + 96 + 192 + 48); }
+// a batch of B folded MSMs over n_pts points of a table configured for n_cfg;
+// v_bytes: the bucket-range record capacity (0: point ranges / one GPU)
+uint64_t msm_work_bytes(uint64_t n_pts, uint64_t n_cfg, int fold_c, int B, uint64_t v_bytes) {
+    const MsmCfg g = msm_cfg(n_cfg, fold_c, true);
+    const uint64_t WB = (uint64_t)B * g.NB;
+    uint64_t nent = (uint64_t)B * g.W * n_pts;  // the dense bound the buffers are sized for
+    const uint64_t digits = nent * 4;
+    uint64_t sort = nent * (4 + 2 + 4) + (uint64_t)B * 512 * 1024 * 4 + (WB + 1) * 4;
+    if (v_bytes) {  // bucket ranges: the received records are sorted and accumulated
+        nent = std::max<uint64_t>(nent, v_bytes / 8);
+        sort += nent * 4;
+    }
+    const uint64_t S = std::max<uint32_t>(16, acc_segment(nent, true));
+    const uint64_t nthr = (nent + S - 1) / S;
+    const uint64_t acc = (WB + 2 * nthr) * 224 + nthr * 12 + (WB + 1) * 4 + (WB * 24 + WB * 72 + 64) * 8;
+    return digits + sort + acc;
+}
+uint64_t msm_work_held(const MsmWork &wk) {
+    uint64_t b = wk.digits.bytes + wk.part_counts.bytes + wk.rec_counts.bytes;
+    for (const MsmGroup &g : wk.grp)
+        b += g.counts.bytes + g.offsets.bytes + g.scan_tmp.bytes + g.ent.bytes + g.fkey.bytes + g.sorted.bytes +
+             g.buckets.bytes + g.seg.bytes + g.redo.bytes + g.exc.bytes + g.heavy.bytes + g.wctr.bytes;
+    return b;
+}
+
 void msm_point_range(uint64_t n, int rank, int world, uint64_t &p0, uint64_t &p1) {
     const uint64_t per = (n + world - 1) / world;
     p0 = std::min<uint64_t>((uint64_t)rank * per, n);
@@ -1519,31 +1578,20 @@ void msm_run_batch(MsmWork &wk, const uint64_t *d_points, const uint64_t *const 
     std::vector<const uint64_t *> sc(B);
     for (int b = 0; b < B; b++) sc[b] = scalars_local ? d_scalars[b] : d_scalars[b] + 4 * p0;
     std::vector<uint64_t> part((size_t)B * 24);
-    // bucket ranges (the folded table covers all n points) or point ranges;
-    // a segmented table always covers every point of its sets
-    const bool full = table && (wk.full_table() || segs);
+    // bucket ranges (the folded table covers all n points) or point ranges; a
+    // segmented table covers every point of its sets, or (sliced) this rank's
+    // range of each
+    const bool full = table && (wk.full_table() || (segs && !segs->sliced));
     const uint64_t n_tab = segs ? segs->n_table : n;
     const uint64_t *off = segs ? segs->off : nullptr;
-    if (!(table && wk.full_table() && msm_bucket_batch(wk, sc.data(), B, n_tab, p0, p1, part.data(), s, table, off)))
-        msm_local_batch(wk, d_points ? d_points + 12 * p0 : nullptr, sc.data(), B, p1 - p0, part.data(), s, table,
-                        full ? n_tab : 0, full ? p0 : 0, off);
-    const uint64_t slot = (uint64_t)B * 24 * 8;
-    if (wk.xbuf_bytes < slot * wk.world) {
-        set_error("msm shard: exchange buffer %llu B < %llu B", (unsigned long long)wk.xbuf_bytes,
-                  (unsigned long long)(slot * wk.world));
+    if (segs && segs->sliced && wk.full_table()) {
+        set_error("msm: a sliced segment table in bucket-range mode");
         throw Error(PNP_E_ARG);
     }
-    PNP_HIP(hipMemcpyAsync(wk.xbuf + (uint64_t)wk.rank * B * 24, part.data(), slot,
-                           hipMemcpyHostToDevice, s));
-    PNP_HIP(hipStreamSynchronize(s));
-    int rc = wk.allgather(wk.user, slot);
-    if (rc != 0) {
-        set_error("msm shard: all-gather callback failed (%d)", rc);
-        throw Error(PNP_E_DEVICE);
-    }
-    std::vector<uint64_t> all((size_t)wk.world * B * 24);
-    PNP_HIP(hipMemcpyAsync(all.data(), wk.xbuf, all.size() * 8, hipMemcpyDeviceToHost, s));
-    PNP_HIP(hipStreamSynchronize(s));
+    if (!(table && wk.full_table() && msm_bucket_batch(wk, sc.data(), B, n_tab, p0, p1, part.data(), s, table, off)))
+        msm_local_batch(wk, d_points ? d_points + 12 * p0 : nullptr, sc.data(), B, p1 - p0, part.data(), s, table,
+                        segs ? n_tab : full ? n_tab : 0, full ? p0 : 0, off);
+    const std::vector<uint64_t> all = rank_allgather(wk, s, part.data(), B * 24, PNP_EX_TAG_MSM_SUMS);
     for (int b = 0; b < B; b++) {
         Xyzz acc = Xyzz::inf();
         for (int r = 0; r < wk.world; r++) acc = add(acc, get_xyzz(&all[((size_t)r * B + b) * 24]));

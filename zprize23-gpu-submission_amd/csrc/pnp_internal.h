@@ -164,10 +164,23 @@ struct MsmWork {
     void *v_user = nullptr;
     uint64_t *v_send = nullptr, *v_recv = nullptr;
     uint64_t v_bytes = 0;
+    // the exchange callbacks enqueue their collectives on the library's
+    // stream (pnp_set_exchange_ordered: RCCL on pnp_ctx_stream): the data they
+    // move is ordered behind the work that made it, no host synchronisation
+    // before a callback; otherwise (host-memory exchanges) the stream is
+    // synchronised first
+    bool ordered = false;
     // the folded table covers ALL n points (bucket ranges gather any point)
     bool full_table() const { return world > 1 && alltoallv != nullptr; }
     DevBuf part_counts, rec_counts;  // bucket-range pass counts
 };
+// before an exchange callback: the data on the stream is complete
+inline void ex_fence(const MsmWork &wk, hipStream_t s) {
+    if (!wk.ordered) PNP_HIP(hipStreamSynchronize(s));
+}
+// all-gather of k words per rank (rank-major result, world x k), every slot
+// tagged (PNP_EX_TAG_*, include/pnp_plonk.h) and the tags checked
+std::vector<uint64_t> rank_allgather(MsmWork &wk, hipStream_t s, const uint64_t *mine, int k, uint64_t tag);
 // sum_i s_i P_i; scalars Montgomery Fr; result written to host as XYZZ Fq (4x6 u64)
 // `table` (optional): msm_build_table(d_points, n) — the folded layout
 void msm_run(MsmWork &w, const uint64_t *d_points, const uint64_t *d_scalars_mont, uint64_t n,
@@ -178,12 +191,23 @@ void msm_run(MsmWork &w, const uint64_t *d_points, const uint64_t *d_scalars_mon
 struct MsmSegs {
     uint64_t n_table = 0;
     uint64_t off[16] = {};
+    // multi-GPU point ranges: the table holds only this rank's slice [p0, p1)
+    // of every set (msm_point_range of the MSM length), off[] are the slices'
+    // starts in it — 1/world of the full table
+    bool sliced = false;
 };
 // scalars_local: multi-GPU, d_scalars[b] hold only this rank's point range
 // segs: `table` is segmented as above (d_points unused)
 void msm_run_batch(MsmWork &w, const uint64_t *d_points, const uint64_t *const *d_scalars, int B,
                    uint64_t n, uint64_t *h_xyzz, hipStream_t s, const uint64_t *table = nullptr,
                    bool scalars_local = false, const MsmSegs *segs = nullptr);
+// HBM of the MSM machinery, upper bounds (the key-load budget): a folded table
+// over n_points (windows of a table for n_cfg points), its build scratch, the
+// work buffers of a B-MSM batch over n_pts points, and what wk holds now
+uint64_t msm_table_bytes(uint64_t n_points, uint64_t n_cfg, int fold_c);
+uint64_t msm_table_build_bytes(uint64_t n_points);
+uint64_t msm_work_bytes(uint64_t n_pts, uint64_t n_cfg, int fold_c, int B, uint64_t v_bytes);
+uint64_t msm_work_held(const MsmWork &wk);
 // multi-GPU MSMs: the points [p0, p1) rank `rank` of `world` takes
 void msm_point_range(uint64_t n, int rank, int world, uint64_t &p0, uint64_t &p1);
 // T[k*n + i] = 2^(c*k) P_i, k < W (msm_cfg(n)), affine, in the radix-2^29

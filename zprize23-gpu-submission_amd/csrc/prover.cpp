@@ -73,25 +73,9 @@ void set_infinity(CommitmentC *c) {
 
 void store_fr_host(uint64_t out[4], const Fr &a) { to_u64_limbs(a, out); }
 
-// k words from every rank (rank-major) through the MSM exchange buffer
-std::vector<uint64_t> shard_allgather(pnp_ctx *ctx, const uint64_t *mine, int k) {
-    MsmWork &wk = ctx->msm;
-    const uint64_t slot = 8 * (uint64_t)k;
-    if (wk.xbuf_bytes < slot * wk.world) {
-        set_error("exchange buffer %llu B < %llu B", (unsigned long long)wk.xbuf_bytes,
-                  (unsigned long long)(slot * wk.world));
-        throw Error(PNP_E_ARG);
-    }
-    PNP_HIP(hipMemcpyAsync(wk.xbuf + (uint64_t)k * wk.rank, mine, slot, hipMemcpyHostToDevice, ctx->stream));
-    PNP_HIP(hipStreamSynchronize(ctx->stream));
-    if (int rc = wk.allgather(wk.user, slot)) {
-        set_error("all-gather callback failed (%d)", rc);
-        throw Error(PNP_E_DEVICE);
-    }
-    std::vector<uint64_t> all((size_t)k * wk.world);
-    PNP_HIP(hipMemcpyAsync(all.data(), wk.xbuf, all.size() * 8, hipMemcpyDeviceToHost, ctx->stream));
-    PNP_HIP(hipStreamSynchronize(ctx->stream));
-    return all;
+// k words from every rank (rank-major), one tagged all-gather
+std::vector<uint64_t> shard_allgather(pnp_ctx *ctx, const uint64_t *mine, int k, uint64_t tag) {
+    return rank_allgather(ctx->msm, ctx->stream, mine, k, tag);
 }
 
 // In place p <- p / (X - z) (kzg10.cu:87-99) where this rank holds the
@@ -111,7 +95,7 @@ void div_linear_range(pnp_ctx *ctx, uint64_t *d, uint64_t len, const Fr &z, bool
     k_poly_eval(d, len, z, ctx->scratch_a, &e, s);
     uint64_t mine[4];
     to_u64_limbs(e, mine);
-    std::vector<uint64_t> all = shard_allgather(ctx, mine, 4);
+    std::vector<uint64_t> all = shard_allgather(ctx, mine, 4, PNP_EX_TAG_DIV_CARRY);
     const uint64_t n = len * world;  // equal ranges (world divides 8 and n)
     Fr c = Fr::zero();
     for (int r = world - 1; r > rank; r--) c = c * pow_u64(z, n / world) + from_u64_limbs<FrP>(&all[4 * r]);
@@ -672,7 +656,7 @@ int prove_impl(pnp_ctx *ctx, const CircuitC *cs, int device_ptrs, ProofC *out, c
                     PNP_HIP(hipMemcpyAsync(a2a + 4 * ((uint64_t)(r * nb + b) * len), t_blk + 4 * ((uint64_t)b * n + r0),
                                            32 * len, hipMemcpyDeviceToDevice, s));
             }
-            PNP_HIP(hipStreamSynchronize(s));
+            ex_fence(ctx->msm, s);
             int rc = ctx->msm.alltoall(ctx->msm.a2a_user, slot);
             if (rc != 0) {
                 set_error("round-4 all-to-all callback failed (%d)", rc);
@@ -697,7 +681,7 @@ int prove_impl(pnp_ctx *ctx, const CircuitC *cs, int device_ptrs, ProofC *out, c
                 for (int k = 0; k < 8; k++) nz[k] = k < npieces && ((bits >> k) & 1);
             }
             if (dist) {  // a chunk is zero when it is zero on every rank (own slot included)
-                std::vector<uint64_t> all = shard_allgather(ctx, nz, 8);
+                std::vector<uint64_t> all = shard_allgather(ctx, nz, 8, PNP_EX_TAG_T_FLAGS);
                 for (int k = 0; k < 8; k++) {
                     nz[k] = 0;
                     for (int r = 0; r < world; r++) nz[k] |= all[8 * r + k];
@@ -768,7 +752,7 @@ int prove_impl(pnp_ctx *ctx, const CircuitC *cs, int device_ptrs, ProofC *out, c
                 const Fr sz = pow_u64(zc, q0), sw = pow_u64(zw, q0);
                 uint64_t mine[4 * 18];
                 for (int k = 0; k < 18; k++) to_u64_limbs(*vals[k] * (k < 14 ? sz : sw), mine + 4 * k);
-                std::vector<uint64_t> all = shard_allgather(ctx, mine, 4 * 18);
+                std::vector<uint64_t> all = shard_allgather(ctx, mine, 4 * 18, PNP_EX_TAG_EVALS);
                 for (int k = 0; k < 18; k++) {
                     Fr acc = Fr::zero();
                     for (int r = 0; r < world; r++) acc += from_u64_limbs<FrP>(&all[4 * (18 * r + k)]);

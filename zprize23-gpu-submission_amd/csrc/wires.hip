@@ -405,19 +405,26 @@ void build_wire_bases(pnp_ctx *ctx, uint64_t n) {
         bx[4].release();
     }
     if (!wb.wires_ok && !wb.z_ok) return;  // wb.ok stays false (kept with its sigma): commit from the evaluations
-    // 4. affine bases of the n-slot segments (wires a..d, z), one folded table
+    // 4. affine bases of the n-slot segments (wires a..d, z), one folded table;
+    // multi-GPU point ranges (no bucket ranges): only this rank's slice
+    // [p0, p1) of every segment, which is all its MSM share reads
+    wb.sliced = ctx->msm.world > 1 && !ctx->msm.full_table();
+    uint64_t p0 = 0, p1 = n;
+    if (wb.sliced) msm_point_range(n, ctx->msm.rank, ctx->msm.world, p0, p1);
+    const uint64_t sl = p1 - p0;
     wb.total = 0;
     for (int j = 0; j < 5; j++) {
         if (j < 4 ? !wb.wires_ok : !wb.z_ok) continue;
         wb.off[j] = wb.total;
-        wb.total += n;
+        wb.total += sl;
     }
     wb.m = n;
-    {
+    if (wb.total) {
         DevBuf xyzz(wb.total * 192), aff(wb.total * 96);
         for (int j = 0; j < 5; j++) {
             if (!bx[j].p) continue;
-            PNP_HIP(hipMemcpyAsync(xyzz.u64() + 24 * wb.off[j], bx[j].u64(), n * 192, hipMemcpyDeviceToDevice, s));
+            PNP_HIP(hipMemcpyAsync(xyzz.u64() + 24 * wb.off[j], bx[j].u64() + 24 * p0, sl * 192,
+                                   hipMemcpyDeviceToDevice, s));
         }
         PNP_HIP(hipStreamSynchronize(s));
         for (auto &b : bx) b.release();
@@ -451,16 +458,43 @@ bool wire_bases_ready(pnp_ctx *ctx, uint64_t n) {
         if (same) wb.pk_gen = ctx->pk_gen;
         else wb.built = false;
     }
-    if (!wb.built || wb.n != n) build_wire_bases(ctx, n);
+    if (!wb.built || wb.n != n) {
+        // built on the same call on every rank; a rank whose HBM cannot hold
+        // the groups makes every rank commit without them
+        bool fits = true;
+        try {
+            build_wire_bases(ctx, n);
+        } catch (const Error &e) {
+            if (e.code != PNP_E_NOMEM) throw;
+            fits = false;
+        }
+        const bool all = all_ranks_ok(ctx, fits);
+        if (!all) {
+            ctx->wb = pnp_ctx::WireBases{};
+            wb.built = true;
+            wb.n = n;
+            wb.pk_gen = ctx->pk_gen;
+            ctx->hbm_groups_off = true;
+        } else if (ctx->msm.world > 1) {  // the ranks' verdicts come from the same key: check they agree
+            const bool w = all_ranks_ok(ctx, wb.wires_ok), z = all_ranks_ok(ctx, wb.z_ok);
+            if (w != wb.wires_ok || z != wb.z_ok) {
+                set_error("wire groups: the ranks built different groups from one prover key");
+                throw Error(PNP_E_DEVICE);
+            }
+        }
+    }
     return wb.ok;
 }
 
 }  // namespace
 
 void wire_bases_reset(pnp_ctx *ctx) { ctx->wb = pnp_ctx::WireBases{}; }
+bool wire_groups_enabled() { return groups_enabled(); }
 
 bool commit_wires_grouped(pnp_ctx *ctx, const uint64_t *const *d_evals, uint64_t n, CommitmentC *const *out) {
-    if (!groups_enabled() || !lagrange_table(ctx, n) || !wire_bases_ready(ctx, n) || !ctx->wb.wires_ok) return false;
+    if (!groups_enabled() || ctx->hbm_groups_off || !lagrange_table(ctx, n) || !wire_bases_ready(ctx, n) ||
+        !ctx->wb.wires_ok)
+        return false;
     auto &wb = ctx->wb;
     hipStream_t s = ctx->stream;
     uint32_t *flag = static_cast<uint32_t *>(wb.flag.p);
@@ -485,6 +519,7 @@ bool commit_wires_grouped(pnp_ctx *ctx, const uint64_t *const *d_evals, uint64_t
     const uint64_t *sc[4];
     MsmSegs segs;
     segs.n_table = wb.total;
+    segs.sliced = wb.sliced;
     for (int j = 0; j < 4; j++) {
         sc[j] = wb.ident[j] ? d_evals[j] : wb.scal[j].u64();
         segs.off[j] = wb.off[j];
@@ -502,7 +537,9 @@ bool commit_wires_grouped(pnp_ctx *ctx, const uint64_t *const *d_evals, uint64_t
 }
 
 bool commit_z_grouped(pnp_ctx *ctx, const uint64_t *d_z, uint64_t n, CommitmentC *out) {
-    if (!z_groups_enabled() || !lagrange_table(ctx, n) || !wire_bases_ready(ctx, n) || !ctx->wb.z_ok) return false;
+    if (!z_groups_enabled() || ctx->hbm_groups_off || !lagrange_table(ctx, n) || !wire_bases_ready(ctx, n) ||
+        !ctx->wb.z_ok)
+        return false;
     auto &wb = ctx->wb;
     hipStream_t s = ctx->stream;
     uint32_t *flag = static_cast<uint32_t *>(wb.flag.p);
@@ -524,6 +561,7 @@ bool commit_z_grouped(pnp_ctx *ctx, const uint64_t *d_z, uint64_t n, CommitmentC
     const uint64_t *sc[1] = {wb.scal[4].u64()};
     MsmSegs segs;
     segs.n_table = wb.total;
+    segs.sliced = wb.sliced;
     segs.off[0] = wb.off[4];
     uint64_t xyzz[24], aff[12];
     msm_run_batch(ctx->msm, nullptr, sc, 1, wb.len, xyzz, s, wb.table.u64(), false, &segs);

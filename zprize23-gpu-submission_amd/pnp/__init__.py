@@ -35,7 +35,8 @@ SYMBOLS = ("gen_proof", "pnp_last_error", "pnp_ctx_create", "pnp_ctx_destroy",
            "pnp_poly_div_linear", "pnp_prefix_product", "pnp_batch_inverse",
            "pnp_synth_random_fr", "pnp_synth_srs", "pnp_synth_coset_consts", "pnp_synth_circuit",
            "pnp_synth_merkle", "pnp_load_commit_key_strided", "pnp_proof_infinity_mask",
-           "pnp_set_exchange_v", "pnp_commit_segments")
+           "pnp_set_exchange_v", "pnp_commit_segments", "pnp_hbm_usage",
+           "pnp_ctx_stream", "pnp_set_exchange_ordered")
 
 
 # int allgather(void *user, uint64_t bytes_per_rank) — pnp_set_msm_shard
@@ -91,6 +92,9 @@ def load(path: str = LIB_PATH):
     lib.pnp_commit.argtypes = [vp, vp, vp, u64, C.POINTER(abi.CommitmentC)]
     lib.pnp_commit_ck.argtypes = [vp, vp, u64, C.POINTER(abi.CommitmentC)]
     lib.pnp_commit_evals.argtypes = [vp, vp, u64, C.POINTER(abi.CommitmentC)]
+    lib.pnp_hbm_usage.argtypes = [vp, C.POINTER(u64)]
+    lib.pnp_ctx_stream.argtypes = [vp, C.POINTER(vp)]
+    lib.pnp_set_exchange_ordered.argtypes = [vp, i32]
     lib.pnp_commit_segments.argtypes = [vp, vp, u64, i32, C.POINTER(u64), C.POINTER(vp), u64,
                                         C.POINTER(abi.CommitmentC)]
     lib.pnp_poly_eval.argtypes = [vp, vp, u64, vp, vp]
@@ -223,9 +227,16 @@ class Context:
             cb3 = exchange.c_alltoallv()
             check(self.lib.pnp_set_exchange_v(self.h, cb3, None, exchange.vsend.data_ptr(),
                                               exchange.vrecv.data_ptr(), exchange.vsend.numel() * 8),
-                  "pnp_set_exchange_v", "pnp_commit_segments")
+                  "pnp_set_exchange_v", "pnp_commit_segments", "pnp_hbm_usage",
+           "pnp_ctx_stream", "pnp_set_exchange_ordered")
             keep.append(cb3)
         self._exchange = keep  # keep the callbacks alive
+
+    def hbm_usage(self) -> dict:
+        """pnp_hbm_usage: bytes held / peak, and the key-load plan's parts."""
+        o = (C.c_uint64 * 6)()
+        check(self.lib.pnp_hbm_usage(self.h, o), "pnp_hbm_usage")
+        return dict(zip(("live", "peak", "mandatory", "lagrange", "groups", "transient"), list(o)))
 
     def kernel_stats(self, name: str):
         ms, cnt = C.c_double(), C.c_int()

@@ -166,31 +166,40 @@ class SoloExchange(WindowExchange):
         self.gather_bytes = self.a2a_bytes_moved = self.v_bytes_moved = 0
         self.error = None
 
-    # the 8-word exchange of the quotient chunks' non-zero flags (prover.cpp):
-    # the loopback all-to-all hands this rank its own blocks in every slot, so
-    # its t_7 / t_8 come out non-zero where the real distributed quotient of a
-    # satisfying circuit has them zero; the flags say zero, as every real
-    # rank would, so the rank commits the same 6 chunks as in the real run
-    T_FLAGS_BYTES = 64
-
-    # the bucket-range count exchange (msm.hip msm_bucket_batch): world counts
-    # + this tag word per rank
-    COUNT_TAG = 0xB0C4E7C0
+    # Every all-gather slot ends with the library's tag word (include/
+    # pnp_plonk.h PNP_EX_TAG_*); the loopback treats two messages specially:
+    #  * the quotient chunks' non-zero flags (prover.cpp): the loopback
+    #    all-to-all hands this rank its own blocks in every slot, so its t_7 /
+    #    t_8 come out non-zero where the real distributed quotient of a
+    #    satisfying circuit has them zero; the flags say zero, as every real
+    #    rank would, so the rank commits the same 6 chunks as in the real run;
+    #  * the bucket-range counts (msm.hip msm_bucket_batch): "rank s" sends
+    #    this rank what this rank sends rank s (alltoallv below returns those
+    #    segments), so this rank accumulates as many distinct entries as a real
+    #    rank, spread over its bucket range like a real rank's.
+    #  * the key load's device ids (abi.cpp hbm_budget): the other ranks of a
+    #    real run have GPUs of their own, so their slots get other ids (the
+    #    rank's HBM budget is its whole GPU, as in the real run).
+    TAG_T_FLAGS = 0x7F1A6500
+    TAG_COUNTS = 0xB0C4E7C0
+    TAG_DEVICE = 0xDE71CE00
+    TAGS = (0xB0C4E7C0, 0x5EC7A111, 0x7F1A6500, 0xD1FC0001, 0xE7A15000, 0x57A7A500, 0xDE71CE00)
 
     def gather(self, bytes_per_rank: int) -> None:
         import torch
         w = bytes_per_rank // 8
         mine = self.buf[self.rank * w:(self.rank + 1) * w].clone()
-        if bytes_per_rank == self.T_FLAGS_BYTES:
+        tag = int(mine[-1]) & 0xFFFFFFFFFFFFFFFF
+        if tag not in self.TAGS:
+            raise ValueError(f"untagged all-gather slot ({bytes_per_rank} B, last word {tag:#x})")
+        if tag == self.TAG_T_FLAGS:
             mine[6:8] = 0
         slots = self.buf[: w * self.world].view(self.world, w)
         slots.copy_(mine.expand(self.world, w))
-        if w == self.world + 1 and int(mine[-1]) == self.COUNT_TAG:
-            # bucket-range counts: "rank s" sends this rank what this rank sends
-            # rank s (alltoallv below returns those segments), so this rank
-            # accumulates as many distinct entries as a real rank, spread over
-            # its bucket range like a real rank's
+        if tag == self.TAG_COUNTS:
             slots[:, self.rank] = mine[: self.world]
+        if tag == self.TAG_DEVICE:
+            slots[:, 0] += torch.arange(self.world, device=slots.device) - self.rank
         torch.cuda.current_stream().synchronize()
         self.calls += 1
         self.gather_bytes += bytes_per_rank * self.world
