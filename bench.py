@@ -362,11 +362,12 @@ def drop_in(ctx, syn, steps: int, v1: bool):
     headline: (a) v2 pnp_prove with the witness in HOST memory (CircuitC as
     prove_pnp builds it, prover.rs:727-762: ~4 x 3.16 M x 32 B over PCIe,
     inside the timed call); (b) the v1 symbol gen_proof with every key in host
-    memory, by default uploading both keys on every call as the reference does
-    (load.cu:311-358; the folded SRS table is kept when the uploaded SRS is
-    unchanged), and with PNP_V1_REUSE=1 (resident keys reused by fingerprint:
-    only the witness is uploaded).  Not `value`: the headline has inputs
-    already in HBM."""
+    memory: uploading both keys on every call as the reference does
+    (PNP_V1_RELOAD=1, load.cu:311-358; the folded SRS table is kept when the
+    uploaded SRS is unchanged), the default (every word of both keys hashed on
+    the host each call, a key uploaded only when its content changed), and
+    PNP_V1_REUSE=1 (resident keys reused by a sampled fingerprint).  Not
+    `value`: the headline has inputs already in HBM."""
     import torch
     from pnp import abi
     cs_h, pk_h, ck_h, keep = host_copy(syn)
@@ -383,7 +384,13 @@ def drop_in(ctx, syn, steps: int, v1: bool):
         lib = ctx.lib
         ref = abi.proof_to_bytes(ctx.prove(syn.cs, device_ptrs=True))
         same = True
-        for mode in ("reload", "reuse"):
+        # reload: upload both keys every call (the reference's load.cu:311-358);
+        # hash (the default): every word of both keys hashed on the host, an
+        # unchanged key not uploaded again; reuse: the sampled fingerprint
+        for mode in ("reload", "hash", "reuse"):
+            os.environ.pop("PNP_V1_RELOAD", None)
+            if mode == "reload":
+                os.environ["PNP_V1_RELOAD"] = "1"
             if mode == "reuse":
                 os.environ["PNP_V1_REUSE"] = "1"
             t0 = time.perf_counter()
@@ -396,6 +403,7 @@ def drop_in(ctx, syn, steps: int, v1: bool):
             out[f"v1_{mode}_gen_proof_s"] = round((time.perf_counter() - t0) / steps, 4)
             same &= abi.proof_to_bytes(p) == ref
         os.environ.pop("PNP_V1_REUSE", None)
+        os.environ.pop("PNP_V1_RELOAD", None)
         out["v1_equals_v2"] = same
     del keep
     torch.cuda.synchronize()

@@ -182,10 +182,11 @@ def test_full_size_height15_properties(circuit):
 
 
 def test_v1_reloads_mutated_key(monkeypatch):
-    """The v1 symbol keeps the reference's per-call key copy (load.cu:311-358):
+    """The v1 symbol keeps the reference's per-call key read (load.cu:311-358):
     a caller that rewrites its key buffers in place between two calls (same
     pointers, a change in words the reuse fingerprint does not sample) gets a
-    proof over the NEW key, byte-identical to the oracle's; an unchanged SRS
+    proof over the NEW key, byte-identical to the oracle's — the default hashes
+    every word the load reads and uploads only a changed key; an unchanged SRS
     keeps its folded table (device-side comparison) and the proof stays exact.
     With PNP_V1_REUSE=1 (opt-in: the caller promises immutable keys) the
     resident copy is reused and the second proof is the stale one."""
@@ -205,6 +206,18 @@ def test_v1_reloads_mutated_key(monkeypatch):
     assert abi.proof_to_bytes(exp) != abi.proof_to_bytes(first)
     second = lib.gen_proof(inp.circuit, inp.pk, inp.ck)
     assert abi.proof_to_bytes(second) == abi.proof_to_bytes(exp)
+    # the default compares the full-content hash of every array the load reads:
+    # an unchanged key is not uploaded again (same proof), a changed word of a
+    # zero selector's evaluations or of the SRS is seen
+    again = lib.gen_proof(inp.circuit, inp.pk, inp.ck)
+    assert abi.proof_to_bytes(again) == abi.proof_to_bytes(exp)
+    pts = inp.arrays["srs"]
+    keep_pt = pts[7].copy()
+    pts[7] = pts[9]  # a different curve point at index 7: every commitment moves
+    exp_ck = inp.oracle_proof()
+    assert abi.proof_to_bytes(lib.gen_proof(inp.circuit, inp.pk, inp.ck)) == abi.proof_to_bytes(exp_ck)
+    pts[7] = keep_pt
+    assert abi.proof_to_bytes(lib.gen_proof(inp.circuit, inp.pk, inp.ck)) == abi.proof_to_bytes(exp)
     # the opt-in reuse: a third call on a reverted key returns the resident
     # (mutated-key) proof, then a reload once the switch is off again
     qc[3] = saved

@@ -5,7 +5,9 @@
 // synchronous, device 0, print-and-exit on device errors (caffe/common.hpp:
 // 23-30).  v2 functions return PNP_* codes and never exit.
 #include <algorithm>
+#include <array>
 #include <atomic>
+#include <thread>
 #include <stdarg.h>
 #include <stdlib.h>
 #include <string.h>
@@ -1061,6 +1063,111 @@ uint64_t pk_fingerprint(const ProverKeyC &pk, uint64_t D) {
     }
     return h;
 }
+// Full-content key hash (the v1 default): every word of every array the key
+// load reads, hashed on the host by up to 16 threads (memory-bound: ~17 GiB at
+// HEIGHT=15 in ~0.1-0.2 s, against ~0.55 s to upload it over PCIe), so an
+// unchanged key is not uploaded again while any change — in any word — is.
+// Per 8 MiB chunk a 4-lane multiply-fold hash (two 64-bit digests of the four
+// lane states) and the OR of its words (a selector's all-zero test), chunks
+// combined in order.
+struct Seg {
+    const uint64_t *p;
+    uint64_t words;
+};
+struct SegHash {
+    uint64_t h0 = 0, h1 = 0;
+    bool nz = false;
+};
+inline uint64_t rotl64(uint64_t x, int r) { return (x << r) | (x >> (64 - r)); }
+inline uint64_t mum(uint64_t a, uint64_t b) {  // 64 x 64 -> 128, folded (wyhash's mixer)
+    const unsigned __int128 t = (unsigned __int128)a * b;
+    return (uint64_t)t ^ (uint64_t)(t >> 64);
+}
+void hash_chunk(const uint64_t *p, uint64_t w, uint64_t seed, uint64_t out[3]) {
+    // 4 independent lanes, one 128-bit product per word: ~1 word per cycle,
+    // faster than host memory
+    const uint64_t K[4] = {0xa0761d6478bd642fULL, 0xe7037ed1a0b428dbULL, 0x8ebc6af09c88c6e3ULL,
+                           0x589965cc75374cc3ULL};
+    uint64_t a[4] = {seed ^ K[0], seed ^ K[1], seed ^ K[2], seed ^ K[3]};
+    uint64_t o = 0, i = 0;
+    for (; i + 4 <= w; i += 4) {
+        for (int k = 0; k < 4; k++) {
+            const uint64_t v = p[i + k];
+            o |= v;
+            a[k] = mum(v ^ a[k], K[k]) ^ v;
+        }
+    }
+    for (; i < w; i++) {
+        o |= p[i];
+        a[0] = mum(p[i] ^ a[0], K[0]) ^ p[i];
+    }
+    out[0] = mix64(mix64(mix64(mix64(w, a[0]), a[1]), a[2]), a[3]);
+    out[1] = mum(a[0] ^ K[2], a[1] ^ K[3]) ^ mum(a[2] ^ K[0], a[3] ^ K[1]) ^ w;
+    out[2] = o;
+}
+std::vector<SegHash> hash_segments(const std::vector<Seg> &segs) {
+    const uint64_t CH = 1 << 20;  // words per chunk (8 MiB)
+    struct Job {
+        int seg;
+        uint64_t off, w;
+    };
+    std::vector<Job> jobs;
+    for (int k = 0; k < (int)segs.size(); k++)
+        for (uint64_t o = 0; o < segs[k].words; o += CH) jobs.push_back({k, o, std::min(CH, segs[k].words - o)});
+    std::vector<uint64_t> res(jobs.size() * 3);
+    std::atomic<size_t> next{0};
+    auto work = [&]() {
+        for (size_t j; (j = next.fetch_add(1)) < jobs.size();)
+            hash_chunk(segs[jobs[j].seg].p + jobs[j].off, jobs[j].w, jobs[j].off, &res[3 * j]);
+    };
+    unsigned T = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    if (const char *e = getenv("OMP_NUM_THREADS")) T = std::max(1, std::min(atoi(e), 64));
+    T = (unsigned)std::min<size_t>(T, std::max<size_t>(1, jobs.size()));
+    std::vector<std::thread> th;
+    for (unsigned t = 1; t < T; t++) th.emplace_back(work);
+    work();
+    for (auto &t : th) t.join();
+    std::vector<SegHash> out(segs.size());
+    for (size_t j = 0; j < jobs.size(); j++) {
+        SegHash &h = out[jobs[j].seg];
+        h.h0 = mix64(h.h0, res[3 * j]);
+        h.h1 = mix64(h.h1, res[3 * j + 1]);
+        h.nz |= res[3 * j + 2] != 0;
+    }
+    return out;
+}
+// the prover key as pnp_load_prover_key reads it at domain D: the fields it
+// copies, the selector evaluations it tests, and a selector's coefficients
+// only when its evaluations are non-zero (an all-zero selector's coefficient
+// Vec is empty, lib.rs:157-223)
+std::array<uint64_t, 2> pk_content_hash(const ProverKeyC &pk, uint64_t D) {
+    uint64_t *const *f = reinterpret_cast<uint64_t *const *>(&pk);
+    std::vector<Seg> segs;
+    std::vector<int> field;
+    for (int i = 0; i < 44; i++) {
+        const FieldKind k = kPkKinds[i];
+        if (k == kSkip || k == kSelCoeffs || !f[i]) continue;
+        segs.push_back({f[i], 4 * ((k == kEvals8 || k == kSelEvals8) ? 8 * D : D)});
+        field.push_back(i);
+    }
+    std::vector<SegHash> h = hash_segments(segs);
+    std::vector<Seg> sel;
+    for (size_t j = 0; j < segs.size(); j++)
+        if (kPkKinds[field[j]] == kSelEvals8 && h[j].nz && f[field[j] - 1]) sel.push_back({f[field[j] - 1], 4 * D});
+    std::vector<SegHash> hs = hash_segments(sel);
+    std::array<uint64_t, 2> r = {mix64(0xABCDEFULL, D), mix64(0xFEDCBAULL, D)};
+    for (size_t j = 0; j < h.size(); j++) {
+        r[0] = mix64(mix64(r[0], field[j]), h[j].h0);
+        r[1] = mix64(mix64(r[1], field[j]), h[j].h1);
+    }
+    for (const SegHash &x : hs) r[0] = mix64(r[0], x.h0), r[1] = mix64(r[1], x.h1);
+    return r;
+}
+std::array<uint64_t, 2> ck_content_hash(const CommitKeyC &ck, uint64_t D) {
+    std::vector<SegHash> h = hash_segments({{ck.powers_of_g, 12 * D}});
+    return {mix64(0x13579BULL ^ D, h[0].h0), mix64(0x2468ACULL ^ D, h[0].h1)};
+}
+
 uint64_t ck_fingerprint(const CommitKeyC &ck, uint64_t D) {
     uint64_t h = mix64(mix64(0x7654321ULL, D), reinterpret_cast<uintptr_t>(ck.powers_of_g));
     return ck.powers_of_g ? sample_words(h, ck.powers_of_g, 12 * D) : h;
@@ -1076,12 +1183,12 @@ extern "C" {
 ProofC gen_proof(CircuitC circuit, ProverKeyC pk, CommitKeyC ck) {
     static pnp_ctx *ctx = nullptr;
     static bool have_pk = false, have_ck = false;
-    static uint64_t fp_pk = 0, fp_ck = 0;
+    static std::array<uint64_t, 2> h_pk{}, h_ck{};
     auto env_on = [](const char *name) {  // read per call: a caller may switch modes
         const char *e = getenv(name);
         return e && atoi(e) != 0;
     };
-    const bool reuse = env_on("PNP_V1_REUSE"), strict = env_on("PNP_V1_STRICT");
+    const bool reuse = env_on("PNP_V1_REUSE"), reload = env_on("PNP_V1_RELOAD"), strict = env_on("PNP_V1_STRICT");
     ProofC out;
     memset(&out, 0, sizeof out);
     auto die = [](int rc) {
@@ -1094,8 +1201,17 @@ ProofC gen_proof(CircuitC circuit, ProverKeyC pk, CommitKeyC ck) {
     uint64_t D = 1;
     while (D < bound) D <<= 1;
     if (!ck.powers_of_g) die(PNP_E_ARG);
-    const uint64_t fpk = reuse ? pk_fingerprint(pk, D) : 0, fck = reuse ? ck_fingerprint(ck, D) : 0;
-    if (!reuse || !have_pk || fpk != fp_pk || !ctx->pk_loaded) {
+    // what identifies "the same key": the full-content hash (default), the
+    // sampled fingerprint (PNP_V1_REUSE), nothing (PNP_V1_RELOAD: upload always)
+    std::array<uint64_t, 2> hp{}, hc{};
+    if (reuse) {
+        hp = {pk_fingerprint(pk, D), D};
+        hc = {ck_fingerprint(ck, D), D};
+    } else if (!reload) {
+        hp = pk_content_hash(pk, D);
+        hc = ck_content_hash(ck, D);
+    }
+    if (reload || !have_pk || hp != h_pk || !ctx->pk_loaded || ctx->pk_n != D) {
         have_pk = false;
         if ((rc = pnp_load_prover_key(ctx, &pk, D, 0)) != PNP_OK) die(rc);
         if (strict && (!ctx->pk_qm_zero || !ctx->pk_qlookup_zero || ctx->pk_custom_nz[0] ||
@@ -1106,13 +1222,13 @@ ProofC gen_proof(CircuitC circuit, ProverKeyC pk, CommitKeyC ck) {
             die(PNP_E_ENVELOPE);
         }
         have_pk = true;
-        fp_pk = fpk;
+        h_pk = hp;
     }
-    if (!reuse || !have_ck || fck != fp_ck || !ctx->ck_loaded) {
+    if (reload || !have_ck || hc != h_ck || !ctx->ck_loaded || ctx->ck_points != D) {
         have_ck = false;
         if ((rc = pnp_load_commit_key(ctx, &ck, D, 0)) != PNP_OK) die(rc);
         have_ck = true;
-        fp_ck = fck;
+        h_ck = hc;
     }
     if ((rc = pnp_prove(ctx, &circuit, 0, &out)) != PNP_OK) die(rc);
     return out;
