@@ -482,10 +482,12 @@ def main():
     # MSM sharding: bucket ranges (default) or point ranges (PNP_MSM_SHARD=points)
     from pnp.shard import v_bytes_for
     vb = (lambda w: 0) if os.environ.get("PNP_MSM_SHARD") == "points" else (lambda w: v_bytes_for(args.lg, w))
+    ex = None
     if world > 1:  # sharded MSMs + distributed round 4, exchanges over RCCL
         from pnp.shard import WindowExchange, a2a_bytes_for
-        ctx.set_msm_shard(WindowExchange(rank, world, device=torch.device("cuda", local),
-                                         a2a_bytes=a2a_bytes_for(args.lg, world), v_bytes=vb(world)))
+        ex = WindowExchange(rank, world, device=torch.device("cuda", local),
+                            a2a_bytes=a2a_bytes_for(args.lg, world), v_bytes=vb(world))
+        ctx.set_msm_shard(ex)
     elif args.solo:
         from pnp.shard import SoloExchange, a2a_bytes_for
         sr, sw = (int(v) for v in args.solo.split("/"))
@@ -635,6 +637,11 @@ def main():
                                       "launch_ms": round(q_ms / max(q_n, 1), 3)}},
             "stages_ms": {k: round(v, 2) for k, v in stages},
         }
+        if ex is not None:
+            k = args.steps + args.warmup
+            out["exchange"] = {"backend": ex.backend, "stream_ordered": ex.ordered,
+                               "callbacks_per_proof": (ex.calls + ex.a2a_calls + getattr(ex, "v_calls", 0)) / k,
+                               "callback_ms_per_proof": round(1e3 * ex.cb_seconds / k, 3)}
         if solo:
             out["solo"] = {"rank": solo.rank, "world": solo.world,
                            "allgathers_per_proof": solo.calls / (args.steps + args.warmup),
@@ -643,8 +650,11 @@ def main():
                            "alltoall_bytes_sent_per_proof": solo.a2a_bytes_moved / (args.steps + args.warmup),
                            "bucket_alltoallvs_per_proof": solo.v_calls / (args.steps + args.warmup),
                            "bucket_bytes_sent_per_proof": solo.v_bytes_moved / (args.steps + args.warmup),
+                           "callbacks_per_proof": (solo.calls + solo.a2a_calls + solo.v_calls) / (args.steps + args.warmup),
+                           "callback_ms_per_proof": round(1e3 * solo.cb_seconds / (args.steps + args.warmup), 3),
                            "note": "per-rank work of a W-GPU proof; the collectives are loopbacks "
-                                   "(their xGMI time is not included)"}
+                                   "(their xGMI time is not included; callback_ms is the host time "
+                                   "spent inside the loopback callbacks)"}
         if not args.no_verify:
             chk = check_proof(syn, proof, args.circuit)
             out["verified"] = chk.pop("verified") and all_equal

@@ -51,6 +51,23 @@ import ctypes
 arr = (ctypes.c_uint64 * 1)(7777 * 8)
 assert cbv(None, arr, arr) == 0 and ex.error is None
 assert (ex.calls, ex.a2a_calls, ex.v_calls) == (2, 2, 2)
+# stream-ordered: the collectives enqueued on another stream (the library's,
+# pnp.Context.set_msm_shard), no host synchronisation; the results appear once
+# that stream is synchronised
+side = torch.cuda.Stream()
+ex.stream = torch.cuda.ExternalStream(side.cuda_stream)
+assert ex.ordered
+with torch.cuda.stream(side):
+    ex.buf[:24].copy_(torch.arange(24, dtype=torch.int64, device=dev) - 5)
+    ex.a2a[:4096].copy_(torch.arange(4096, dtype=torch.int64, device=dev) * 3)
+ex.gather(24 * 8)
+ex.alltoall(4096 * 8)
+ex.alltoallv([1000 * 8], [1000 * 8])
+side.synchronize()
+assert torch.equal(ex.buf[:24].cpu(), torch.arange(24, dtype=torch.int64) - 5)
+assert torch.equal(ex.a2a[4096:].cpu(), torch.arange(4096, dtype=torch.int64) * 3)
+assert torch.equal(ex.vrecv[:1000], ex.vsend[:1000])
+assert (ex.calls, ex.a2a_calls, ex.v_calls) == (3, 3, 3)
 # the bench's max-over-ranks timing
 t = torch.tensor([1.25], dtype=torch.float64, device=dev)
 dist.all_reduce(t, op=dist.ReduceOp.MAX)

@@ -208,11 +208,19 @@ class Context:
         """Window-sharded MSM across ranks (pnp_set_msm_shard); `exchange` is a
         pnp.shard.WindowExchange, or None to go back to single-GPU MSMs."""
         if exchange is None or exchange.world == 1:
+            check(self.lib.pnp_set_exchange_ordered(self.h, 0), "pnp_set_exchange_ordered")
             check(self.lib.pnp_set_msm_shard(self.h, 0, 1, ALLGATHER_FN(), None, None, 0),
                   "pnp_set_msm_shard")
             check(self.lib.pnp_set_exchange_v(self.h, ALLTOALLV_FN(), None, None, None, 0), "pnp_set_exchange_v")
             self._exchange = None
             return
+        # RCCL exchanges run on the library's stream, without host syncs
+        import torch
+        sp = C.c_void_p()
+        check(self.lib.pnp_ctx_stream(self.h, C.byref(sp)), "pnp_ctx_stream")
+        if exchange.buf.is_cuda and sp.value:
+            exchange.stream = torch.cuda.ExternalStream(sp.value, device=exchange.buf.device)
+        check(self.lib.pnp_set_exchange_ordered(self.h, int(exchange.ordered)), "pnp_set_exchange_ordered")
         cb = exchange.c_callback()
         check(self.lib.pnp_set_msm_shard(self.h, exchange.rank, exchange.world, cb, None,
                                          exchange.buf.data_ptr(), exchange.buf.numel() * 8),

@@ -43,6 +43,23 @@ class WindowExchange:
         self.calls = 0
         self.a2a_calls = 0
         self.error = None
+        # the library's stream (pnp.Context.set_msm_shard sets it): RCCL
+        # collectives are enqueued behind the library's work on that stream and
+        # the library's next work behind them — no host synchronisation
+        # (pnp_set_exchange_ordered); PNP_EXCHANGE_SYNC=1 keeps the host syncs
+        self.stream = None
+        self.cb_seconds = 0.0
+
+    @property
+    def ordered(self) -> bool:
+        import os
+        return (self.backend == "nccl" and self.buf.is_cuda and self.stream is not None
+                and os.environ.get("PNP_EXCHANGE_SYNC") != "1")
+
+    def _on_stream(self):
+        import contextlib
+        import torch
+        return torch.cuda.stream(self.stream) if self.ordered else contextlib.nullcontext()
 
     def gather(self, bytes_per_rank: int) -> None:
         import torch
@@ -56,8 +73,10 @@ class WindowExchange:
             # RCCL all-gather; the input is a copy of this rank's slot (B x 192 B)
             # rather than a view into the output, so no overlap rule of the
             # torch / RCCL versions at hand can reject it
-            dist.all_gather_into_tensor(out, mine.clone(), group=self.group)
-            torch.cuda.current_stream().synchronize()
+            with self._on_stream():
+                dist.all_gather_into_tensor(out, mine.clone(), group=self.group)
+            if not self.ordered:
+                torch.cuda.current_stream().synchronize()
         else:
             host_mine = mine.cpu().clone()
             parts = [torch.empty_like(host_mine) for _ in range(self.world)]
@@ -76,8 +95,10 @@ class WindowExchange:
         send = self.a2a[: w * self.world]
         recv = self.a2a[w * self.world: 2 * w * self.world]
         if self.a2a.is_cuda and self.backend == "nccl":
-            dist.all_to_all_single(recv, send, group=self.group)
-            torch.cuda.current_stream().synchronize()
+            with self._on_stream():
+                dist.all_to_all_single(recv, send, group=self.group)
+            if not self.ordered:
+                torch.cuda.current_stream().synchronize()
         else:
             # through host memory, one exchange per peer pair (gloo)
             h_send = send.cpu().clone()
@@ -101,8 +122,10 @@ class WindowExchange:
         send = self.vsend[: sum(ss)]
         recv = self.vrecv[: sum(rs)]
         if self.vsend.is_cuda and self.backend == "nccl":
-            dist.all_to_all_single(recv, send, output_split_sizes=rs, input_split_sizes=ss, group=self.group)
-            torch.cuda.current_stream().synchronize()
+            with self._on_stream():
+                dist.all_to_all_single(recv, send, output_split_sizes=rs, input_split_sizes=ss, group=self.group)
+            if not self.ordered:
+                torch.cuda.current_stream().synchronize()
         else:
             h_recv = torch.empty(sum(rs), dtype=torch.int64)
             dist.all_to_all_single(h_recv, send.cpu(), output_split_sizes=rs, input_split_sizes=ss,
@@ -112,35 +135,32 @@ class WindowExchange:
                 torch.cuda.current_stream().synchronize()
         self.v_calls += 1
 
+    def _timed(self, fn, *a) -> int:
+        import time
+        t0 = time.perf_counter()
+        try:
+            fn(*a)
+            return 0
+        except Exception as e:  # never unwind through the C++ frames
+            self.error = e
+            return 1
+        finally:
+            self.cb_seconds += time.perf_counter() - t0
+
     def c_alltoallv(self):
         def cb(_user, send_bytes, recv_bytes):
-            try:
-                self.alltoallv([send_bytes[i] for i in range(self.world)],
+            return self._timed(self.alltoallv, [send_bytes[i] for i in range(self.world)],
                                [recv_bytes[i] for i in range(self.world)])
-                return 0
-            except Exception as e:
-                self.error = e
-                return 1
         return ALLTOALLV_FN(cb)
 
     def c_callback(self):
         def cb(_user, bytes_per_rank):
-            try:
-                self.gather(int(bytes_per_rank))
-                return 0
-            except Exception as e:  # never unwind through the C++ frames
-                self.error = e
-                return 1
+            return self._timed(self.gather, int(bytes_per_rank))
         return ALLGATHER_FN(cb)
 
     def c_alltoall(self):
         def cb(_user, bytes_per_peer):
-            try:
-                self.alltoall(int(bytes_per_peer))
-                return 0
-            except Exception as e:
-                self.error = e
-                return 1
+            return self._timed(self.alltoall, int(bytes_per_peer))
         return ALLTOALL_FN(cb)
 
 
@@ -162,6 +182,8 @@ class SoloExchange(WindowExchange):
         self.vrecv = torch.empty(v_bytes // 8, dtype=torch.int64, device=device) if v_bytes else None
         torch.cuda.synchronize()
         self.backend = "loopback"
+        self.stream = None
+        self.cb_seconds = 0.0
         self.calls = self.a2a_calls = self.v_calls = 0
         self.gather_bytes = self.a2a_bytes_moved = self.v_bytes_moved = 0
         self.error = None
