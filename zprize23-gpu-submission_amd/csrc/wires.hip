@@ -28,9 +28,9 @@
 //      representative row; run sums of the L_i (exact XYZZ additions, chunked
 //      so large groups — the zero variable's — stay parallel) -> affine bases;
 //   4. one folded table (msm_build_table) over the bases of all four wires,
-//      MSM b reading its wire's n-slot segment (MsmSegs); group k of g sits at
-//      slot floor(k n / g), so the groups spread over the whole segment and
-//      every rank of a sharded MSM gets its share of them.
+//      MSM b reading its wire's n-slot segment (MsmSegs); group k sits at
+//      slot bitrev(k) (wb_slot), so the groups spread over the whole segment
+//      and every rank of a sharded MSM gets its share of them.
 // A wire whose groups are nearly all single rows (g > 0.9 n, the Merkle
 // circuit's wire c) keeps the plain Lagrange points as its segment: its
 // scalars are its evaluations.
