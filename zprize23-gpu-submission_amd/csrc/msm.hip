@@ -46,9 +46,11 @@ namespace pnp {
 constexpr uint32_t KEY_ZERO = 0xFFFFFFFFu;
 // the W signed c-bit digits of scalar i as keys (magnitude - 1 | sign << 31,
 // KEY_ZERO for a zero digit), row w of keys at keys[w n + i]; fn(key) per digit
+// top_sh (folded tables, MsmCfg::top_sh): the top window's digit d becomes
+// magnitude d 2^top_sh (its table level is divided by 2^top_sh)
 template <class F>
 __device__ __forceinline__ void scalar_digits(const uint64_t *scalars, uint64_t i, uint64_t n, int c, int W,
-                                              uint32_t *keys, F fn) {
+                                              int top_sh, uint32_t *keys, F fn) {
     Fr s = from_mont(load_fr(scalars, i));
     const uint32_t NB = 1u << (c - 1);
     uint32_t carry = 0;
@@ -72,17 +74,17 @@ __device__ __forceinline__ void scalar_digits(const uint64_t *scalars, uint64_t 
             if (mag) key = (mag - 1) | 0x80000000u;
         } else {
             carry = 0;
-            if (raw) key = raw - 1;
+            if (raw) key = (w == W - 1 ? raw << top_sh : raw) - 1;
         }
         // the top window never carries: W c >= 255 + 1 for the configured c (scalars < 2^255)
         keys[(uint64_t)w * n + i] = key;
         fn(key);
     }
 }
-__global__ void k_digits(const uint64_t *scalars, uint64_t n, int c, int W, uint32_t *keys) {
+__global__ void k_digits(const uint64_t *scalars, uint64_t n, int c, int W, int top_sh, uint32_t *keys) {
     uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
     if (i >= n) return;
-    scalar_digits(scalars, i, n, c, W, keys, [](uint32_t) {});
+    scalar_digits(scalars, i, n, c, W, top_sh, keys, [](uint32_t) {});
 }
 
 // Virtual window v reads `rows` key rows starting at row v*vstride + off of
@@ -168,7 +170,8 @@ struct ScalarPtrs {
     static constexpr int MAX = MSM_BATCH_MAX;
     const uint64_t *p[MAX];
 };
-__global__ __launch_bounds__(1024) void k_digits_hist(ScalarPtrs sp, uint64_t n, int c, int W, int fb, int NBc,
+__global__ __launch_bounds__(1024) void k_digits_hist(ScalarPtrs sp, uint64_t n, int c, int W, int top_sh, int fb,
+                                                      int NBc,
                                                       uint64_t chunk, int nch, uint32_t *keys, uint32_t *counts,
                                                       int wmaj = 1) {
     __shared__ uint32_t hist[1 << SORT_CB];
@@ -178,7 +181,7 @@ __global__ __launch_bounds__(1024) void k_digits_hist(ScalarPtrs sp, uint64_t n,
     const uint64_t lo = (uint64_t)ch * chunk, hi = lo + chunk < n ? lo + chunk : n;
     uint32_t *kv = keys + (uint64_t)v * W * n;
     for (uint64_t i = lo + threadIdx.x; i < hi; i += blockDim.x)
-        scalar_digits(sp.p[v], i, n, c, W, kv, [&](uint32_t key) {
+        scalar_digits(sp.p[v], i, n, c, W, top_sh, kv, [&](uint32_t key) {
             if (key != KEY_ZERO) atomicAdd(&hist[(key & 0x7FFFFFFFu) >> fb], 1u);
         });
     __syncthreads();
@@ -874,7 +877,10 @@ void msm_build_table(DevBuf &tab, const uint64_t *d_points, uint64_t n, int c, h
         const uint64_t lanes = (n + CH - 1) / CH;
         const uint64_t *src = d_points;
         for (int k = 1; k < g.W; k++) {
-            hipLaunchKernelGGL(k_table_dbl, nb, dim3(256), 0, s, src, n, g.c, xyzz.u64());
+            // level k = 2^c level k-1; the top level 2^(c - top_sh) level W-2
+            // (its digits are scaled by 2^top_sh, MsmCfg::top_sh)
+            const int dbls = k == g.W - 1 ? g.c - g.top_sh : g.c;
+            hipLaunchKernelGGL(k_table_dbl, nb, dim3(256), 0, s, src, n, dbls, xyzz.u64());
             PNP_HIP(hipGetLastError());
             hipLaunchKernelGGL(k_table_affine, dim3((uint32_t)((lanes + 255) / 256)), dim3(256), 0, s,
                                xyzz.u64(), n, CH, pre.u64(), nxt.u64());
@@ -953,7 +959,7 @@ static void sort_group(MsmWork &wk, MsmGroup &gb, const uint32_t *keys, const Gr
     if (scalars) {
         ScalarPtrs sp{};
         for (int v = 0; v < nv; v++) sp.p[v] = scalars[v];
-        hipLaunchKernelGGL(k_digits_hist, grid, dim3(1024), 0, s, sp, n, g.c, g.W, fb, NBc, chunk, nch,
+        hipLaunchKernelGGL(k_digits_hist, grid, dim3(1024), 0, s, sp, n, g.c, g.W, g.top_sh, fb, NBc, chunk, nch,
                            const_cast<uint32_t *>(keys), counts, 1);
     } else {
         hipLaunchKernelGGL(k_coarse_hist, grid, dim3(1024), 0, s, keys, gp.kr, fb, NBc, chunk, nch, counts);
@@ -1155,7 +1161,7 @@ static void msm_local_batch(MsmWork &wk, const uint64_t *d_points, const uint64_
     if (!fuse) {
         for (int b = 0; b < B; b++) {
             hipLaunchKernelGGL(k_digits, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, s, d_scalars[b], n,
-                               g.c, g.W, keys + (uint64_t)b * g.W * n);
+                               g.c, g.W, g.top_sh, keys + (uint64_t)b * g.W * n);
             PNP_HIP(hipGetLastError());
         }
     }
@@ -1364,7 +1370,7 @@ static bool msm_bucket_batch(MsmWork &wk, const uint64_t *const *sc, int B, uint
     const bool fuse = B <= ScalarPtrs::MAX;  // digits made by the histogram pass
     for (int b = 0; b < B && n && !fuse; b++) {
         hipLaunchKernelGGL(k_digits, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, s, sc[b], n, g.c, g.W,
-                           keys + (uint64_t)b * g.W * n);
+                           g.top_sh, keys + (uint64_t)b * g.W * n);
         PNP_HIP(hipGetLastError());
     }
     // 2. pass A, destination-major (chunks as sort_group: ~512 workgroups)
@@ -1385,8 +1391,8 @@ static bool msm_bucket_batch(MsmWork &wk, const uint64_t *const *sc, int B, uint
     if (n && fuse) {
         ScalarPtrs sp{};
         for (int b = 0; b < B; b++) sp.p[b] = sc[b];
-        hipLaunchKernelGGL(k_digits_hist, grid, dim3(1024), 0, s, sp, n, g.c, g.W, fb, NBc, chunk, nch, keys, counts,
-                           W);
+        hipLaunchKernelGGL(k_digits_hist, grid, dim3(1024), 0, s, sp, n, g.c, g.W, g.top_sh, fb, NBc, chunk, nch, keys,
+                           counts, W);
         PNP_HIP(hipGetLastError());
     } else if (n) {
         hipLaunchKernelGGL(k_coarse_hist, grid, dim3(1024), 0, s, keys, kr, fb, NBc, chunk, nch, counts, W);

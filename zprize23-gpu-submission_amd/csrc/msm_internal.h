@@ -9,6 +9,14 @@ namespace pnp {
 // NB = 2^(c-1) buckets per window.
 struct MsmCfg {
     int c, W, NB;
+    // folded tables: the top window's digit d is taken as bucket d 2^top_sh
+    // against table level W-1 = 2^(c (W-1) - top_sh) P (msm_build_table).  A
+    // scalar < 2^255 leaves only 255 - c (W-1) bits (+ a carry) for the top
+    // window (15 of c = 20): unscaled, its entries — one per point and MSM —
+    // would all land in the lowest 2^15 of the 2^19 buckets, 2.3x their share,
+    // and in a bucket-range sharded MSM on rank 0 alone (1.67x the entries of
+    // the other ranks at 8 GPUs); scaled they spread over every bucket range
+    int top_sh;
 };
 
 // c = 0: the default for n; W c >= 256 so the top window of a scalar < 2^255
@@ -29,6 +37,8 @@ inline MsmCfg msm_cfg(uint64_t n, int c = 0, bool folded = false) {
     if (c > 0) g.c = c;
     g.W = (256 + g.c - 1) / g.c;
     g.NB = 1 << (g.c - 1);
+    const int top_bits = 255 - g.c * (g.W - 1);  // top raw value <= 2^top_bits (carry included)
+    g.top_sh = folded && top_bits >= 0 && g.c - 1 - top_bits > 0 ? g.c - 1 - top_bits : 0;
     return g;
 }
 
