@@ -107,3 +107,37 @@ def test_budget_refuses_a_key_that_cannot_prove(monkeypatch):
         ctx.prove(syn.cs, device_ptrs=True)
     finally:
         ctx.close()
+
+
+def test_device_srs_reload_keeps_derived_tables():
+    """reloading the SAME device-resident SRS (same address, size
+    and bytes) keeps the tables derived from it (folded tables, Lagrange
+    basis, copy groups); a changed point drops them (their plan parts are
+    positive again)."""
+    import torch
+    import pnp
+    from pnp import abi
+    ctx = pnp.Context(0)
+    try:
+        syn = _instance(ctx, 14)
+        _load(ctx, syn)
+        ref = abi.proof_to_bytes(ctx.prove(syn.cs, device_ptrs=True))
+        u = ctx.hbm_usage()
+        assert u["lagrange"] == 0 and u["groups"] == 0, u
+        ctx.load_commit_key(syn.ck, syn.n, device_ptrs=True)  # same bytes
+        u = ctx.hbm_usage()
+        assert u["lagrange"] == 0 and u["groups"] == 0, u
+        assert abi.proof_to_bytes(ctx.prove(syn.cs, device_ptrs=True)) == ref
+        srs = syn.keep["srs"]
+        saved = srs[5].clone()
+        srs[5] = srs[6]
+        torch.cuda.synchronize()
+        ctx.load_commit_key(syn.ck, syn.n, device_ptrs=True)  # one point changed
+        u = ctx.hbm_usage()
+        assert u["lagrange"] > 0, u
+        srs[5] = saved
+        torch.cuda.synchronize()
+        ctx.load_commit_key(syn.ck, syn.n, device_ptrs=True)
+        assert abi.proof_to_bytes(ctx.prove(syn.cs, device_ptrs=True)) == ref
+    finally:
+        ctx.close()

@@ -918,12 +918,22 @@ int pnp_load_commit_key(pnp_ctx *ctx, const CommitKeyC *ck, uint64_t n_points, i
         PNP_HIP(hipSetDevice(ctx->device));
         ctx->ck_loaded = false;
         if (device_ptrs) {
+            // the tables derived from the SRS survive a reload of the same
+            // bytes (same address, size and content hash)
+            uint64_t h[2];
+            pnp::k_hash_words(ck->powers_of_g, 12 * n_points, ctx->scratch_b, ctx->stream, h);
+            const bool same = ctx->ck_hash_valid && !ctx->ck_owned.p && ctx->ck_dev == ck->powers_of_g &&
+                              ctx->ck_points == n_points && h[0] == ctx->ck_hash[0] && h[1] == ctx->ck_hash[1];
             ctx->ck_owned.release();
             ctx->ck_dev = ck->powers_of_g;
             ctx->ck_points = n_points;
-            pnp::ck_derived_reset(ctx);
+            if (!same) pnp::ck_derived_reset(ctx);
+            ctx->ck_hash[0] = h[0];
+            ctx->ck_hash[1] = h[1];
+            ctx->ck_hash_valid = true;
             ctx->ck_loaded = true;
         } else {
+            ctx->ck_hash_valid = false;
             // upload (as the reference does per call, load.cu:348-358)
             pnp::DevBuf up(n_points * 96);
             PNP_HIP(hipMemcpyAsync(up.p, ck->powers_of_g, n_points * 96, hipMemcpyHostToDevice, ctx->stream));

@@ -55,6 +55,11 @@ struct pnp_ctx {
     uint64_t ck_points = 0;
     pnp::DevBuf ck_owned;
     const uint64_t *ck_dev = nullptr;
+    // device-pointer loads: the content hash of the SRS the derived tables
+    // (folded tables, Lagrange basis, groups) were built from — a reload of
+    // the same bytes keeps them
+    uint64_t ck_hash[2] = {0, 0};
+    bool ck_hash_valid = false;
     // folded MSM table of the first ck_table_n SRS points (msm_build_table),
     // built on the first commitment of that size
     pnp::DevBuf ck_table;

@@ -94,6 +94,8 @@ void k_any_nonzero_n(const uint64_t *v, uint64_t words, uint64_t stride, int cnt
                      hipStream_t s);
 // any word of a differs from b
 bool k_any_diff(const uint64_t *a, const uint64_t *b, uint64_t words, DevBuf &scratch, hipStream_t s);
+// 128-bit content hash of `words` u64 in HBM (synchronous)
+void k_hash_words(const uint64_t *a, uint64_t words, DevBuf &scratch, hipStream_t s, uint64_t out[2]);
 // strided affine points (x / y: 6 u64 each at x_off / y_off, an infinity byte
 // at inf_off, `stride` bytes per point) -> packed 12-u64 points; false when a
 // point is flagged infinity (synchronous)

@@ -199,6 +199,47 @@ bool k_any_diff(const uint64_t *a, const uint64_t *b, uint64_t words, DevBuf &sc
     return h != 0;
 }
 
+// 128-bit content hash of `words` u64 on the device: two position-keyed sums
+// of multiply-folded words (any changed word changes both with overwhelming
+// probability); one launch, one host synchronisation
+__device__ __forceinline__ uint64_t dmum(uint64_t a, uint64_t b) {
+    return a * b ^ __umul64hi(a, b);
+}
+__global__ void k_hash_words_(const uint64_t *a, uint64_t words, unsigned long long *out) {
+    uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    uint64_t h0 = 0, h1 = 0;
+    for (; i < words; i += stride) {
+        const uint64_t v = a[i];
+        h0 += dmum(v ^ 0xa0761d6478bd642fULL, (2 * i + 1) * 0xe7037ed1a0b428dbULL);
+        h1 += dmum(v ^ 0x8ebc6af09c88c6e3ULL, (2 * i + 1) * 0x589965cc75374cc3ULL);
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+        h0 += __shfl_xor(h0, off, 64);
+        h1 += __shfl_xor(h1, off, 64);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        atomicAdd(out, (unsigned long long)h0);
+        atomicAdd(out + 1, (unsigned long long)h1);
+    }
+}
+void k_hash_words(const uint64_t *a, uint64_t words, DevBuf &scratch, hipStream_t s, uint64_t out[2]) {
+    if (scratch.bytes < 16) scratch.alloc(16);
+    unsigned long long *d = static_cast<unsigned long long *>(scratch.p);
+    PNP_HIP(hipMemsetAsync(d, 0, 16, s));
+    if (words) {
+        uint64_t blocks = (words + 255) / 256;
+        if (blocks > 4096) blocks = 4096;
+        hipLaunchKernelGGL(k_hash_words_, dim3((uint32_t)blocks), dim3(256), 0, s, a, words, d);
+        PNP_HIP(hipGetLastError());
+    }
+    unsigned long long h[2];
+    PNP_HIP(hipMemcpyAsync(h, d, 16, hipMemcpyDeviceToHost, s));
+    PNP_HIP(hipStreamSynchronize(s));
+    out[0] = h[0] ^ words;
+    out[1] = h[1];
+}
+
 // Strided affine points (arkworks' in-memory G1Affine: x, y Montgomery Fp384
 // limbs, an infinity bool, padding; layout given by offsets) -> packed
 // {x[6], y[6]}; *bad = 1 when a point is flagged infinity.
