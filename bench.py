@@ -639,7 +639,10 @@ def main():
         }
         if ex is not None:
             k = args.steps + args.warmup
+            sent = getattr(ex, "v_sent_to", None)
             out["exchange"] = {"backend": ex.backend, "stream_ordered": ex.ordered,
+                               "bucket_range_balance": (round(max(sent) * len(sent) / max(sum(sent), 1), 4)
+                                                        if sent else None),
                                "callbacks_per_proof": (ex.calls + ex.a2a_calls + getattr(ex, "v_calls", 0)) / k,
                                "callback_ms_per_proof": round(1e3 * ex.cb_seconds / k, 3)}
         if solo:
@@ -651,6 +654,12 @@ def main():
                            "bucket_alltoallvs_per_proof": solo.v_calls / (args.steps + args.warmup),
                            "bucket_bytes_sent_per_proof": solo.v_bytes_moved / (args.steps + args.warmup),
                            "callbacks_per_proof": (solo.calls + solo.a2a_calls + solo.v_calls) / (args.steps + args.warmup),
+                           # records this rank's points send to each bucket range: max / mean
+                           # (1 = every range gets its share; the unscaled top window gave
+                           # range 0 ~1.67x at 8 ranks)
+                           "bucket_range_balance": (round(max(solo.v_sent_to) * len(solo.v_sent_to)
+                                                          / max(sum(solo.v_sent_to), 1), 4)
+                                                    if getattr(solo, "v_sent_to", None) else None),
                            "callback_ms_per_proof": round(1e3 * solo.cb_seconds / (args.steps + args.warmup), 3),
                            "note": "per-rank work of a W-GPU proof; the collectives are loopbacks "
                                    "(their xGMI time is not included; callback_ms is the host time "

@@ -112,11 +112,20 @@ class WindowExchange:
                 torch.cuda.current_stream().synchronize()
         self.a2a_calls += 1
 
+    def _count_dest(self, send_bytes):
+        """bytes this rank sent to each bucket range (the balance of the
+        bucket-range split: bench.py reports max / mean)"""
+        if not hasattr(self, "v_sent_to") or len(self.v_sent_to) != self.world:
+            self.v_sent_to = [0] * self.world
+        for d in range(self.world):
+            self.v_sent_to[d] += int(send_bytes[d])
+
     def alltoallv(self, send_bytes, recv_bytes) -> None:
         """Segment s of `vsend` (send_bytes[s] bytes, back to back) goes to rank
         s; what rank s sent lands at sum(recv_bytes[:s]) of `vrecv`."""
         import torch
         import torch.distributed as dist
+        self._count_dest(send_bytes)
         ss = [int(b) // 8 for b in send_bytes]
         rs = [int(b) // 8 for b in recv_bytes]
         send = self.vsend[: sum(ss)]
@@ -239,6 +248,7 @@ class SoloExchange(WindowExchange):
         exchange above made the sizes agree): distinct entries of this rank's
         points, bucket indices within a range, as many as a real rank gets."""
         import torch
+        self._count_dest(send_bytes)
         ss = [int(b) // 8 for b in send_bytes]
         rs = [int(b) // 8 for b in recv_bytes]
         assert rs == ss, (rs, ss)
