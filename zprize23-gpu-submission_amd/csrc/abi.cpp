@@ -173,21 +173,31 @@ HbmPlan hbm_plan(pnp_ctx *ctx, uint64_t n) {
     const bool dist = ctx->pk_nb < 8;
     const uint64_t len = dist ? per : n, NB = (uint64_t)ctx->pk_nb * n, N8 = 8 * n;
     const bool lookups = !ctx->pk_qlookup_zero;
-    // per-proof buffers (prover.cpp ctx->buf), the division / scan scratch and
-    // the PI term's 1 / (x - w^pos)
-    const uint64_t work = 32 * (25 * n + 11 * len + NB * (7 + (lookups ? 5 : 0) + (ctx->pk_std_coset ? 1 : 3))) +
-                          32 * 4 * std::max(n, NB);
+    // per-proof buffers (prover.cpp ctx->buf): 21 of n always (wires, their
+    // coefficients, the lookup / grand-product vectors), the PI and L1
+    // polynomials when not in closed form; 11 of the coefficient range (t
+    // chunks, linearisation, opening combinations); of the rank's blocks: the
+    // wire / z / z2 LDEs and t (7), the PI term's 1 / (x - w^pos), the lookup
+    // LDEs, the L1 / PI LDEs when not in closed form; the batch-inverse /
+    // scan scratch (about one vector of the longest length)
+    const bool closed = ctx->pk_std_coset;
+    const uint64_t work = 32 * (21 * n + (closed ? 0 : 2 * n) + 11 * len +
+                                NB * (8 + (lookups ? 4 : 0) + (closed ? 0 : 2)) + std::max(n, NB) * 9 / 8);
     const uint64_t work_held = map_bytes(ctx->work) + ctx->scratch_a.bytes + ctx->scratch_b.bytes + ctx->pk_pinv.bytes;
-    // NTT tables: twiddles of n and 8n (both directions, 2^256 and 2^261
-    // forms), the block twists (forward, inverse, x32, 2^261 forms)
-    const uint64_t ntt = 32 * 2 * (n + N8) + 36 * 2 * (n + N8) + 32 * 4 * N8 + 36 * 2 * N8;
-    const uint64_t ntt_held = map_bytes(ctx->ntt.fwd) + map_bytes(ctx->ntt.inv) + map_bytes(ctx->ntt.lde_twist) +
-                              map_bytes(ctx->ntt.blk_twist) + map_bytes(ctx->ntt.blk_twist_inv) +
-                              map_bytes(ctx->ntt.fwd29) + map_bytes(ctx->ntt.inv29) +
-                              map_bytes(ctx->ntt.blk_twist29) + map_bytes(ctx->ntt.blk_twist_inv29) +
-                              map_bytes(ctx->ntt.blk_twist32);
+    // NTT tables: twiddles of n (both directions), the block twists (forward,
+    // inverse, x32) of the 8n coset; with PNP_NTT29 their 2^261 forms
+    static const bool ntt29 = [] {
+        const char *e = getenv("PNP_NTT29");
+        return e && atoi(e) != 0;
+    }();
+    const uint64_t ntt = 32 * n + 3 * 32 * N8 + (ntt29 ? 36 * n / 2 * 2 + 2 * 36 * N8 : 0);
+    // (the 8n LDE twist of pnp_coset_lde8 is not a proof's: not counted as held)
+    const uint64_t ntt_held = map_bytes(ctx->ntt.fwd) + map_bytes(ctx->ntt.inv) + map_bytes(ctx->ntt.blk_twist) +
+                              map_bytes(ctx->ntt.blk_twist_inv) + map_bytes(ctx->ntt.fwd29) +
+                              map_bytes(ctx->ntt.inv29) + map_bytes(ctx->ntt.blk_twist29) +
+                              map_bytes(ctx->ntt.blk_twist_inv29) + map_bytes(ctx->ntt.blk_twist32);
     const uint64_t ck_tab = msm_table_bytes(n_tab, n, wk.fold_c);
-    const uint64_t msm = msm_work_bytes(per, n, wk.fold_c, 9, wk.v_bytes);
+    const uint64_t msm = msm_work_bytes(per, n, wk.fold_c, 9, wk.v_bytes, world);
     const uint64_t held = work_held + ntt_held + ctx->ck_table.bytes + msm_work_held(wk);
     const uint64_t total = work + ntt + ck_tab + msm;
     p.mandatory = total > held ? total - held : 0;

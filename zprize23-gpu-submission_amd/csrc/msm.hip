@@ -1532,21 +1532,22 @@ uint64_t msm_table_bytes(uint64_t n_points, uint64_t n_cfg, int fold_c) {
 }
 uint64_t msm_table_build_bytes(uint64_t n_points) { return n_points * (96 + 96 + 192 + 48); }
 // a batch of B folded MSMs over n_pts points of a table configured for n_cfg;
-// v_bytes: the bucket-range record capacity (0: point ranges / one GPU)
-uint64_t msm_work_bytes(uint64_t n_pts, uint64_t n_cfg, int fold_c, int B, uint64_t v_bytes) {
+// world > 1 with v_bytes > 0: bucket ranges (1/world of the buckets, at most
+// v_bytes / 8 received records accumulated), else point ranges / one GPU
+uint64_t msm_work_bytes(uint64_t n_pts, uint64_t n_cfg, int fold_c, int B, uint64_t v_bytes, int world) {
     const MsmCfg g = msm_cfg(n_cfg, fold_c, true);
-    const uint64_t WB = (uint64_t)B * g.NB;
-    uint64_t nent = (uint64_t)B * g.W * n_pts;  // the dense bound the buffers are sized for
-    const uint64_t digits = nent * 4;
-    uint64_t sort = nent * (4 + 2 + 4) + (uint64_t)B * 512 * 1024 * 4 + (WB + 1) * 4;
-    if (v_bytes) {  // bucket ranges: the received records are sorted and accumulated
-        nent = std::max<uint64_t>(nent, v_bytes / 8);
-        sort += nent * 4;
-    }
-    const uint64_t S = std::max<uint32_t>(16, acc_segment(nent, true));
-    const uint64_t nthr = (nent + S - 1) / S;
+    const bool buckets = world > 1 && v_bytes > 0;
+    const uint64_t WB = (uint64_t)B * (buckets ? g.NB / world : g.NB);
+    const uint64_t nent = (uint64_t)B * g.W * n_pts;  // the dense bound the buffers are sized for
+    const uint64_t digits = nent * 4, counts = (uint64_t)B * 512 * 1024 * 4 + (WB + 1) * 4;
+    // point ranges: pass-A entries + fine keys + sorted entries; bucket
+    // ranges: the received records sorted into `sorted`
+    const uint64_t acc_ent = buckets ? v_bytes / 8 : nent;
+    const uint64_t sort = buckets ? acc_ent * 4 : nent * (4 + 2 + 4);
+    const uint64_t S = std::max<uint32_t>(16, acc_segment(acc_ent, true));
+    const uint64_t nthr = (acc_ent + S - 1) / S;
     const uint64_t acc = (WB + 2 * nthr) * 224 + nthr * 12 + (WB + 1) * 4 + (WB * 24 + WB * 72 + 64) * 8;
-    return digits + sort + acc;
+    return digits + counts + sort + acc;
 }
 uint64_t msm_work_held(const MsmWork &wk) {
     uint64_t b = wk.digits.bytes + wk.part_counts.bytes + wk.rec_counts.bytes;

@@ -206,7 +206,7 @@ void msm_run_batch(MsmWork &w, const uint64_t *d_points, const uint64_t *const *
 // work buffers of a B-MSM batch over n_pts points, and what wk holds now
 uint64_t msm_table_bytes(uint64_t n_points, uint64_t n_cfg, int fold_c);
 uint64_t msm_table_build_bytes(uint64_t n_points);
-uint64_t msm_work_bytes(uint64_t n_pts, uint64_t n_cfg, int fold_c, int B, uint64_t v_bytes);
+uint64_t msm_work_bytes(uint64_t n_pts, uint64_t n_cfg, int fold_c, int B, uint64_t v_bytes, int world);
 uint64_t msm_work_held(const MsmWork &wk);
 // multi-GPU MSMs: the points [p0, p1) rank `rank` of `world` takes
 void msm_point_range(uint64_t n, int rank, int world, uint64_t &p0, uint64_t &p1);
