@@ -410,10 +410,11 @@ int pnp_commit_evals(pnp_ctx *ctx, const uint64_t *d_evals, uint64_t n, Commitme
  * to be allocated on this rank: out[2] mandatory (per-proof buffers, NTT
  * tables, the commit key's folded table, MSM work), out[3] the Lagrange-basis
  * key + table, out[4] the copy-constraint groups + table, out[5] the largest
- * build scratch.  pnp_load_prover_key fails with PNP_E_NOMEM (every rank of a
- * multi-GPU run, naming the short one) when out[2] + out[5] exceeds the rank's
- * share of its GPU's free HBM, and switches the optional tables off (same
- * proof bytes) when they do not fit. */
+ * build scratch.  The first pnp_prove after a key load checks them against
+ * the rank's share of its GPU's free HBM: it fails with PNP_E_NOMEM before any
+ * work (every rank of a multi-GPU run, naming the short one) when out[2] +
+ * out[5] does not fit, and switches the optional tables off (same proof bytes)
+ * when they do not. */
 int pnp_hbm_usage(pnp_ctx *ctx, uint64_t out[6]);
 
 /* Extension (operator form of gen_proof's copy-group commitments, wires.hip):

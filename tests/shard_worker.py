@@ -74,8 +74,9 @@ def main():
         with open(f"{out}.{rank}", "w") as f:
             f.write("ok")
     elif mode == "hbm":
-        # one rank short of HBM (PNP_TEST_SHORT_RANK): every rank's key load
-        # must fail with PNP_E_NOMEM naming that rank (abi.cpp hbm_budget)
+        # one rank short of HBM (PNP_TEST_SHORT_RANK): every rank's first
+        # proof must fail with PNP_E_NOMEM naming that rank, before any work
+        # (abi.cpp hbm_budget)
         short = int(os.environ["PNP_TEST_SHORT_RANK"])
         if rank == short:
             os.environ["PNP_HBM_LIMIT"] = "1"
@@ -88,9 +89,11 @@ def main():
         ex = WindowExchange(rank, world, device="cuda", a2a_bytes=a2a_bytes_for(lg, world),
                             v_bytes=_v_bytes(lg, world))
         ctx.set_msm_shard(ex)
+        ctx.load_prover_key(inp.pk, inp.n, device_ptrs=False)
+        ctx.load_commit_key(inp.ck, inp.n, device_ptrs=False)
         try:
-            ctx.load_prover_key(inp.pk, inp.n, device_ptrs=False)
-            msg = "loaded"
+            ctx.prove(inp.circuit, device_ptrs=False)
+            msg = "proved"
         except pnp.PnpError as e:
             msg = str(e)
         assert "PNP_E_NOMEM" in msg and f"rank {short} of {world}" in msg, msg

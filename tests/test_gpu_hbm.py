@@ -6,8 +6,9 @@
   * a budget without room for the optional tables (PNP_HBM_LIMIT) switches the
     copy-constraint groups / the Lagrange-basis key off and the proof bytes do
     not change;
-  * a budget without room for the proof fails the key load with PNP_E_NOMEM
-    and a message naming the bytes — on every rank of a multi-rank run, even
+  * a budget without room for the proof fails the first proof after the key
+    load with PNP_E_NOMEM and a message naming the bytes, before any work — on
+    every rank of a multi-rank run, even
     when only one rank is short (tests/test_shard.py
     test_hbm_short_rank_fails_every_load)."""
 import os
@@ -79,32 +80,29 @@ def test_budget_switches_optional_tables_off(monkeypatch):
             _load(ctx, syn)  # (plans with nothing built yet)
             u = ctx.hbm_usage()
             room = u["live"] + u["mandatory"] + u["transient"] + (u["lagrange"] if keep_lag else 0) + (1 << 20)
-            monkeypatch.setenv("PNP_HBM_LIMIT", str(room))
-            ctx.load_prover_key(syn.pk, syn.n, device_ptrs=True)
-            monkeypatch.delenv("PNP_HBM_LIMIT")
+            monkeypatch.setenv("PNP_HBM_LIMIT", str(room))  # read by the first proof's budget check
             ctx.kernel_timing(True)
             got = abi.proof_to_bytes(ctx.prove(syn.cs, device_ptrs=True))
             groups = ctx.kernel_bytes("wire_groups_used")
             ctx.kernel_timing(False)
+            monkeypatch.delenv("PNP_HBM_LIMIT")
             assert got == ref, keep_lag
             assert groups == 0, keep_lag
         finally:
             ctx.close()
 
 
-def test_budget_refuses_a_key_that_cannot_prove(monkeypatch):
+def test_budget_refuses_a_proof_that_cannot_fit(monkeypatch):
     import pnp
     ctx = pnp.Context(0)
     try:
         syn = _instance(ctx, 16)
+        _load(ctx, syn)
         monkeypatch.setenv("PNP_HBM_LIMIT", "1")
         with pytest.raises(pnp.PnpError, match="PNP_E_NOMEM.*HBM budget"):
-            ctx.load_prover_key(syn.pk, syn.n, device_ptrs=True)
-        monkeypatch.delenv("PNP_HBM_LIMIT")
-        with pytest.raises(pnp.PnpError, match="PNP_E_NOKEY"):
             ctx.prove(syn.cs, device_ptrs=True)
-        _load(ctx, syn)  # room again: loads and proves
-        ctx.prove(syn.cs, device_ptrs=True)
+        monkeypatch.delenv("PNP_HBM_LIMIT")
+        ctx.prove(syn.cs, device_ptrs=True)  # room again: the key is still loaded and proves
     finally:
         ctx.close()
 

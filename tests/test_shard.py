@@ -123,7 +123,7 @@ def test_sharded_full_size_matches_golden(tmp_path, golden, world, shard):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("world,shard", [(4, "buckets"), (8, "buckets"), (2, "points"), (4, "points")])
+@pytest.mark.parametrize("world,shard", [(4, "buckets"), (8, "buckets"), (2, "points")])
 def test_sharded_merkle_h13_groups_on(tmp_path, world, shard):
     """The production default at a size where every rank fits one shared GPU:
     the HEIGHT=13 Merkle circuit (n = 2^20, bench.Synthetic seed 1) with the
@@ -169,9 +169,9 @@ def test_sharded_merkle_circuit(tmp_path, world):
 @pytest.mark.parametrize("world", [2, 4])
 def test_hbm_short_rank_fails_every_load(tmp_path, world):
     """One rank whose HBM budget cannot hold a proof (PNP_HBM_LIMIT=1 on rank
-    world - 1): pnp_load_prover_key fails with PNP_E_NOMEM on EVERY rank, the
-    message naming the short rank — no rank runs into an exchange its peer
-    left (an 8-rank run that ran out of HBM surfaced as "count
+    world - 1): the first pnp_prove fails with PNP_E_NOMEM on EVERY rank
+    before any work, the message naming the short rank — no rank runs into an
+    exchange its peer left (an 8-rank run that ran out of HBM surfaced as "count
     all-gather failed" on the other ranks)."""
     prefix = str(tmp_path / "hbm")
     _launch(world, ["hbm", prefix, "10", "5"], tmp_path, 300, PNP_TEST_SHORT_RANK=str(world - 1))

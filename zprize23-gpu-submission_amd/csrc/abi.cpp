@@ -223,13 +223,15 @@ HbmPlan hbm_plan(pnp_ctx *ctx, uint64_t n) {
     return p;
 }
 
-// The key-load budget: the rank's share of its GPU's free HBM (ranks on one
-// device split it) against hbm_plan.  The optional tables that do not fit are
-// switched off on every rank (the proof bytes do not change); when even the
-// mandatory part does not fit, every rank's load fails with PNP_E_NOMEM and a
-// message naming the rank and the bytes, instead of one rank running out of
-// memory mid-proof and its peers failing in an exchange.  PNP_HBM_LIMIT
-// (bytes) caps the budget (tests).
+// The HBM budget, checked by the first proof after a key load (by then the
+// caller has released what it no longer needs, e.g. its own 8n key arrays
+// once the context holds their block copies): the rank's share of its GPU's
+// free HBM (ranks on one device split it) against hbm_plan.  The optional
+// tables that do not fit are switched off on every rank (the proof bytes do
+// not change); when even the mandatory part does not fit, every rank's proof
+// fails with PNP_E_NOMEM before any work, with a message naming the rank and
+// the bytes, instead of one rank running out of memory mid-proof and its
+// peers failing in an exchange.  PNP_HBM_LIMIT (bytes) caps the budget (tests).
 static uint64_t device_key(int dev) {
     char bus[64] = {0};
     if (hipDeviceGetPCIBusId(bus, sizeof bus, dev) != hipSuccess) snprintf(bus, sizeof bus, "dev%d", dev);
@@ -274,7 +276,6 @@ void hbm_budget(pnp_ctx *ctx) {
     ctx->hbm_lag_off = !lag;
     ctx->hbm_groups_off = !groups;
     if (!ok) {
-        ctx->pk_loaded = false;
         set_error("HBM budget: rank %d of %d needs %.2f GiB more for a proof at n = %llu, %.2f GiB free to it "
                   "(%llu rank(s) on this rank's GPU)", bad, W, all[5 * bad + 3] / 1073741824.0,
                   (unsigned long long)ctx->pk_n, all[5 * bad + 4] / 1073741824.0, (unsigned long long)share);
@@ -894,7 +895,7 @@ int pnp_load_prover_key(pnp_ctx *ctx, const ProverKeyC *pk, uint64_t D, int devi
         ctx->pk_dev = dev;
         ctx->pk_n = D;
         ctx->pk_loaded = true;
-        pnp::hbm_budget(ctx);
+        ctx->hbm_checked = false;  // the budget is checked by the next proof (pnp::hbm_budget)
     });
 }
 
@@ -916,6 +917,7 @@ void adopt_ck(pnp_ctx *ctx, pnp::DevBuf &up, uint64_t n_points) {
     }
     ctx->ck_points = n_points;
     ctx->ck_loaded = true;
+    ctx->hbm_checked = false;
 }
 
 }  // namespace
@@ -942,6 +944,7 @@ int pnp_load_commit_key(pnp_ctx *ctx, const CommitKeyC *ck, uint64_t n_points, i
             ctx->ck_hash[1] = h[1];
             ctx->ck_hash_valid = true;
             ctx->ck_loaded = true;
+            ctx->hbm_checked = false;
         } else {
             ctx->ck_hash_valid = false;
             // upload (as the reference does per call, load.cu:348-358)

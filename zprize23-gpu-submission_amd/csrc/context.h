@@ -95,6 +95,7 @@ struct pnp_ctx {
     // the key-load HBM budget (pnp_load_prover_key) left no room for these
     // optional tables: the prover commits without them (same proof bytes)
     bool hbm_lag_off = false, hbm_groups_off = false;
+    bool hbm_checked = false;  // the budget of the loaded keys has been checked (first proof)
 
     // ---- per-proof working set (sized on first use, reused) ----
     std::map<std::string, pnp::DevBuf> work;
@@ -118,7 +119,8 @@ HbmPlan hbm_plan(pnp_ctx *ctx, uint64_t n);
 // multi-GPU: AND of every rank's `mine` (one tagged all-gather); world 1: mine
 bool all_ranks_ok(pnp_ctx *ctx, bool mine);
 bool lagrange_enabled();
-// the key-load HBM budget (sets hbm_lag_off / hbm_groups_off, or throws PNP_E_NOMEM)
+// the HBM budget of the loaded keys, checked by the first proof (sets
+// hbm_lag_off / hbm_groups_off, or throws PNP_E_NOMEM)
 void hbm_budget(pnp_ctx *ctx);
 bool wire_groups_enabled();
 Fr root_of_unity(uint32_t lg);

@@ -159,6 +159,10 @@ int prove_impl(pnp_ctx *ctx, const CircuitC *cs, int device_ptrs, ProofC *out, c
             pi_val.push_back(v[k].second);
         }
     }
+    if (!ctx->hbm_checked) {  // the first proof after a key load: the HBM budget (every rank)
+        hbm_budget(ctx);
+        ctx->hbm_checked = true;
+    }
     const uint64_t N8 = 8 * n, ng = cs->n;
     const ProverKeyC &pk = ctx->pk_dev;
     Timer tm(ctx);
