@@ -12,6 +12,7 @@
 #   bench[=ARGS]     bench.py (default arguments unless ARGS, '+'-separated),
 #                    JSON line in bench.json, log in bench.err
 #   stats[=STEPS]    rocprofv3 --kernel-trace --stats over a short bench
+#   trace=ARGS       the same over bench.py ARGS ('+'-separated, e.g. --solo+7/8+--steps+2)
 #   pmc[=COUNTERS]   one rocprofv3 --pmc pass over one bench proof (counters
 #                    '+'-separated; default the SQ issue / VALU group)
 #   traffic          FETCH_SIZE and WRITE_SIZE passes (two runs)
@@ -40,6 +41,11 @@ run_step() {
     stats*)
       (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d "$OUT/stats" -o run -- \
           python3 "$R/bench.py" --steps ${arg:-3} --warmup 1 --cpu-lg 0 --drop-in "" --no-verify > "$OUT/stats.log" 2>&1) ;;
+    trace=*)
+      # kernel trace of a bench run with these arguments ('+'-separated)
+      local d=$OUT/trace_$(echo "$arg" | tr -c 'A-Za-z0-9' '_' | cut -c1-40)
+      (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d "$d" -o run -- \
+          python3 "$R/bench.py" --cpu-lg 0 --drop-in "" --no-verify ${arg//+/ } > "$d.log" 2>&1) ;;
     pmc*)
       local c=${arg:-SQ_WAVES+SQ_INSTS_VALU+SQ_WAVE_CYCLES+SQ_WAIT_ANY+SQ_WAIT_INST_ANY+SQ_ACTIVE_INST_ANY+SQ_ACTIVE_INST_VALU+SQ_INSTS_SALU}
       local d=$OUT/pmc_$(echo "$c" | tr '+' '_' | cut -c1-40)
