@@ -5,6 +5,7 @@
 // synchronous, device 0, print-and-exit on device errors (caffe/common.hpp:
 // 23-30).  v2 functions return PNP_* codes and never exit.
 #include <algorithm>
+#include <dlfcn.h>
 #include <array>
 #include <atomic>
 #include <thread>
@@ -42,6 +43,17 @@ void DevBuf::alloc(size_t b) {
     }
     bytes = b;
     const uint64_t now = g_dev_live.fetch_add(b) + b;
+    static const uint64_t trace = [] {  // PNP_HBM_TRACE=bytes: log allocations at least that large
+        const char *e = getenv("PNP_HBM_TRACE");
+        return e ? strtoull(e, nullptr, 0) : 0ULL;
+    }();
+    if (trace && b >= trace) {
+        Dl_info di{};
+        void *ra = __builtin_return_address(0);
+        dladdr(ra, &di);
+        fprintf(stderr, "pnp hbm: +%zu B (%.3f GiB live) from %s+%#lx\n", b, now / 1073741824.0,
+                di.dli_sname ? di.dli_sname : "?", (unsigned long)((char *)ra - (char *)di.dli_saddr));
+    }
     uint64_t pk = g_dev_peak.load();
     while (now > pk && !g_dev_peak.compare_exchange_weak(pk, now)) {
     }
@@ -206,7 +218,8 @@ HbmPlan hbm_plan(pnp_ctx *ctx, uint64_t n) {
     // the radix-2^29 layer array, the window tables, the XYZZ output
     const uint64_t lag = n * 96 + msm_table_bytes(n_tab, n, wk.fold_c);
     const uint64_t lag_held = ctx->lag_points.bytes + ctx->lag_table.bytes;
-    p.lag = lag > lag_held ? lag - lag_held : 0;
+    const bool lag_built = ctx->lag_n == n && (!ctx->lag_ok || ctx->lag_table_n == n);
+    p.lag = lag_built ? 0 : lag > lag_held ? lag - lag_held : 0;
     if (p.lag)
         p.transient = std::max<uint64_t>(p.transient, n * (224 + 16 + 192 + 48) +
                                                           std::min<uint64_t>(n / 2, 1ULL << 18) * 15 * 224);
@@ -215,8 +228,10 @@ HbmPlan hbm_plan(pnp_ctx *ctx, uint64_t n) {
     // sigma copy; the build: sort keys and labels, XYZZ bases, affine points
     const uint64_t seg = full ? n : (world > 1 ? per : n);
     const uint64_t grp = msm_table_bytes(5 * seg, n, wk.fold_c) + 5 * n * (4 + 4 + 32) + 4 * n * 32;
-    const uint64_t grp_held = ctx->wb.table.bytes + ctx->wb.sigma.bytes;
-    p.groups = grp > grp_held ? grp - grp_held : 0;
+    uint64_t grp_held = ctx->wb.table.bytes + ctx->wb.sigma.bytes + ctx->wb.flag.bytes;
+    for (int j = 0; j < 5; j++) grp_held += ctx->wb.grp[j].bytes + ctx->wb.rep[j].bytes + ctx->wb.scal[j].bytes;
+    const bool grp_built = ctx->wb.built && ctx->wb.n == n;
+    p.groups = grp_built ? 0 : grp > grp_held ? grp - grp_held : 0;
     if (p.groups)
         p.transient = std::max<uint64_t>(p.transient, 4 * n * (32 + 8 + 8 + 4 + 4 + 4 + 4 + 4 + 4) + 5 * n * 192 +
                                                           5 * seg * (192 + 96) + msm_table_build_bytes(5 * seg));
@@ -592,10 +607,11 @@ int pnp_commit_segments(pnp_ctx *ctx, const uint64_t *d_points, uint64_t n_point
         std::vector<uint64_t> xyzz((size_t)B * 24), aff((size_t)B * 12);
         if (n != 0) {  // n = 0: every sum is infinity (ZZ = 0)
             DevBuf tab;
-            msm_build_table(tab, d_points, n_points, ctx->msm.fold_c, ctx->stream);
+            msm_build_table(tab, d_points, n_points, msm_fold_c(n, ctx->msm.fold_c), ctx->stream);
             MsmSegs segs;
             segs.n_table = n_points;
             for (int b = 0; b < B; b++) segs.off[b] = seg_off[b];
+            segs.c = msm_fold_c(n, ctx->msm.fold_c);
             msm_run_batch(ctx->msm, nullptr, d_scalars, B, n, xyzz.data(), ctx->stream, tab.u64(), false, &segs);
         }
         xyzz_to_affine_batch_host(xyzz.data(), B, aff.data());

@@ -81,6 +81,7 @@ struct pnp_ctx {
     struct WireBases {
         bool built = false, ok = false, wires_ok = false, z_ok = false;
         bool sliced = false;            // the table holds this rank's point range of each segment
+        int c = 0;                      // its window bits (msm_fold_c of one segment's n)
         uint64_t n = 0, total = 0, m = 0, len = 0;  // domain, bases, largest group count, MSM length
         uint64_t g[5] = {}, off[5] = {};
         bool ident[5] = {};             // ungrouped wire: its scalars are its evaluations

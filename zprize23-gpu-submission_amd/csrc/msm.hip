@@ -1139,14 +1139,14 @@ static bool pipe_off() { return pipe_min_b() == 0; }
 static void msm_local_batch(MsmWork &wk, const uint64_t *d_points, const uint64_t *const *d_scalars,
                             int B, uint64_t n, uint64_t *h_xyzz, hipStream_t s,
                             const uint64_t *table, uint64_t n_table = 0, uint64_t id_base = 0,
-                            const uint64_t *seg_off = nullptr) {
+                            const uint64_t *seg_off = nullptr, int cfg_c = 0) {
     if (n == 0 || B == 0) {
         for (int b = 0; b < B; b++) put_xyzz(Xyzz::inf(), h_xyzz + 24 * b);
         return;
     }
     const bool folded = table != nullptr;
     if (!n_table) n_table = n;
-    const MsmCfg g = msm_cfg(n_table, folded ? wk.fold_c : 0, folded);
+    const MsmCfg g = msm_cfg(n_table, folded ? (cfg_c ? cfg_c : wk.fold_c) : 0, folded);
     auto need = [](DevBuf &b, size_t bytes) { if (b.bytes < bytes) b.alloc(bytes); };
     need(wk.digits, (uint64_t)g.W * B * n * 4);
     uint32_t *keys = static_cast<uint32_t *>(wk.digits.p);
@@ -1342,7 +1342,7 @@ static Xyzz mul_small(const Xyzz &p, uint64_t k) {
 // then takes point ranges.
 static bool msm_bucket_batch(MsmWork &wk, const uint64_t *const *sc, int B, uint64_t n_full, uint64_t p0,
                              uint64_t p1, uint64_t *part, hipStream_t s, const uint64_t *table,
-                             const uint64_t *seg_off = nullptr) {
+                             const uint64_t *seg_off = nullptr, int cfg_c = 0) {
     const int W = wk.world;
     // Bucket ranges pay from 4 ranks on (solo-rank times per proof at n = 2^22,
     // points vs buckets: 2 ranks 91.1 vs 94.0 ms, 4 ranks 56.0 vs 55.3, 8 ranks
@@ -1354,7 +1354,7 @@ static bool msm_bucket_batch(MsmWork &wk, const uint64_t *const *sc, int B, uint
         return e ? atoi(e) : 4;
     }();
     if (W < min_world) return false;
-    const MsmCfg g = msm_cfg(n_full, wk.fold_c, true);
+    const MsmCfg g = msm_cfg(n_full, cfg_c ? cfg_c : wk.fold_c, true);
     int lgW = 0;
     while ((1 << lgW) < W) lgW++;
     const int cbits = std::min(SORT_CB, g.c - 1);  // coarse bits of the whole bucket index
@@ -1525,6 +1525,8 @@ static bool msm_bucket_batch(MsmWork &wk, const uint64_t *const *sc, int B, uint
     return true;
 }
 
+int msm_fold_c(uint64_t n_points, int fold_c) { return msm_cfg(n_points, fold_c, true).c; }
+
 // ---- HBM of the MSM machinery (upper bounds for the key-load budget,
 // abi.cpp hbm_plan; checked against the measured peak by tests/test_gpu_hbm.py)
 uint64_t msm_table_bytes(uint64_t n_points, uint64_t n_cfg, int fold_c) {
@@ -1575,7 +1577,7 @@ void msm_run_batch(MsmWork &wk, const uint64_t *d_points, const uint64_t *const 
     }
     if (wk.world == 1) {
         if (segs)
-            msm_local_batch(wk, nullptr, d_scalars, B, n, h_xyzz, s, table, segs->n_table, 0, segs->off);
+            msm_local_batch(wk, nullptr, d_scalars, B, n, h_xyzz, s, table, segs->n_table, 0, segs->off, segs->c);
         else
             msm_local_batch(wk, d_points, d_scalars, B, n, h_xyzz, s, table);
         return;
@@ -1595,9 +1597,11 @@ void msm_run_batch(MsmWork &wk, const uint64_t *d_points, const uint64_t *const 
         set_error("msm: a sliced segment table in bucket-range mode");
         throw Error(PNP_E_ARG);
     }
-    if (!(table && wk.full_table() && msm_bucket_batch(wk, sc.data(), B, n_tab, p0, p1, part.data(), s, table, off)))
+    const int cc = segs ? segs->c : 0;
+    if (!(table && wk.full_table() &&
+          msm_bucket_batch(wk, sc.data(), B, n_tab, p0, p1, part.data(), s, table, off, cc)))
         msm_local_batch(wk, d_points ? d_points + 12 * p0 : nullptr, sc.data(), B, p1 - p0, part.data(), s, table,
-                        segs ? n_tab : full ? n_tab : 0, full ? p0 : 0, off);
+                        segs ? n_tab : full ? n_tab : 0, full ? p0 : 0, off, cc);
     const std::vector<uint64_t> all = rank_allgather(wk, s, part.data(), B * 24, PNP_EX_TAG_MSM_SUMS);
     for (int b = 0; b < B; b++) {
         Xyzz acc = Xyzz::inf();

@@ -195,7 +195,13 @@ struct MsmSegs {
     // of every set (msm_point_range of the MSM length), off[] are the slices'
     // starts in it — 1/world of the full table
     bool sliced = false;
+    // window bits of the table (0: msm_cfg(n_table)); a table over several
+    // point sets takes the width for ONE set's size (msm_fold_c(n)): its
+    // buckets serve one set per MSM
+    int c = 0;
 };
+// the folded layout's window bits for an MSM over n_points points
+int msm_fold_c(uint64_t n_points, int fold_c);
 // scalars_local: multi-GPU, d_scalars[b] hold only this rank's point range
 // segs: `table` is segmented as above (d_points unused)
 void msm_run_batch(MsmWork &w, const uint64_t *d_points, const uint64_t *const *d_scalars, int B,

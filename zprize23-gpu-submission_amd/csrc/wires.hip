@@ -419,6 +419,8 @@ void build_wire_bases(pnp_ctx *ctx, uint64_t n) {
         wb.total += sl;
     }
     wb.m = n;
+    // the windows of ONE segment's MSM (n points), not of the whole table
+    wb.c = msm_fold_c(n, ctx->msm.fold_c);
     if (wb.total) {
         DevBuf xyzz(wb.total * 192), aff(wb.total * 96);
         for (int j = 0; j < 5; j++) {
@@ -430,7 +432,7 @@ void build_wire_bases(pnp_ctx *ctx, uint64_t n) {
         for (auto &b : bx) b.release();
         xyzz_to_affine_dev(xyzz.u64(), wb.total, aff.u64(), s);
         xyzz.release();
-        msm_build_table(wb.table, aff.u64(), wb.total, ctx->msm.fold_c, s);
+        msm_build_table(wb.table, aff.u64(), wb.total, wb.c, s);
     }
     // every MSM of the batch reads n scalars: an ungrouped wire's evaluations,
     // a grouped wire's group values at their slots (zero elsewhere)
@@ -520,6 +522,7 @@ bool commit_wires_grouped(pnp_ctx *ctx, const uint64_t *const *d_evals, uint64_t
     MsmSegs segs;
     segs.n_table = wb.total;
     segs.sliced = wb.sliced;
+    segs.c = wb.c;
     for (int j = 0; j < 4; j++) {
         sc[j] = wb.ident[j] ? d_evals[j] : wb.scal[j].u64();
         segs.off[j] = wb.off[j];
@@ -562,6 +565,7 @@ bool commit_z_grouped(pnp_ctx *ctx, const uint64_t *d_z, uint64_t n, CommitmentC
     MsmSegs segs;
     segs.n_table = wb.total;
     segs.sliced = wb.sliced;
+    segs.c = wb.c;
     segs.off[0] = wb.off[4];
     uint64_t xyzz[24], aff[12];
     msm_run_batch(ctx->msm, nullptr, sc, 1, wb.len, xyzz, s, wb.table.u64(), false, &segs);
