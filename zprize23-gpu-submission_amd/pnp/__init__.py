@@ -235,8 +235,7 @@ class Context:
             cb3 = exchange.c_alltoallv()
             check(self.lib.pnp_set_exchange_v(self.h, cb3, None, exchange.vsend.data_ptr(),
                                               exchange.vrecv.data_ptr(), exchange.vsend.numel() * 8),
-                  "pnp_set_exchange_v", "pnp_commit_segments", "pnp_hbm_usage",
-           "pnp_ctx_stream", "pnp_set_exchange_ordered")
+                  "pnp_set_exchange_v")
             keep.append(cb3)
         self._exchange = keep  # keep the callbacks alive
 
