@@ -763,9 +763,14 @@ __global__ __launch_bounds__(256, PNP_ACC_WAVES) void k_accumulate29(const uint3
 // sorted entries E = offs[WB] and the pieces the lanes start fresh — one per
 // lane with entries (ceil(E / S)) plus one per non-empty bucket whose first
 // entry is not a lane's first (offs[b] % S != 0).  Every other entry is one
-// mixed addition: madds = E - pieces.  ctr[0] += E, ctr[1] += pieces.
-__global__ __launch_bounds__(256) void k_count_pieces(const uint32_t *offs, uint64_t WB, uint32_t S,
-                                                      unsigned long long *ctr) {
+// mixed addition: madds = E - pieces.  ctr[0] = E, ctr[1 + (block & 63)] +=
+// the block's pieces (64 counters: one atomic per 1024 buckets, spread, so
+// the ~2M-bucket launch takes microseconds, not the ~0.3 ms one contended
+// counter cost); the host sums them.
+constexpr int WCTR_SLOTS = 64;
+__global__ __launch_bounds__(1024) void k_count_pieces(const uint32_t *offs, uint64_t WB, uint32_t S,
+                                                       unsigned long long *ctr) {
+    __shared__ uint32_t part[16];
     const uint64_t b = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
     bool fresh = false;
     if (b < WB) {
@@ -773,11 +778,17 @@ __global__ __launch_bounds__(256) void k_count_pieces(const uint32_t *offs, uint
         fresh = offs[b + 1] > o && (o % S) != 0;
     }
     const unsigned long long m = __ballot(fresh);
-    if ((threadIdx.x & 63) == 0 && m) atomicAdd(&ctr[1], (unsigned long long)__popcll(m));
-    if (b == 0) {
-        const unsigned long long tot = offs[WB];
-        atomicAdd(&ctr[0], tot);
-        atomicAdd(&ctr[1], (tot + S - 1) / S);
+    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = (uint32_t)__popcll(m);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t t = 0;
+        for (int w = 0; w < (int)(blockDim.x >> 6); w++) t += part[w];
+        if (t) atomicAdd(&ctr[1 + (blockIdx.x & (WCTR_SLOTS - 1))], (unsigned long long)t);
+        if (blockIdx.x == 0) {
+            const unsigned long long tot = offs[WB];
+            ctr[0] = tot;
+            atomicAdd(&ctr[1], (tot + S - 1) / S);
+        }
     }
 }
 
@@ -1065,9 +1076,9 @@ static void accumulate_group(MsmWork &wk, MsmGroup &gb, const GroupPlan &gp, con
         // the dense bound nv x rows x n (zero digits drop out of the real count)
         wk.timer->credit("msm_entries_dense", (double)nent);
         if (table) {  // the real work, counted on the device (k_count_pieces)
-            need(gb.wctr, 16);
-            PNP_HIP(hipMemsetAsync(gb.wctr.p, 0, 16, s));
-            hipLaunchKernelGGL(k_count_pieces, dim3((uint32_t)((WB + 255) / 256)), dim3(256), 0, s, bstart, WB, S,
+            need(gb.wctr, 8 * (1 + WCTR_SLOTS));
+            PNP_HIP(hipMemsetAsync(gb.wctr.p, 0, 8 * (1 + WCTR_SLOTS), s));
+            hipLaunchKernelGGL(k_count_pieces, dim3((uint32_t)((WB + 1023) / 1024)), dim3(1024), 0, s, bstart, WB, S,
                                static_cast<unsigned long long *>(gb.wctr.p));
             PNP_HIP(hipGetLastError());
             gb.wctr_live = true;
@@ -1078,14 +1089,16 @@ static void accumulate_group(MsmWork &wk, MsmGroup &gb, const GroupPlan &gp, con
 // queue the D2H copy of a timed launch's work counters (before the caller's
 // stream synchronisation) / credit them to the timer after it
 static void wctr_fetch(MsmGroup &gb, hipStream_t s) {
-    if (gb.wctr_live) PNP_HIP(hipMemcpyAsync(gb.wctr_h, gb.wctr.p, 16, hipMemcpyDeviceToHost, s));
+    if (gb.wctr_live) PNP_HIP(hipMemcpyAsync(gb.wctr_h, gb.wctr.p, 8 * (1 + WCTR_SLOTS), hipMemcpyDeviceToHost, s));
 }
 static void wctr_credit(MsmWork &wk, MsmGroup &gb) {
     if (!gb.wctr_live) return;
     gb.wctr_live = false;
     if (!wk.timer) return;
+    unsigned long long pieces = 0;
+    for (int k = 1; k <= WCTR_SLOTS; k++) pieces += gb.wctr_h[k];
     wk.timer->credit("msm_entries", (double)gb.wctr_h[0]);
-    wk.timer->credit("msm_madds", (double)(gb.wctr_h[0] - gb.wctr_h[1]));
+    wk.timer->credit("msm_madds", (double)(gb.wctr_h[0] - pieces));
 }
 
 static const uint64_t *reduce_group(MsmGroup &gb, const GroupPlan &gp, const MsmCfg &g, hipStream_t s,

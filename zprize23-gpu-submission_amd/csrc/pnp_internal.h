@@ -135,7 +135,7 @@ struct MsmGroup {
     // really did, counted on the device from the bucket starts — {sorted
     // entries, pieces started fresh}; mixed additions = entries - pieces
     DevBuf wctr;
-    unsigned long long wctr_h[2] = {0, 0};
+    unsigned long long wctr_h[65] = {};  // entries, then 64 piece counters (msm.hip k_count_pieces)
     bool wctr_live = false;
 };
 struct MsmWork {
