@@ -109,13 +109,19 @@ def main():
         from pnp import abi
         from bench import Synthetic
         from pnp.shard import a2a_bytes_for
+        import time
+        t0 = time.time()
+        say = lambda what: print(f"rank {rank}: {what} ({time.time() - t0:.1f} s)", flush=True)
         ctx = pnp.Context(0)
         ex = WindowExchange(rank, world, device="cuda", a2a_bytes=a2a_bytes_for(lg, world),
                             v_bytes=_v_bytes(lg, world))
         ctx.set_msm_shard(ex)
+        say("context")
         syn = Synthetic(ctx, lg, gates, seed=seed, circuit=circuit)
+        say("instance")
         ctx.load_prover_key(syn.pk, syn.n, device_ptrs=True)
         ctx.load_commit_key(syn.ck, syn.n, device_ptrs=True)
+        say(f"keys loaded, hbm {ctx.hbm_usage()}")
         # the context keeps block-layout copies of this rank's 8n evaluations
         # and never reads the caller's 8n arrays again: free them, so that 8
         # ranks fit one GPU's HBM
@@ -126,11 +132,13 @@ def main():
         groups = os.environ.get("PNP_EXPECT_GROUPS") == "1"
         if groups:
             ctx.kernel_timing(True)
+        say("proving")
         try:
             proof = ctx.prove(syn.cs, device_ptrs=True)
         except Exception:
             print(f"rank {rank}: exchange error: {ex.error!r}", flush=True)
             raise
+        say(f"proved, hbm {ctx.hbm_usage()}")
         if groups:  # the wires and z were committed over their groups
             assert ctx.kernel_bytes("wire_groups_used") == 1, ctx.kernel_bytes("wire_groups_used")
             assert ctx.kernel_bytes("z_groups_used") == 1, ctx.kernel_bytes("z_groups_used")

@@ -34,15 +34,28 @@ def _launch(world, args, tmp_path, timeout, **extra_env):
                                       + args, env=env, stdout=log, stderr=subprocess.STDOUT))
     outs = []
     try:
-        # a heartbeat on the real stderr (pytest captures sys.stderr): a GPU box
-        # takes a run that prints nothing for minutes for a hung one
+        # a heartbeat a GPU box can see (pytest captures fd 1 and 2 during a
+        # test): a line every 30 s in gpurun_out/heartbeat.log when that
+        # directory exists — the box takes a run that writes nothing for
+        # minutes for a hung one
         import time
-        t0 = time.time()
+        hb_dir = os.path.join(os.path.dirname(HERE), "gpurun_out")
+        t0 = last = time.time()
         while any(p.poll() is None for p in procs) and time.time() - t0 < timeout:
             time.sleep(1)
-            if int(time.time() - t0) % 30 == 0:
-                print(f"  [{world} ranks: {sum(p.poll() is None for p in procs)} running, "
-                      f"{time.time() - t0:.0f} s]", file=sys.__stderr__, flush=True)
+            if time.time() - last >= 30:
+                last = time.time()
+                line = (f"[{time.strftime('%H:%M:%S')}] {world} ranks ({' '.join(args[:1])}): "
+                        f"{sum(p.poll() is None for p in procs)} running, {last - t0:.0f} s\n")
+                for r in range(world):  # each rank's last progress line
+                    try:
+                        tail = (tmp_path / f"rank{r}.log").read_bytes().decode(errors="replace").strip()
+                        line += f"    rank {r}: {tail.splitlines()[-1][:160] if tail else ''}\n"
+                    except OSError:
+                        pass
+                if os.path.isdir(hb_dir):
+                    with open(os.path.join(hb_dir, "heartbeat.log"), "a") as f:
+                        f.write(line)
         for r, p in enumerate(procs):
             p.wait(timeout=max(1, timeout - (time.time() - t0)))
             outs.append((tmp_path / f"rank{r}.log").read_bytes().decode(errors="replace"))
