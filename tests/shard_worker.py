@@ -111,7 +111,9 @@ def main():
         from pnp.shard import a2a_bytes_for
         import time
         t0 = time.time()
-        say = lambda what: print(f"rank {rank}: {what} ({time.time() - t0:.1f} s)", flush=True)
+        def say(what):
+            f_, t_ = torch.cuda.mem_get_info()
+            print(f"rank {rank}: {what} ({time.time() - t0:.1f} s, HBM free {f_ / 2**30:.1f} GiB)", flush=True)
         ctx = pnp.Context(0)
         ex = WindowExchange(rank, world, device="cuda", a2a_bytes=a2a_bytes_for(lg, world),
                             v_bytes=_v_bytes(lg, world))

@@ -45,8 +45,16 @@ def _launch(world, args, tmp_path, timeout, **extra_env):
             time.sleep(1)
             if time.time() - last >= 30:
                 last = time.time()
+                free = ""
+                try:
+                    import torch
+                    if torch.cuda.is_initialized():
+                        f_, t_ = torch.cuda.mem_get_info()
+                        free = f", HBM free {f_ / 2**30:.1f} of {t_ / 2**30:.0f} GiB"
+                except Exception:
+                    pass
                 line = (f"[{time.strftime('%H:%M:%S')}] {world} ranks ({' '.join(args[:1])}): "
-                        f"{sum(p.poll() is None for p in procs)} running, {last - t0:.0f} s\n")
+                        f"{sum(p.poll() is None for p in procs)} running, {last - t0:.0f} s{free}\n")
                 for r in range(world):  # each rank's last progress line
                     try:
                         tail = (tmp_path / f"rank{r}.log").read_bytes().decode(errors="replace").strip()
