@@ -213,16 +213,14 @@ HbmPlan hbm_plan(pnp_ctx *ctx, uint64_t n) {
     const uint64_t held = work_held + ntt_held + ctx->ck_table.bytes + msm_work_held(wk);
     const uint64_t total = work + ntt + ck_tab + msm;
     p.mandatory = total > held ? total - held : 0;
-    p.transient = ctx->ck_table.bytes ? 0 : msm_table_build_bytes(n_tab);
+    p.t_mand = ctx->ck_table.bytes ? 0 : msm_table_build_bytes(n_tab);
     // the Lagrange basis (n affine points) + its folded table; its build:
     // the radix-2^29 layer array, the window tables, the XYZZ output
     const uint64_t lag = n * 96 + msm_table_bytes(n_tab, n, wk.fold_c);
     const uint64_t lag_held = ctx->lag_points.bytes + ctx->lag_table.bytes;
     const bool lag_built = ctx->lag_n == n && (!ctx->lag_ok || ctx->lag_table_n == n);
     p.lag = lag_built ? 0 : lag > lag_held ? lag - lag_held : 0;
-    if (p.lag)
-        p.transient = std::max<uint64_t>(p.transient, n * (224 + 16 + 192 + 48) +
-                                                          std::min<uint64_t>(n / 2, 1ULL << 18) * 15 * 224);
+    if (p.lag) p.t_lag = n * (224 + 16 + 192 + 48) + std::min<uint64_t>(n / 2, 1ULL << 18) * 15 * 224;
     // the copy-constraint groups: 5 segments of n slots (this rank's slice in
     // point-range mode), their folded table, the group maps and scalars, the
     // sigma copy; the build: sort keys and labels, XYZZ bases, affine points
@@ -233,8 +231,9 @@ HbmPlan hbm_plan(pnp_ctx *ctx, uint64_t n) {
     const bool grp_built = ctx->wb.built && ctx->wb.n == n;
     p.groups = grp_built ? 0 : grp > grp_held ? grp - grp_held : 0;
     if (p.groups)
-        p.transient = std::max<uint64_t>(p.transient, 4 * n * (32 + 8 + 8 + 4 + 4 + 4 + 4 + 4 + 4) + 5 * n * 192 +
-                                                          5 * seg * (192 + 96) + msm_table_build_bytes(5 * seg));
+        p.t_groups = 4 * n * (32 + 8 + 8 + 4 + 4 + 4 + 4 + 4 + 4) + 5 * n * 192 + 5 * seg * (192 + 96) +
+                     msm_table_build_bytes(5 * seg);
+    p.transient = std::max({p.t_mand, p.t_lag, p.t_groups});
     return p;
 }
 
@@ -271,11 +270,15 @@ void hbm_budget(pnp_ctx *ctx) {
         budget = std::min<uint64_t>(budget, lim > live ? lim - live : 0);
     }
     const HbmPlan p = hbm_plan(ctx, ctx->pk_n);
-    const uint64_t base = p.mandatory + p.transient;
+    // each optional table with the largest build scratch among what is built
+    const uint64_t base = p.mandatory + p.t_mand;
+    const uint64_t with_lag = p.mandatory + p.lag + std::max(p.t_mand, p.t_lag);
+    const uint64_t with_groups = with_lag - std::max(p.t_mand, p.t_lag) + p.groups +
+                                 std::max({p.t_mand, p.t_lag, p.t_groups});
     uint64_t mine[5];
     mine[0] = base <= budget;
-    mine[1] = lagrange_enabled() && base + p.lag <= budget;
-    mine[2] = mine[1] && wire_groups_enabled() && base + p.lag + p.groups <= budget;
+    mine[1] = lagrange_enabled() && with_lag <= budget;
+    mine[2] = mine[1] && wire_groups_enabled() && with_groups <= budget;
     mine[3] = base;
     mine[4] = budget;
     std::vector<uint64_t> all(mine, mine + 5);

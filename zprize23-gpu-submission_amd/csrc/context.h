@@ -114,7 +114,8 @@ struct HbmPlan {
     uint64_t mandatory = 0;  // per-proof buffers, NTT tables, commit-key table, MSM work
     uint64_t lag = 0;        // the Lagrange-basis key and its folded table (optional)
     uint64_t groups = 0;     // the copy-constraint groups and their table (optional)
-    uint64_t transient = 0;  // the largest build scratch on top of them
+    uint64_t transient = 0;  // the largest build scratch on top of them (max of the three below)
+    uint64_t t_mand = 0, t_lag = 0, t_groups = 0;  // build scratch of the commit-key table, Lagrange, groups
 };
 HbmPlan hbm_plan(pnp_ctx *ctx, uint64_t n);
 // multi-GPU: AND of every rank's `mine` (one tagged all-gather); world 1: mine
