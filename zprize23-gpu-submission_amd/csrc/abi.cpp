@@ -442,6 +442,11 @@ void pnp_ctx_destroy(pnp_ctx *ctx) {
         for (hipEvent_t e : {ctx->ev_fork, ctx->ev_w8, ctx->ev_z8}) (void)hipEventDestroy(e);
     }
     (void)hipStreamDestroy(ctx->stream);
+    for (hipEvent_t e : ctx->ktimer.pool) (void)hipEventDestroy(e);
+    for (auto &p : ctx->ktimer.pending) {
+        (void)hipEventDestroy(p.e0);
+        (void)hipEventDestroy(p.e1);
+    }
     delete ctx;
 }
 
