@@ -29,17 +29,19 @@ for key in sorted(acc, key=lambda k: -sum(acc[k]["_dur_ns"])):
           f"{100 * mean('SQ_ACTIVE_INST_ANY') / wc:7.1f} {100 * mean('SQ_WAIT_ANY') / wc:6.1f} "
           f"{100 * mean('SQ_WAIT_INST_ANY') / wc:9.1f}")
 
-# k_accumulate29: the mixed additions the counters allow per launch.  Every
-# lane-addition issues ~5,154 VALU wave-instructions per 64 lanes
-# (tools/isa_model.py); SQ_INSTS_VALU also counts the non-addition work (the
-# binary search, staging, stores), so this is an upper bound on the real count
-# the bench credits (roofline.madds_per_launch).
+# k_accumulate29: the mixed additions the counters allow per launch.  The
+# static model of the compiled kernel (tools/isa_model.py) issues ~5,154 VALU
+# wave-instructions per 64 lane-additions on its longest path; SQ_INSTS_VALU
+# also counts the non-addition work (the binary search, staging, stores).  With
+# a bench JSON as the second argument the measured VALU per device-counted
+# addition (roofline.madds_per_proof) is printed beside it: a count the
+# counters cannot have issued would show as far fewer VALU per addition.
 VALU_PER_MADD = 5154
 rows = [(k, acc[k]) for k in acc if k[0].endswith("k_accumulate29") and acc[k].get("SQ_INSTS_VALU")]
 if rows:
     tot_m = tot_ns = tot_n = 0
     print()
-    print(f"{'k_accumulate29 grid':>20s} {'n':>3s} {'dur_us':>9s} {'VALU_G/launch':>13s} {'madds_le_M':>11s}")
+    print(f"{'k_accumulate29 grid':>20s} {'n':>3s} {'dur_us':>9s} {'VALU_G/launch':>13s} {'madds_mdl_M':>11s}")
     for k, d in sorted(rows, key=lambda r: -r[0][1]):
         v = [x for x in d["SQ_INSTS_VALU"]]
         n = len(v)
@@ -49,5 +51,12 @@ if rows:
         tot_ns += dur * n
         tot_n += n
         print(f"{k[1]:20d} {n:3d} {dur / 1e3:9.1f} {sum(v) / n / 1e9:13.3f} {m / 1e6:11.2f}")
-    print(f"all launches: {tot_n}, madds <= {tot_m / 1e6:.1f} M, {tot_m / (tot_ns / 1e9) / 1e9:.3f} G madd/s "
+    print(f"all launches: {tot_n}, madds at the model VALU/addition {tot_m / 1e6:.1f} M, {tot_m / (tot_ns / 1e9) / 1e9:.3f} G madd/s "
           f"over their summed duration")
+    if len(sys.argv) > 2:
+        import json
+        with open(sys.argv[2]) as f:
+            counted = json.loads(f.read().strip().splitlines()[-1])["roofline"]["madds_per_proof"]
+        valu = sum(sum(d["SQ_INSTS_VALU"]) for _, d in rows)
+        print(f"device-counted madds per proof {counted / 1e6:.1f} M (bench): {valu * 64 / counted:.0f} VALU "
+              f"lane-instructions per counted madd vs {VALU_PER_MADD} in the static model")
