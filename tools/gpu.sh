@@ -7,7 +7,7 @@
 # and the steps are chained: the first failing step ends the call (no step
 # runs on the GPU after a fault, an abort or a time limit).  Steps:
 #
-#   tests[=K]        pytest -m gpu (optionally -k K), one process
+#   tests[=K]        pytest -m gpu (optionally -k K, '+' for spaces), one process
 #   smoke            __graft_entry__.smoke()
 #   bench[=ARGS]     bench.py (default arguments unless ARGS, '+'-separated),
 #                    JSON line in bench.json, log in bench.err
@@ -33,7 +33,7 @@ run_step() {
   case "$step" in
     tests*)
       timeout -k 10 1100 python -u -m pytest tests -m gpu -x -v --timeout ${TEST_TIMEOUT:-400} --timeout-method thread \
-          ${arg:+-k "$arg"} > "$OUT/pytest_gpu.log" 2>&1 ;;
+          ${arg:+-k "${arg//+/ }"} > "$OUT/pytest_gpu.log" 2>&1 ;;
     smoke)
       timeout -k 10 180 python -u -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 ;;
     bench*)
