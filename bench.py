@@ -661,9 +661,15 @@ def main():
                                                           / max(sum(solo.v_sent_to), 1), 4)
                                                     if getattr(solo, "v_sent_to", None) else None),
                            "callback_ms_per_proof": round(1e3 * solo.cb_seconds / (args.steps + args.warmup), 3),
+                           "ordered": solo.ordered,
+                           # the (meaningless, deterministic) proof bytes: the same with the
+                           # ordered and the synchronised loopback (tests/test_gpu_rccl.py)
+                           "proof_sha256": __import__("hashlib").sha256(abi.proof_to_bytes(proof)).hexdigest(),
                            "note": "per-rank work of a W-GPU proof; the collectives are loopbacks "
                                    "(their xGMI time is not included; callback_ms is the host time "
-                                   "spent inside the loopback callbacks)"}
+                                   "spent inside the loopback callbacks; ordered: enqueued on the "
+                                   "library stream without host syncs, as the RCCL exchange)"}
+            solo.check_tags()
         if not args.no_verify:
             chk = check_proof(syn, proof, args.circuit)
             out["verified"] = chk.pop("verified") and all_equal

@@ -409,3 +409,23 @@ def test_commit_segments_refuses_out_of_range(ctx):
     ds = to_dev(rand_fr_mont_arr(np.random.default_rng(3), 4))
     with pytest.raises(pnp.PnpError, match="PNP_E_ARG"):
         ctx.commit_segments(dp.data_ptr(), 10, [7], [ds.data_ptr()], 4)
+
+
+def test_commit_segments_empty_and_sparse_msms(ctx):
+    """A batch whose MSMs leave long runs of empty buckets: one all-zero MSM
+    (every bucket of its range empty: an accumulation lane crossing it skips
+    2^c buckets at once, msm.hip next_bucket), one with three non-zero scalars
+    and one whose scalars are all equal (one bucket per window holds every
+    entry), beside a random one — each against the oracle."""
+    n = 1 << 14
+    rng = np.random.default_rng(4242)
+    pts = _srs_host(n, 42)
+    dp = to_dev(pts)
+    scs = [rand_fr_mont_arr(rng, n), np.zeros((n, 4), dtype=np.uint64), np.zeros((n, 4), dtype=np.uint64),
+           np.repeat(rand_fr_mont_arr(rng, 1), n, axis=0)]
+    scs[2][[5, 4000, n - 1]] = rand_fr_mont_arr(rng, 3)
+    ds = [to_dev(s) for s in scs]
+    got = ctx.commit_segments(dp.data_ptr(), n, [0] * 4, [d.data_ptr() for d in ds], n)
+    for b in range(4):
+        e = _oracle_commit(pts, scs[b])
+        assert (np.array(list(got[b].x) + list(got[b].y), dtype=np.uint64) == e).all(), b

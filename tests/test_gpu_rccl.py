@@ -107,3 +107,26 @@ def test_native_rccl_world1(tmp_path):
     out = log.read_text(errors="replace")
     assert p.returncode == 0, out[-3000:]
     assert "native rccl world-1 exchange ok" in out
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("solo", ["1/4", "7/8"])
+def test_solo_ordered_loopback_matches_synchronised(tmp_path, solo):
+    """bench.py --solo with the loopback enqueued on the library stream (no
+    host syncs, as the RCCL exchange: pnp.shard.SoloExchange.ordered) gives
+    the same proof bytes as the synchronised loopback (PNP_EXCHANGE_SYNC=1):
+    the stream ordering alone carries the exchange dependencies."""
+    import json
+    root = os.path.dirname(HERE)
+    res = {}
+    for mode, extra in (("ordered", {}), ("sync", {"PNP_EXCHANGE_SYNC": "1"})):
+        env = dict(os.environ, **extra)
+        out = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--lg", "16", "--solo", solo,
+                              "--steps", "2", "--warmup", "1", "--cpu-lg", "0", "--drop-in", "", "--no-verify"],
+                             env=env, capture_output=True, text=True, timeout=110, cwd=root)
+        assert out.returncode == 0, out.stderr[-3000:]
+        res[mode] = json.loads(out.stdout.strip().splitlines()[-1])
+    assert res["ordered"]["solo"]["ordered"] is True
+    assert res["sync"]["solo"]["ordered"] is False
+    assert res["ordered"]["timed_proofs_identical"] and res["sync"]["timed_proofs_identical"]
+    assert res["ordered"]["solo"]["proof_sha256"] == res["sync"]["solo"]["proof_sha256"]

@@ -261,6 +261,10 @@ static void scan_u32(uint32_t *d, uint64_t n, DevBuf &scratch, hipStream_t s) {
 #ifndef PNP_TILE_K
 #define PNP_TILE_K 16384
 #endif
+// the next tile's loads issued before this tile's LDS phases (both passes)
+#ifndef PNP_SORT_PREFETCH
+#define PNP_SORT_PREFETCH 1
+#endif
 constexpr int TILE_K = PNP_TILE_K;
 constexpr int KPT = TILE_K / 1024;  // keys per lane per tile
 static_assert(TILE_K % 4096 == 0 && TILE_K <= 16384, "PNP_TILE_K: a multiple of 4096 up to 16384");
@@ -303,24 +307,40 @@ __global__ __launch_bounds__(1024) void k_coarse_scatter(const uint32_t *keys, K
     uint64_t lo = (uint64_t)ch * chunk, hi = lo + chunk < n ? lo + chunk : n;
     const uint32_t *kb = keys + ((uint64_t)v * kr.vstride + kr.off) * n;
     const bool vec = ((n | chunk) & 3) == 0;
-    for (int r = 0; r < kr.rows; r++) {
-        const uint32_t *k = kb + (uint64_t)r * n;
+    // the tiles of every row in one sequence, so the next tile's keys (even
+    // the next row's first) are loaded while this tile goes through its LDS
+    // phases: the barriers wait for LDS only, not for loads in flight
+    const uint64_t ntile = hi > lo ? (hi - lo + TILE_K - 1) / TILE_K : 0, nt = ntile * kr.rows;
+    uint32_t nxt[KPT];
+    auto load_tile = [&](uint64_t t, uint32_t *key) {
+        const uint32_t *k = kb + (t / ntile) * n;
+        const uint64_t tb = lo + (t % ntile) * TILE_K;
+        // KPT keys per lane, in groups of four consecutive points (16-byte loads)
+#pragma unroll
+        for (int g = 0; g < KPT / 4; g++) {
+            const uint64_t i0 = tb + 4 * (threadIdx.x + 1024 * g);
+            if (vec && i0 + 4 <= hi) {
+                uint4 q = *reinterpret_cast<const uint4 *>(k + i0);
+                key[4 * g] = q.x; key[4 * g + 1] = q.y; key[4 * g + 2] = q.z; key[4 * g + 3] = q.w;
+            } else {
+#pragma unroll
+                for (int j = 0; j < 4; j++) key[4 * g + j] = i0 + j < hi ? k[i0 + j] : KEY_ZERO;
+            }
+        }
+    };
+    if (nt) load_tile(0, nxt);
+    for (uint64_t t = 0; t < nt; t++) {
+        const int r = (int)(t / ntile);
+        const uint64_t tb = lo + (t % ntile) * TILE_K;
         const uint64_t so = v < kr.nseg ? kr.seg_off[v] : 0;
         const uint32_t idb = (uint32_t)((kr.id_row0 + r) * kr.id_mul + kr.id_base + so);
-        for (uint64_t tb = lo; tb < hi; tb += TILE_K) {
-            // KPT keys per lane, in groups of four consecutive points (16-byte loads)
+        {
             uint32_t key[KPT], rank[KPT];
 #pragma unroll
-            for (int g = 0; g < KPT / 4; g++) {
-                const uint64_t i0 = tb + 4 * (threadIdx.x + 1024 * g);
-                if (vec && i0 + 4 <= hi) {
-                    uint4 q = *reinterpret_cast<const uint4 *>(k + i0);
-                    key[4 * g] = q.x; key[4 * g + 1] = q.y; key[4 * g + 2] = q.z; key[4 * g + 3] = q.w;
-                } else {
-#pragma unroll
-                    for (int j = 0; j < 4; j++) key[4 * g + j] = i0 + j < hi ? k[i0 + j] : KEY_ZERO;
-                }
-            }
+            for (int j = 0; j < KPT; j++) key[j] = nxt[j];
+#if PNP_SORT_PREFETCH
+            if (t + 1 < nt) load_tile(t + 1, nxt);
+#endif
 #pragma unroll
             for (int j = 0; j < KPT; j++)
                 if (key[j] != KEY_ZERO) rank[j] = atomicAdd(&lh[(key[j] & 0x7FFFFFFFu) >> fb], 1u);
@@ -354,6 +374,9 @@ __global__ __launch_bounds__(1024) void k_coarse_scatter(const uint32_t *keys, K
             }
             __syncthreads();
         }
+#if !PNP_SORT_PREFETCH
+        if (t + 1 < nt) load_tile(t + 1, nxt);
+#endif
     }
 }
 
@@ -400,20 +423,32 @@ __global__ __launch_bounds__(1024) void k_fine_sort(const uint32_t *ent, const u
     __syncthreads();
     for (int f = threadIdx.x; f < NF; f += blockDim.x) bstart[p * NF + f] = h[f];
     constexpr int PER = TILE_F / 1024;
+    uint32_t ne[PER], nf[PER];
+    auto load_tile = [&](uint32_t tb) {
+#pragma unroll
+        for (int j = 0; j < PER; j++) {
+            uint32_t k = tb + threadIdx.x + j * 1024;  // coalesced, one entry per lane per step
+            nf[j] = 0;
+            ne[j] = 0xFFFFFFFFu;
+            if (k < pe) {
+                nf[j] = fk[k];
+                ne[j] = ent[k];
+            }
+        }
+    };
+    if (ps < pe) load_tile(ps);
     for (uint32_t tb = ps; tb < pe; tb += TILE_F) {
         uint32_t e[PER], rank[PER];
         uint32_t f[PER];
 #pragma unroll
-        for (int j = 0; j < PER; j++) {
-            uint32_t k = tb + threadIdx.x + j * 1024;  // coalesced, one entry per lane per step
-            f[j] = 0;
-            e[j] = 0xFFFFFFFFu;
-            if (k < pe) {
-                f[j] = fk[k];
-                e[j] = ent[k];
-                rank[j] = atomicAdd(&lh[f[j]], 1u);
-            }
-        }
+        for (int j = 0; j < PER; j++) e[j] = ne[j], f[j] = nf[j];
+#if PNP_SORT_PREFETCH
+        // in flight through this tile's LDS phases (the barriers wait for LDS only)
+        if (pe - tb > (uint32_t)TILE_F) load_tile(tb + TILE_F);
+#endif
+#pragma unroll
+        for (int j = 0; j < PER; j++)
+            if (tb + threadIdx.x + j * 1024 < pe) rank[j] = atomicAdd(&lh[f[j]], 1u);
         __syncthreads();
         tile_scan(lh, lofs, NF);
         __syncthreads();
@@ -438,6 +473,9 @@ __global__ __launch_bounds__(1024) void k_fine_sort(const uint32_t *ent, const u
             lh[q] = 0;
         }
         __syncthreads();
+#if !PNP_SORT_PREFETCH
+        if (pe - tb > (uint32_t)TILE_F) load_tile(tb + TILE_F);
+#endif
     }
 }
 
@@ -522,6 +560,32 @@ __global__ __launch_bounds__(1024) void k_fine_sort_runs(const uint64_t *rec, co
 __device__ __forceinline__ uint32_t bucket_start(const uint32_t *offs, uint64_t u, int nch) {
     return offs[u * nch];
 }
+// The bucket holding sorted entry k once bucket a starts at k (start(a) == k,
+// a < U): the last u >= a with start(u) <= k; `next` = start(u + 1).  Empty
+// buckets (start(u + 1) == start(u)) are skipped by a galloping search — one
+// load when bucket a is not empty, ~2 log2(run) for a run of empty ones.  The
+// one-by-one walk it replaces made a lane crossing a whole MSM with no entries
+// in a rank's bucket range (wire c over the padding rows: 65,536 empty buckets)
+// issue 65,536 dependent loads: 4.7 ms on rank 7 of an 8-rank proof.
+__device__ __forceinline__ uint64_t next_bucket(const uint32_t *offs, int nch, uint64_t U, uint64_t a, uint32_t k,
+                                                uint32_t &next) {
+    uint64_t lo = a, hi = a + 1, step = 1;
+    uint32_t vhi = bucket_start(offs, hi, nch);
+    while (vhi <= k) {  // start(U) = total > k: hi stays <= U
+        lo = hi;
+        step <<= 1;
+        hi = lo + step < U ? lo + step : U;
+        vhi = bucket_start(offs, hi, nch);
+    }
+    while (hi - lo > 1) {
+        const uint64_t m = (lo + hi) >> 1;
+        const uint32_t vm = bucket_start(offs, m, nch);
+        if (vm <= k) lo = m;
+        else hi = m, vhi = vm;
+    }
+    next = vhi;
+    return lo;
+}
 // The segment walk shared by the exact kernels; `ld(e)` yields the affine
 // point of sorted entry e (sign bit stripped by the caller).
 // The segment walk shared by the exact kernels; `ld(e)` yields the affine
@@ -551,10 +615,7 @@ __device__ __forceinline__ void segment32(uint64_t t, LoadPt ld, StorePt st, con
             else st(0, cur, acc);
             first = false;
             acc = Xyzz::inf();
-            do {  // skip empty buckets
-                cur++;
-                next = bucket_start(offs, cur + 1, nch);
-            } while (next == k);
+            cur = next_bucket(offs, nch, U, cur + 1, k, next);  // skips empty buckets
         }
         uint32_t e = sorted[k];
         Fq x, y;
@@ -716,10 +777,7 @@ __global__ __launch_bounds__(256, PNP_ACC_WAVES) void k_accumulate29(const uint3
             ok &= store29(first ? head + 56 * t : buckets + 56 * cur, acc);
             first = false;
             fresh = true;
-            do {
-                cur++;
-                next = offs[cur + 1];
-            } while (next == k);
+            cur = next_bucket(offs, 1, U, cur + 1, k, next);
         }
 #if PNP_ACC_GLDS
         F29 x, y;

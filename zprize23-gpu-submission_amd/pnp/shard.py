@@ -216,30 +216,66 @@ class SoloExchange(WindowExchange):
     TAG_DEVICE = 0xDE71CE00
     TAGS = (0xB0C4E7C0, 0x5EC7A111, 0x7F1A6500, 0xD1FC0001, 0xE7A15000, 0x57A7A500, 0xDE71CE00)
 
+    @property
+    def ordered(self) -> bool:
+        """Like the RCCL exchange: the loopback copies are enqueued on the
+        library's stream with no host synchronisation (PNP_EXCHANGE_SYNC=1:
+        synchronised, as the gloo exchange), so the solo time carries the host
+        round trips a real ordered rank pays and no others."""
+        import os
+        return self.buf.is_cuda and self.stream is not None and os.environ.get("PNP_EXCHANGE_SYNC") != "1"
+
+    def _done(self):
+        import torch
+        if not self.ordered:
+            torch.cuda.current_stream().synchronize()
+
+    def check_tags(self) -> None:
+        """Raise if an ordered gather saw an untagged slot (the ordered path
+        checks the tags on the device and cannot raise inside the callback)."""
+        if getattr(self, "_bad", None) is not None and int(self._bad.item()):
+            raise ValueError("untagged all-gather slot in an ordered loopback exchange")
+
     def gather(self, bytes_per_rank: int) -> None:
         import torch
         w = bytes_per_rank // 8
-        mine = self.buf[self.rank * w:(self.rank + 1) * w].clone()
-        tag = int(mine[-1]) & 0xFFFFFFFFFFFFFFFF
-        if tag not in self.TAGS:
-            raise ValueError(f"untagged all-gather slot ({bytes_per_rank} B, last word {tag:#x})")
-        if tag == self.TAG_T_FLAGS:
-            mine[6:8] = 0
-        slots = self.buf[: w * self.world].view(self.world, w)
-        slots.copy_(mine.expand(self.world, w))
-        if tag == self.TAG_COUNTS:
-            slots[:, self.rank] = mine[: self.world]
-        if tag == self.TAG_DEVICE:
-            slots[:, 0] += torch.arange(self.world, device=slots.device) - self.rank
-        torch.cuda.current_stream().synchronize()
+        with self._on_stream():
+            mine = self.buf[self.rank * w:(self.rank + 1) * w].clone()
+            slots = self.buf[: w * self.world].view(self.world, w)
+            if not self.ordered:
+                tag = int(mine[-1]) & 0xFFFFFFFFFFFFFFFF
+                if tag not in self.TAGS:
+                    raise ValueError(f"untagged all-gather slot ({bytes_per_rank} B, last word {tag:#x})")
+                if tag == self.TAG_T_FLAGS:
+                    mine[6:8] = 0
+                slots.copy_(mine.expand(self.world, w))
+                if tag == self.TAG_COUNTS:
+                    slots[:, self.rank] = mine[: self.world]
+                if tag == self.TAG_DEVICE:
+                    slots[:, 0] += torch.arange(self.world, device=slots.device) - self.rank
+            else:
+                # the same three cases, decided on the device (no host read)
+                tag = mine[-1]
+                if getattr(self, "_tags", None) is None:
+                    self._tags = torch.tensor(self.TAGS, dtype=torch.int64, device=mine.device)
+                    self._bad = torch.zeros((), dtype=torch.int64, device=mine.device)
+                self._bad |= (~torch.isin(tag, self._tags)).to(torch.int64)
+                if w >= 8:
+                    mine[6:8] = torch.where(tag == self.TAG_T_FLAGS, torch.zeros_like(mine[6:8]), mine[6:8])
+                slots.copy_(mine.expand(self.world, w))
+                if w > self.world:
+                    slots[:, self.rank] = torch.where(tag == self.TAG_COUNTS, mine[: self.world], slots[:, self.rank])
+                off = (torch.arange(self.world, device=slots.device) - self.rank) * (tag == self.TAG_DEVICE)
+                slots[:, 0] += off
+        self._done()
         self.calls += 1
         self.gather_bytes += bytes_per_rank * self.world
 
     def alltoall(self, bytes_per_peer: int) -> None:
-        import torch
         w = bytes_per_peer // 8
-        self.a2a[w * self.world: 2 * w * self.world].copy_(self.a2a[: w * self.world])
-        torch.cuda.current_stream().synchronize()
+        with self._on_stream():
+            self.a2a[w * self.world: 2 * w * self.world].copy_(self.a2a[: w * self.world])
+        self._done()
         self.a2a_calls += 1
         self.a2a_bytes_moved += bytes_per_peer * (self.world - 1)
 
@@ -247,14 +283,14 @@ class SoloExchange(WindowExchange):
         """Loopback: receive segment s = this rank's send segment s (the count
         exchange above made the sizes agree): distinct entries of this rank's
         points, bucket indices within a range, as many as a real rank gets."""
-        import torch
         self._count_dest(send_bytes)
         ss = [int(b) // 8 for b in send_bytes]
         rs = [int(b) // 8 for b in recv_bytes]
         assert rs == ss, (rs, ss)
         n = sum(ss)
-        self.vrecv[:n].copy_(self.vsend[:n])
-        torch.cuda.current_stream().synchronize()
+        with self._on_stream():
+            self.vrecv[:n].copy_(self.vsend[:n])
+        self._done()
         self.v_calls += 1
         self.v_bytes_moved += sum(send_bytes) - send_bytes[self.rank]
 
