@@ -669,7 +669,6 @@ def main():
                                    "(their xGMI time is not included; callback_ms is the host time "
                                    "spent inside the loopback callbacks; ordered: enqueued on the "
                                    "library stream without host syncs, as the RCCL exchange)"}
-            solo.check_tags()
         if not args.no_verify:
             chk = check_proof(syn, proof, args.circuit)
             out["verified"] = chk.pop("verified") and all_equal

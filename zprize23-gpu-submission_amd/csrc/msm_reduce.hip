@@ -138,7 +138,10 @@ void msm_merge_pieces(const uint32_t *offs, int nch, uint64_t U, uint32_t S, uin
 // pieces (clustered or repeated scalars, a short top window) is not summed
 // here, where one lane would add its pieces one after another, but queued
 // for k_merge_heavy29.
-constexpr uint32_t MERGE_HEAVY = 64;
+#ifndef PNP_MERGE_HEAVY
+#define PNP_MERGE_HEAVY 64
+#endif
+constexpr uint32_t MERGE_HEAVY = PNP_MERGE_HEAVY;
 __global__ __launch_bounds__(256) void k_merge_tails29(const uint32_t *offs, uint64_t U, uint32_t S, uint64_t nthr,
                                                        const uint32_t *tailb, uint32_t *bk29, const uint32_t *head,
                                                        const uint32_t *tail, uint32_t *exc, uint32_t *heavy,
