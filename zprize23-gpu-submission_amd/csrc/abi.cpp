@@ -380,7 +380,11 @@ hipStream_t pnp_ctx::side_stream() {
     if (!stream_lo) {
         int lo = 0, hi = 0;
         PNP_HIP(hipDeviceGetStreamPriorityRange(&lo, &hi));  // lo = least priority
-        PNP_HIP(hipStreamCreateWithPriority(&stream_lo, hipStreamNonBlocking, lo));
+        // PNP_SIDE_PRIORITY=hi: the side stream's transforms ahead of the main
+        // stream's MSM (experiments)
+        const char *pe = getenv("PNP_SIDE_PRIORITY");
+        const bool side_hi = pe && !strcmp(pe, "hi");
+        PNP_HIP(hipStreamCreateWithPriority(&stream_lo, hipStreamNonBlocking, side_hi ? hi : lo));
         for (hipEvent_t *e : {&ev_fork, &ev_w8, &ev_z8})
             PNP_HIP(hipEventCreateWithFlags(e, hipEventDisableTiming));
     }
