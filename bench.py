@@ -187,7 +187,7 @@ def mad_cycles():
     return 4.1  # DESIGN.md 4 (round 1 measurement)
 
 
-PMC_FILE = os.path.join(REPO, "profiles", "r03_accumulate_traffic.json")
+PMC_FILE = os.path.join(REPO, "profiles", "r04_accumulate_traffic.json")
 
 
 def pmc_traffic():

@@ -18,6 +18,7 @@
 #   traffic          FETCH_SIZE and WRITE_SIZE passes (two runs)
 #   solo[=R/W,...]   bench.py --solo for each R/W (default 0/2,0/4,0/8,7/8)
 #   ab=N:V1,V2,...   tools/abn.sh N rounds over the variants
+#   rehearse=N:LG    bench.py --gpus N at 2^LG, N gloo ranks sharing the GPU
 #   py=SCRIPT[+ARGS] python SCRIPT ARGS (a tool or test driver), 300 s limit
 set -o pipefail
 R=$(pwd)
@@ -62,6 +63,10 @@ run_step() {
     ab=*)
       local n=${arg%%:*} v=${arg#*:}
       bash tools/abn.sh "$n" $(echo "$v" | tr ',' ' ') > "$OUT/ab.txt" 2>&1 ;;
+    rehearse=*)
+      # bench.py's multi-rank path with N gloo ranks sharing the GPU (N:LG)
+      local rn=${arg%%:*} rl=${arg#*:}
+      bash tools/bench_rehearse.sh "$rn" "$rl" && cp gpurun_out/rehearse_n$rn.json gpurun_out/rehearse_n$rn.err "$OUT/" ;;
     py=*)
       timeout -k 10 300 python -u ${arg//+/ } > "$OUT/py_$(basename "${arg%%+*}").log" 2>&1 ;;
     *)
