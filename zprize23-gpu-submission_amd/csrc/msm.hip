@@ -310,11 +310,9 @@ __global__ __launch_bounds__(1024) void k_coarse_scatter(const uint32_t *keys, K
     // the tiles of every row in one sequence, so the next tile's keys (even
     // the next row's first) are loaded while this tile goes through its LDS
     // phases: the barriers wait for LDS only, not for loads in flight
-    const uint64_t ntile = hi > lo ? (hi - lo + TILE_K - 1) / TILE_K : 0, nt = ntile * kr.rows;
     uint32_t nxt[KPT];
-    auto load_tile = [&](uint64_t t, uint32_t *key) {
-        const uint32_t *k = kb + (t / ntile) * n;
-        const uint64_t tb = lo + (t % ntile) * TILE_K;
+    auto load_tile = [&](int r, uint64_t tb, uint32_t *key) {
+        const uint32_t *k = kb + (uint64_t)r * n;
         // KPT keys per lane, in groups of four consecutive points (16-byte loads)
 #pragma unroll
         for (int g = 0; g < KPT / 4; g++) {
@@ -328,10 +326,16 @@ __global__ __launch_bounds__(1024) void k_coarse_scatter(const uint32_t *keys, K
             }
         }
     };
-    if (nt) load_tile(0, nxt);
-    for (uint64_t t = 0; t < nt; t++) {
-        const int r = (int)(t / ntile);
-        const uint64_t tb = lo + (t % ntile) * TILE_K;
+    // tile (r, tb); the next one (nr, ntb) by stepping, row by row (no 64-bit
+    // division per tile)
+    int r = 0;
+    uint64_t tb = lo;
+    if (hi > lo && kr.rows > 0) load_tile(0, lo, nxt);
+    else r = kr.rows;
+    while (r < kr.rows) {
+        int nr = r;
+        uint64_t ntb = tb + TILE_K;
+        if (ntb >= hi) ntb = lo, nr++;
         const uint64_t so = v < kr.nseg ? kr.seg_off[v] : 0;
         const uint32_t idb = (uint32_t)((kr.id_row0 + r) * kr.id_mul + kr.id_base + so);
         {
@@ -339,7 +343,7 @@ __global__ __launch_bounds__(1024) void k_coarse_scatter(const uint32_t *keys, K
 #pragma unroll
             for (int j = 0; j < KPT; j++) key[j] = nxt[j];
 #if PNP_SORT_PREFETCH
-            if (t + 1 < nt) load_tile(t + 1, nxt);
+            if (nr < kr.rows) load_tile(nr, ntb, nxt);
 #endif
 #pragma unroll
             for (int j = 0; j < KPT; j++)
@@ -375,8 +379,9 @@ __global__ __launch_bounds__(1024) void k_coarse_scatter(const uint32_t *keys, K
             __syncthreads();
         }
 #if !PNP_SORT_PREFETCH
-        if (t + 1 < nt) load_tile(t + 1, nxt);
+        if (nr < kr.rows) load_tile(nr, ntb, nxt);
 #endif
+        r = nr, tb = ntb;
     }
 }
 
