@@ -188,6 +188,10 @@ def mad_cycles():
 
 
 PMC_FILE = os.path.join(REPO, "profiles", "r04_accumulate_traffic.json")
+def msm_windows(lg: int) -> int:
+    """folded windows of an MSM over 2^lg points (msm.hip msm_cfg; as pnp/shard.py v_bytes_for)"""
+    c = 20 if lg >= 19 else (lg - 3 if lg > 7 else 4)
+    return (256 + c - 1) // c
 
 
 def pmc_traffic():
@@ -631,7 +635,13 @@ def main():
                                  "frac": round(achieved / HBM_PEAK_GBS, 5),
                                  "algorithmic_bytes_per_launch": round(alg_per_launch),
                                  "basis": f"{ALG_BYTES_PER_ENTRY} B per sorted entry (one 96-B affine "
-                                          "point + its 4-B index) x real entries"},
+                                          "point + its 4-B index) x real entries",
+                                 # SURVEY 8(d)'s per-MSM figure: every point and scalar once,
+                                 # n (96 + 32) B; the folded table reads one 128-B line per
+                                 # (point, window) instead, trading bytes for the doublings
+                                 "survey_bytes_per_launch": round(dense / max(acc_n, 1) / msm_windows(args.lg) * 128),
+                                 "traffic_over_survey": (round(traffic / (dense / max(acc_n, 1) / msm_windows(args.lg) * 128), 2)
+                                                         if traffic and dense else None)},
                          "quotient": {"bound": "hbm", "achieved": round(q_gbs, 1),
                                       "peak": HBM_PEAK_GBS, "frac": round(q_gbs / HBM_PEAK_GBS, 4),
                                       "launch_ms": round(q_ms / max(q_n, 1), 3)}},
