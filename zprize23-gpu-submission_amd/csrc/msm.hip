@@ -880,15 +880,33 @@ __global__ __launch_bounds__(64) void k_accumulate_redo(const uint32_t *pts29, c
 }
 
 // ---------------------------------------------------------------- folded table
-// level k -> k+1: xyzz[i] = 2^c * (x, y)_i
+// level k -> k+1: xyzz[i] = 2^c * (x, y)_i.  The c doublings run in radix
+// 2^29 (ec29.cuh xdbl29, as the reduction tree's; the points of the prime-order
+// group have Y != 0) between one conversion in and one out: the same canonical
+// XYZZ as the 32-bit chain (PNP_TABLE_DBL29=0), 25.6 instead of 28.9 ms per
+// level of 2^22 points (profiles/r04_kernel_stats_table_dbl29.csv) — part of
+// the first proof after a key or SRS change.
+#ifndef PNP_TABLE_DBL29
+#define PNP_TABLE_DBL29 1
+#endif
 __global__ __launch_bounds__(256) void k_table_dbl(const uint64_t *src, uint64_t n, int c,
                                                    uint64_t *xyzz) {
     uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
     if (i >= n) return;
+#if PNP_TABLE_DBL29
+    Xyzz29 q;
+    q.x = from_fq32(load_fq(src + 12 * i));
+    q.y = from_fq32(load_fq(src + 12 * i + 6));
+    q.zz = q.zzz = const29(F29_ONE);
+#pragma unroll 1
+    for (int k = 0; k < c; k++) q = xdbl29(q);
+    store_xyzz(xyzz + 24 * i, to32(q));
+#else
     Xyzz q = dbl_affine(load_fq(src + 12 * i), load_fq(src + 12 * i + 6));
 #pragma unroll 1
     for (int k = 1; k < c; k++) q = dbl(q);
     store_xyzz(xyzz + 24 * i, q);
+#endif
 }
 // XYZZ -> affine for CH consecutive points per lane, one Fermat inversion per
 // lane (Montgomery's trick over ZZZ; 1/ZZ = (ZZ/ZZZ)^2).  Points of the prime
