@@ -209,8 +209,14 @@ def test_v1_reloads_mutated_key(monkeypatch):
     # the default compares the full-content hash of every array the load reads:
     # an unchanged key is not uploaded again (same proof), a changed word of a
     # zero selector's evaluations or of the SRS is seen
+    # (with both keys resident the call proves on them while the hash runs and
+    # proves again after the upload when the hash differs: the second call above
+    # and the SRS change below take that path; PNP_V1_NO_SPECULATE hashes first)
     again = lib.gen_proof(inp.circuit, inp.pk, inp.ck)
     assert abi.proof_to_bytes(again) == abi.proof_to_bytes(exp)
+    monkeypatch.setenv("PNP_V1_NO_SPECULATE", "1")
+    assert abi.proof_to_bytes(lib.gen_proof(inp.circuit, inp.pk, inp.ck)) == abi.proof_to_bytes(exp)
+    monkeypatch.delenv("PNP_V1_NO_SPECULATE")
     pts = inp.arrays["srs"]
     keep_pt = pts[7].copy()
     pts[7] = pts[9]  # a different curve point at index 7: every commitment moves
