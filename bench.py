@@ -677,8 +677,9 @@ def main():
                            "proof_sha256": __import__("hashlib").sha256(abi.proof_to_bytes(proof)).hexdigest(),
                            "note": "per-rank work of a W-GPU proof; the collectives are loopbacks "
                                    "(their xGMI time is not included; callback_ms is the host time "
-                                   "spent inside the loopback callbacks; ordered: enqueued on the "
-                                   "library stream without host syncs, as the RCCL exchange)"}
+                                   "spent inside the loopback callbacks — when ordered (enqueued on the "
+                                   "library stream without host syncs, as the RCCL exchange) it includes "
+                                   "the host waiting for queue space while it runs ahead of the GPU)"}
         if not args.no_verify:
             chk = check_proof(syn, proof, args.circuit)
             out["verified"] = chk.pop("verified") and all_equal
