@@ -188,6 +188,18 @@ def mad_cycles():
 
 
 PMC_FILE = os.path.join(REPO, "profiles", "r04_accumulate_traffic.json")
+def parallelism_label(world: int) -> str:
+    """what the multi-rank proof shards: the MSMs by bucket ranges from
+    PNP_MSM_BUCKETS_MIN_WORLD (4) ranks on, else by point ranges (msm.hip);
+    round 4 by coset blocks when the world size divides 8 (prover.cpp)"""
+    points = (os.environ.get("PNP_MSM_SHARD") == "points"
+              or world < int(os.environ.get("PNP_MSM_BUCKETS_MIN_WORLD", "4")))
+    label = f"msm-{'point' if points else 'bucket'}-range-shard"
+    if 8 % world == 0:
+        label += " + round4-block-shard"
+    return f"{label} x{world}"
+
+
 def msm_windows(lg: int) -> int:
     """folded windows of an MSM over 2^lg points (msm.hip msm_cfg; as pnp/shard.py v_bytes_for)"""
     c = 20 if lg >= 19 else (lg - 3 if lg > 7 else 4)
@@ -590,9 +602,7 @@ def main():
                                    + f" gen_proof: {gates} gates, domain 2^{args.lg}, "
                                    f"quotient on 2^{args.lg + 3} coset, pk+SRS+witness HBM-resident",
                        "circuit": args.circuit, "domain_log2": args.lg, "gates": gates,
-                       "parallelism": (f"msm-{'point' if os.environ.get('PNP_MSM_SHARD') == 'points' else 'bucket'}"
-                                       f"-range-shard + round4-block-shard x{world}"
-                                       if world > 1 else
+                       "parallelism": (parallelism_label(world) if world > 1 else
                                        f"solo rank {solo.rank} of {solo.world} (loopback exchanges, "
                                        f"proof discarded)" if solo else "single")},
             "timed_proofs_identical": all_equal,
