@@ -139,3 +139,37 @@ def test_device_srs_reload_keeps_derived_tables():
         assert abi.proof_to_bytes(ctx.prove(syn.cs, device_ptrs=True)) == ref
     finally:
         ctx.close()
+
+
+def test_deferred_tables_first_proof(monkeypatch):
+    """PNP_DEFER_TABLES=1: the context's first proof commits without the
+    optional tables (no Lagrange basis, no copy groups built: their plan bytes
+    stay), the second builds and uses them; all three proofs are the same bytes
+    as without the switch."""
+    import pnp
+    from pnp import abi
+    lg = 16
+    ctx = pnp.Context(0)
+    try:
+        syn = _instance(ctx, lg)
+        _load(ctx, syn)
+        ref = abi.proof_to_bytes(ctx.prove(syn.cs, device_ptrs=True))
+    finally:
+        ctx.close()
+    monkeypatch.setenv("PNP_DEFER_TABLES", "1")
+    ctx = pnp.Context(0)  # the switch is read when the context is made
+    try:
+        syn = _instance(ctx, lg)
+        _load(ctx, syn)
+        proofs, used, lag = [], [], []
+        for _ in range(3):
+            ctx.kernel_timing(True)
+            proofs.append(abi.proof_to_bytes(ctx.prove(syn.cs, device_ptrs=True)))
+            used.append(ctx.kernel_bytes("wire_groups_used"))
+            ctx.kernel_timing(False)
+            lag.append(ctx.hbm_usage()["lagrange"])
+        assert used == [0, 1, 1], used
+        assert lag[0] > 0 and lag[1] == 0 and lag[2] == 0, lag
+        assert proofs == [ref] * 3
+    finally:
+        ctx.close()

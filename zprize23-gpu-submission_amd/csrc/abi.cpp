@@ -115,6 +115,10 @@ const uint64_t *lagrange_table(pnp_ctx *ctx, uint64_t n) {
     if (!lagrange_enabled() || ctx->hbm_lag_off || n < 2 || (n & (n - 1)) || n > ctx->ck_points) return nullptr;
     uint64_t p0 = 0, p1 = n;
     if (!ctx->msm.full_table()) msm_point_range(n, ctx->msm.rank, ctx->msm.world, p0, p1);
+    // a deferring proof (PNP_DEFER_TABLES) uses the table only if it is there
+    if (ctx->defer_now &&
+        !(ctx->lag_n == n && ctx->lag_ok && ctx->lag_table_n == n && ctx->lag_table_p0 == p0 && ctx->lag_table_p1 == p1))
+        return nullptr;
     // (re)built on the same call on every rank (same key and call sequence):
     // a rank whose HBM could not hold it makes every rank go without
     bool built = false, fits = true;
@@ -420,6 +424,7 @@ int pnp_ctx_create(int device, pnp_ctx **out) {
     try {
         c->device = device;
         if (const char *e = getenv("PNP_FOLD_C")) c->msm.fold_c = atoi(e);  // experiments
+        if (const char *e = getenv("PNP_DEFER_TABLES")) c->defer_tables = atoi(e) != 0;
         PNP_HIP(hipSetDevice(device));
         PNP_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     } catch (const Error &e) {

@@ -97,6 +97,15 @@ struct pnp_ctx {
     // optional tables: the prover commits without them (same proof bytes)
     bool hbm_lag_off = false, hbm_groups_off = false;
     bool hbm_checked = false;  // the budget of the loaded keys has been checked (first proof)
+    // PNP_DEFER_TABLES=1: the context's first proof commits without the
+    // optional tables it would have to build first (Lagrange basis, copy
+    // groups: ~3.4 s at 2^22), the next proof builds them — for callers that
+    // prove once per process; same proof bytes either way.  Once per context,
+    // so a caller reloading its keys every call (PNP_V1_RELOAD) still gets the
+    // tables from its second proof on
+    bool defer_tables = false;
+    bool defer_now = false;  // this proof defers (set per proof)
+    uint64_t proofs_started = 0;
 
     // ---- per-proof working set (sized on first use, reused) ----
     std::map<std::string, pnp::DevBuf> work;

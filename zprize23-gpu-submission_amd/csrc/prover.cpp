@@ -159,6 +159,9 @@ int prove_impl(pnp_ctx *ctx, const CircuitC *cs, int device_ptrs, ProofC *out, c
             pi_val.push_back(v[k].second);
         }
     }
+    // the context's first proof may go without the optional tables (every
+    // rank: the same call sequence)
+    ctx->defer_now = ctx->defer_tables && ctx->proofs_started++ == 0;
     if (!ctx->hbm_checked) {  // the first proof after a key load: the HBM budget (every rank)
         hbm_budget(ctx);
         ctx->hbm_checked = true;

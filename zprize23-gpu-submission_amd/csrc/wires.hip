@@ -460,6 +460,7 @@ bool wire_bases_ready(pnp_ctx *ctx, uint64_t n) {
         if (same) wb.pk_gen = ctx->pk_gen;
         else wb.built = false;
     }
+    if ((!wb.built || wb.n != n) && ctx->defer_now) return false;  // PNP_DEFER_TABLES: next proof
     if (!wb.built || wb.n != n) {
         // built on the same call on every rank; a rank whose HBM cannot hold
         // the groups makes every rank commit without them
