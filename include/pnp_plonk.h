@@ -220,6 +220,13 @@ ProofC gen_proof(CircuitC circuit, ProverKeyC pk, CommitKeyC ck);
 #define PNP_E_NOMEM        -5   /* device allocation failed                 */
 
 typedef struct pnp_ctx pnp_ctx;
+/* The context the v1 symbol proves on (created by its first call; NULL
+ * before).  Its first proof goes without the optional tables (Lagrange basis,
+ * copy groups), which then build in the background (v2 pnp_prove likewise on
+ * one GPU; PNP_DEFER_TABLES=0 builds them inside the first proof instead,
+ * PNP_DEFER_BG=0 inside the second): pnp_sync(pnp_v1_context()) waits for
+ * that build, e.g. before timing a steady state.  Extension, diagnostics. */
+pnp_ctx *pnp_v1_context(void);
 
 /* Human-readable message of the last error on this thread. */
 const char *pnp_last_error(void);
@@ -327,7 +334,7 @@ typedef int (*pnp_allgather_fn)(void *user, uint64_t bytes_per_rank);
 #define PNP_EX_TAG_COUNTS    0xB0C4E7C0ULL  /* bucket-range MSMs: entry bytes per destination */
 #define PNP_EX_TAG_MSM_SUMS  0x5EC7A111ULL  /* point-range MSMs: B partial sums (XYZZ)       */
 #define PNP_EX_TAG_T_FLAGS   0x7F1A6500ULL  /* round 4: non-zero quotient chunks (8 words)   */
-#define PNP_EX_TAG_DIV_CARRY 0xD1FC0001ULL  /* split division by (X - z): slice values      */
+#define PNP_EX_TAG_DIV_CARRY 0xD1FC0001ULL  /* split divisions by (X - z): slice values   */
 #define PNP_EX_TAG_EVALS     0xE7A15000ULL  /* round 5: partial evaluations (18 x 4 words)  */
 #define PNP_EX_TAG_STATUS    0x57A7A500ULL  /* key load / derived tables: per-rank status   */
 #define PNP_EX_TAG_DEVICE    0xDE71CE00ULL  /* key load: which GPU each rank runs on        */

@@ -214,3 +214,13 @@ int or_num_threads(void) {
     return 1;
 #endif
 }
+
+/* the CPU baseline runs on every core the process may use,
+   whatever OMP_NUM_THREADS the environment inherited */
+void or_set_num_threads(int t) {
+#ifdef _OPENMP
+    if (t > 0) omp_set_num_threads(t);
+#else
+    (void)t;
+#endif
+}

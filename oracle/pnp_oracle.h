@@ -137,6 +137,7 @@ int or_synth_merkle(uint32_t height, const uint64_t *pc_mont, const uint64_t *le
 
 /* threads used by the OpenMP loops (for cpu_baseline.cores) */
 int or_num_threads(void);
+void or_set_num_threads(int t);
 
 #ifdef __cplusplus
 }

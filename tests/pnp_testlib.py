@@ -121,6 +121,7 @@ def oracle():
         lib.or_gen_proof.argtypes = [vp, vp, vp, vp]
         lib.or_gen_proof.restype = C.c_int
         lib.or_num_threads.restype = C.c_int
+        lib.or_set_num_threads.argtypes = [C.c_int]
         _ORACLE = lib
     return _ORACLE
 

@@ -149,6 +149,8 @@ def main():
         assert (ex.a2a_calls > 0) == (8 % world == 0)
         if os.environ.get("PNP_EXPECT_BUCKETS"):
             assert (ex.v_calls > 0) == (os.environ["PNP_EXPECT_BUCKETS"] == "1"), ex.v_calls
+        again = _prove_again(ctx, ex, lambda: ctx.prove(syn.cs, device_ptrs=True), proof)
+        say(f"second proof: {again}")
         with open(f"{out}.{rank}", "wb") as f:
             f.write(abi.proof_to_bytes(proof))
         ctx.close()
@@ -171,10 +173,32 @@ def main():
         # bucket ranges whenever the bucket count splits (not 3 ranks, not tiny MSMs)
         if os.environ.get("PNP_EXPECT_BUCKETS"):
             assert (ex.v_calls > 0) == (os.environ["PNP_EXPECT_BUCKETS"] == "1"), ex.v_calls
+        _prove_again(ctx, ex, lambda: ctx.prove(inp.circuit, device_ptrs=False), proof)
         with open(f"{out}.{rank}", "wb") as f:
             f.write(abi.proof_to_bytes(proof))
         ctx.close()
     dist.destroy_process_group()
+
+
+def _prove_again(ctx, ex, prove, first):
+    """A second proof on the same context must give the same bytes.  In
+    bucket-range mode it moves its records through the fixed-slot exchange
+    (capacities learned from the first proof, msm.hip msm_bucket_batch): every
+    batch slotted, none redone — unless PNP_TEST_SLOT_CAP shrinks the slots,
+    when every batch overflows, is redone on the variable path and the bytes
+    still match."""
+    from pnp import abi
+    ctx.kernel_timing(True)
+    proof = prove()
+    slotted, over = ctx.kernel_bytes("msm_slot_batches"), ctx.kernel_bytes("msm_slot_overflows")
+    ctx.kernel_timing(False)
+    assert abi.proof_to_bytes(proof) == abi.proof_to_bytes(first), "second proof differs"
+    if os.environ.get("PNP_EXPECT_BUCKETS") == "1":
+        if os.environ.get("PNP_TEST_SLOT_CAP"):
+            assert over > 0 and slotted == 0, (slotted, over)
+        else:
+            assert slotted > 0 and over == 0, (slotted, over)
+    return {"slotted": slotted, "overflows": over, "v_calls": ex.v_calls}
 
 
 if __name__ == "__main__":

@@ -43,6 +43,11 @@ def test_plan_bounds_the_first_proof(lg):
         _load(ctx, syn)
         u0 = ctx.hbm_usage()
         plan = u0["mandatory"] + u0["lagrange"] + u0["groups"] + u0["transient"]
+        # the first proof goes without the optional tables and starts their
+        # background build (context.h deferred tables); sync waits for it, the
+        # second proof uses them: the plan must cover the proof and the build
+        ctx.prove(syn.cs, device_ptrs=True)
+        ctx.sync()
         ctx.kernel_timing(True)
         ctx.prove(syn.cs, device_ptrs=True)
         used = ctx.kernel_bytes("wire_groups_used")
@@ -55,7 +60,7 @@ def test_plan_bounds_the_first_proof(lg):
         assert used == 1  # the groups were built and used, so the plan covered them
         assert grew <= plan, (grew, plan)
         assert plan <= 3 * grew + (256 << 20), (grew, plan)
-        # a second proof allocates nothing new
+        # a third proof allocates nothing new
         ctx.prove(syn.cs, device_ptrs=True)
         assert ctx.hbm_usage()["peak"] <= u1["live"] + (64 << 20)
     finally:
@@ -142,10 +147,67 @@ def test_device_srs_reload_keeps_derived_tables():
 
 
 def test_deferred_tables_first_proof(monkeypatch):
-    """PNP_DEFER_TABLES=1: the context's first proof commits without the
-    optional tables (no Lagrange basis, no copy groups built: their plan bytes
-    stay), the second builds and uses them; all three proofs are the same bytes
-    as without the switch."""
+    """Deferred tables (context.h, the default on one GPU): the context's
+    first proof commits without the optional tables (no Lagrange basis, no
+    copy groups) and starts their build in the background; a proof right
+    after it runs beside the build (and goes without them); pnp_commit_evals
+    between proofs waits for the basis (it used to fail with "no
+    Lagrange-basis key"); once the build is done the proofs use the tables.
+    Every proof is the bytes of a context that builds the tables up front
+    (PNP_DEFER_TABLES=0)."""
+    import torch
+    import pnp
+    from pnp import abi
+    lg = 16
+    monkeypatch.setenv("PNP_DEFER_TABLES", "0")
+    ctx = pnp.Context(0)  # the switch is read when the context is made
+    try:
+        syn = _instance(ctx, lg)
+        _load(ctx, syn)
+        ctx.kernel_timing(True)
+        ref = abi.proof_to_bytes(ctx.prove(syn.cs, device_ptrs=True))
+        assert ctx.kernel_bytes("wire_groups_used") == 1  # built by the first proof itself
+        ctx.kernel_timing(False)
+        ev = syn.keep["w_l"]
+        evals = torch.zeros((syn.n, 4), dtype=torch.int64, device="cuda")
+        evals[: ev.shape[0]] = ev
+        torch.cuda.synchronize()
+        c_ref = ctx.commit_evals(evals.data_ptr(), syn.n)
+    finally:
+        ctx.close()
+    monkeypatch.delenv("PNP_DEFER_TABLES")
+    ctx = pnp.Context(0)
+    try:
+        syn = _instance(ctx, lg)
+        _load(ctx, syn)
+        ctx.kernel_timing(True)
+        p1 = abi.proof_to_bytes(ctx.prove(syn.cs, device_ptrs=True))
+        assert ctx.kernel_bytes("wire_groups_used") == 0
+        ctx.kernel_timing(False)
+        p2 = abi.proof_to_bytes(ctx.prove(syn.cs, device_ptrs=True))  # beside the build (or after it)
+        ev = syn.keep["w_l"]
+        evals = torch.zeros((syn.n, 4), dtype=torch.int64, device="cuda")
+        evals[: ev.shape[0]] = ev
+        torch.cuda.synchronize()
+        c = ctx.commit_evals(evals.data_ptr(), syn.n)  # waits for the background basis
+        assert (bytes(c.x), bytes(c.y)) == (bytes(c_ref.x), bytes(c_ref.y))
+        ctx.sync()
+        lag = ctx.hbm_usage()["lagrange"]
+        ctx.kernel_timing(True)
+        p3 = abi.proof_to_bytes(ctx.prove(syn.cs, device_ptrs=True))
+        used = ctx.kernel_bytes("wire_groups_used")
+        ctx.kernel_timing(False)
+        assert lag == 0 and used == 1, (lag, used)
+        assert [p1, p2, p3] == [ref] * 3
+    finally:
+        ctx.close()
+
+
+def test_background_build_then_key_load():
+    """A key load while the background build runs waits for it (the build
+    reads the keys being replaced); an unchanged key keeps the tables, and the
+    proofs keep their bytes.  Destroying a context with a build in flight
+    stops it at its next kernel."""
     import pnp
     from pnp import abi
     lg = 16
@@ -153,23 +215,18 @@ def test_deferred_tables_first_proof(monkeypatch):
     try:
         syn = _instance(ctx, lg)
         _load(ctx, syn)
-        ref = abi.proof_to_bytes(ctx.prove(syn.cs, device_ptrs=True))
+        p1 = abi.proof_to_bytes(ctx.prove(syn.cs, device_ptrs=True))  # starts the build
+        _load(ctx, syn)                                                # waits for it
+        ctx.kernel_timing(True)
+        p2 = abi.proof_to_bytes(ctx.prove(syn.cs, device_ptrs=True))
+        used = ctx.kernel_bytes("wire_groups_used")
+        ctx.kernel_timing(False)
+        assert used == 1
+        assert p1 == p2
     finally:
         ctx.close()
-    monkeypatch.setenv("PNP_DEFER_TABLES", "1")
-    ctx = pnp.Context(0)  # the switch is read when the context is made
-    try:
-        syn = _instance(ctx, lg)
-        _load(ctx, syn)
-        proofs, used, lag = [], [], []
-        for _ in range(3):
-            ctx.kernel_timing(True)
-            proofs.append(abi.proof_to_bytes(ctx.prove(syn.cs, device_ptrs=True)))
-            used.append(ctx.kernel_bytes("wire_groups_used"))
-            ctx.kernel_timing(False)
-            lag.append(ctx.hbm_usage()["lagrange"])
-        assert used == [0, 1, 1], used
-        assert lag[0] > 0 and lag[1] == 0 and lag[2] == 0, lag
-        assert proofs == [ref] * 3
-    finally:
-        ctx.close()
+    ctx = pnp.Context(0)
+    syn = _instance(ctx, lg)
+    _load(ctx, syn)
+    assert abi.proof_to_bytes(ctx.prove(syn.cs, device_ptrs=True)) == p1  # starts a build
+    ctx.close()  # stops it

@@ -103,6 +103,24 @@ def test_sharded_gen_proof_parity(tmp_path, world, shard):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 4])
+def test_sharded_slot_overflow_redone(tmp_path, world):
+    """The fixed-slot bucket exchange with slots far too small
+    (PNP_TEST_SLOT_CAP=64 records): every batch of the second proof overflows,
+    every rank sees the overflow flag in the slot headers, redoes the batch on
+    the variable path, and the proof is still the oracle's."""
+    from pnp_testlib import Inputs
+    from pnp import abi
+    lg, seed = 13, 3
+    exp = abi.proof_to_bytes(Inputs(lg, seed).oracle_proof())
+    prefix = str(tmp_path / "proof")
+    _launch(world, ["gpu", prefix, str(lg), str(seed)], tmp_path, 600, PNP_TEST_MSM_SHARD="buckets",
+            PNP_EXPECT_BUCKETS="1", PNP_MSM_BUCKETS_MIN_WORLD="2", PNP_TEST_SLOT_CAP="64")
+    for r in range(world):
+        assert open(f"{prefix}.{r}", "rb").read() == exp, f"rank {r}"
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("golden,world,shard", [("full_2e22_seed1.json", 2, "buckets"),
                                                 ("full_2e22_seed1.json", 4, "buckets"),
                                                 ("full_2e22_seed1.json", 8, "buckets"),

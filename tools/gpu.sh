@@ -38,7 +38,9 @@ run_step() {
     smoke)
       timeout -k 10 180 python -u -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 ;;
     bench*)
-      timeout -k 10 900 python -u bench.py ${arg//+/ } > "$OUT/bench.json" 2> "$OUT/bench.err" ;;
+      # bench.json for the default arguments, bench_<args>.json otherwise
+      local bn=bench${arg:+_$(echo "$arg" | tr -c 'A-Za-z0-9' '_' | cut -c1-40)}
+      timeout -k 10 900 python -u bench.py ${arg//+/ } > "$OUT/$bn.json" 2> "$OUT/$bn.err" ;;
     stats*)
       (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d "$OUT/stats" -o run -- \
           python3 "$R/bench.py" --steps ${arg:-3} --warmup 1 --cpu-lg 0 --drop-in "" --no-verify > "$OUT/stats.log" 2>&1) ;;

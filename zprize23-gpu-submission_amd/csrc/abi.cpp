@@ -8,6 +8,8 @@
 #include <dlfcn.h>
 #include <array>
 #include <atomic>
+#include <mutex>
+#include <set>
 #include <thread>
 #include <stdarg.h>
 #include <stdlib.h>
@@ -103,6 +105,114 @@ bool all_ranks_ok(pnp_ctx *ctx, bool mine) {
     return true;
 }
 
+// ---- background table build (context.h pnp_ctx::bg) ----
+thread_local bool t_bg_build = false;
+static thread_local std::atomic<bool> *t_bg_cancel = nullptr;
+
+void bg_step(hipStream_t s) {
+    if (!t_bg_build) return;
+    PNP_HIP(hipStreamSynchronize(s));
+    if (t_bg_cancel && t_bg_cancel->load()) {
+        set_error("background table build cancelled");
+        throw Error(PNP_E_DEVICE);
+    }
+}
+
+hipStream_t tables_stream(pnp_ctx *ctx) { return t_bg_build ? ctx->bg_stream : ctx->stream; }
+
+// contexts whose builder may still run at process exit (the v1 symbol's
+// context is never destroyed): stopped and joined before the HIP runtime's
+// own exit handlers run (registered after them, so called first)
+static std::mutex g_bg_mu;
+static std::set<pnp_ctx *> g_bg_live;
+static void bg_atexit() {
+    std::vector<pnp_ctx *> live;
+    {
+        std::lock_guard<std::mutex> lk(g_bg_mu);
+        live.assign(g_bg_live.begin(), g_bg_live.end());
+    }
+    for (pnp_ctx *c : live) tables_cancel(c);
+}
+
+static void bg_build(pnp_ctx *ctx, uint64_t n) {
+    t_bg_build = true;
+    t_bg_cancel = &ctx->bg_cancel;
+    bool groups_started = false;
+    try {
+        PNP_HIP(hipSetDevice(ctx->device));
+        if (lagrange_table(ctx, n)) {
+            groups_started = true;
+            wire_bases_build(ctx, n);
+        }
+        PNP_HIP(hipStreamSynchronize(ctx->bg_stream));
+    } catch (...) {
+        // cancelled (a key load or the context's end) or failed: a half-built
+        // group set is dropped (the next deferring proof starts a new build,
+        // which resumes from the finished Lagrange parts); a failure leaves
+        // the proofs without what is not complete
+        (void)hipStreamSynchronize(ctx->bg_stream);
+        if (groups_started) wire_bases_reset(ctx);
+        if (!ctx->bg_cancel.load()) {
+            ctx->hbm_lag_off = !(ctx->lag_ok && ctx->lag_table_n == n);
+            ctx->hbm_groups_off = true;
+        }
+    }
+    ctx->bg_state.store(2, std::memory_order_release);
+}
+
+bool tables_bg_enabled() {
+    static const bool on = [] {
+        const char *e = getenv("PNP_DEFER_BG");
+        return !(e && atoi(e) == 0);
+    }();
+    return on;
+}
+
+void tables_start_background(pnp_ctx *ctx, uint64_t n) {
+    if (ctx->msm.world > 1 || ctx->bg.joinable() || !tables_bg_enabled()) return;
+    if (!ctx->bg_stream) {
+        int lo = 0, hi = 0;
+        PNP_HIP(hipDeviceGetStreamPriorityRange(&lo, &hi));
+        PNP_HIP(hipStreamCreateWithPriority(&ctx->bg_stream, hipStreamNonBlocking, lo));
+    }
+    // the builder reads what this proof's stream wrote (the key uploads)
+    PNP_HIP(hipStreamSynchronize(ctx->stream));
+    {
+        static std::once_flag once;
+        std::call_once(once, [] { atexit(bg_atexit); });
+        std::lock_guard<std::mutex> lk(g_bg_mu);
+        g_bg_live.insert(ctx);
+    }
+    ctx->bg_cancel.store(false);
+    ctx->bg_state.store(1, std::memory_order_release);
+    ctx->bg = std::thread(bg_build, ctx, n);
+}
+
+static void bg_join(pnp_ctx *ctx) {
+    if (ctx->bg.joinable()) ctx->bg.join();
+    ctx->bg_state.store(0);
+    std::lock_guard<std::mutex> lk(g_bg_mu);
+    g_bg_live.erase(ctx);
+}
+
+bool tables_busy(pnp_ctx *ctx) {
+    if (t_bg_build) return false;
+    const int st = ctx->bg_state.load(std::memory_order_acquire);
+    if (st == 2) bg_join(ctx);
+    return st == 1;
+}
+
+void tables_wait(pnp_ctx *ctx) {
+    if (!t_bg_build && ctx->bg.joinable()) bg_join(ctx);
+}
+
+void tables_cancel(pnp_ctx *ctx) {
+    if (t_bg_build || !ctx->bg.joinable()) return;
+    ctx->bg_cancel.store(true);
+    bg_join(ctx);
+    ctx->bg_cancel.store(false);
+}
+
 bool lagrange_enabled() {
     static const bool enabled = [] {
         const char *e = getenv("PNP_LAGRANGE");
@@ -113,12 +223,16 @@ bool lagrange_enabled() {
 
 const uint64_t *lagrange_table(pnp_ctx *ctx, uint64_t n) {
     if (!lagrange_enabled() || ctx->hbm_lag_off || n < 2 || (n & (n - 1)) || n > ctx->ck_points) return nullptr;
+    if (tables_busy(ctx)) return nullptr;  // being built in the background: commit without it
     uint64_t p0 = 0, p1 = n;
     if (!ctx->msm.full_table()) msm_point_range(n, ctx->msm.rank, ctx->msm.world, p0, p1);
-    // a deferring proof (PNP_DEFER_TABLES) uses the table only if it is there
-    if (ctx->defer_now &&
-        !(ctx->lag_n == n && ctx->lag_ok && ctx->lag_table_n == n && ctx->lag_table_p0 == p0 && ctx->lag_table_p1 == p1))
+    // a deferring proof uses the table only if it is there
+    if (ctx->defer_now && !t_bg_build &&
+        !(ctx->lag_n == n && ctx->lag_ok && ctx->lag_table_n == n && ctx->lag_table_p0 == p0 &&
+          ctx->lag_table_p1 == p1)) {
+        if (!(ctx->lag_n == n && !ctx->lag_ok)) ctx->tables_wanted = true;  // (not a degenerate key)
         return nullptr;
+    }
     // (re)built on the same call on every rank (same key and call sequence):
     // a rank whose HBM could not hold it makes every rank go without
     bool built = false, fits = true;
@@ -132,14 +246,15 @@ const uint64_t *lagrange_table(pnp_ctx *ctx, uint64_t n) {
             uint32_t lg = 0;
             while ((1ULL << lg) < n) lg++;
             ctx->lag_ok = srs_lagrange(ctx->ck_dev, n, inverse(root_of_unity(lg)), inverse(fr_from_u64(n)),
-                                       ctx->lag_points.u64(), ctx->stream);
+                                       ctx->lag_points.u64(), tables_stream(ctx));
             ctx->lag_n = n;
             if (!ctx->lag_ok) ctx->lag_points.release();
         }
         if (ctx->lag_ok && (ctx->lag_table_n != n || ctx->lag_table_p0 != p0 || ctx->lag_table_p1 != p1)) {
             built = true;
             ctx->lag_table_n = 0;
-            msm_build_table(ctx->lag_table, ctx->lag_points.u64() + 12 * p0, p1 - p0, ctx->msm.fold_c, ctx->stream);
+            msm_build_table(ctx->lag_table, ctx->lag_points.u64() + 12 * p0, p1 - p0, ctx->msm.fold_c,
+                            tables_stream(ctx));
             ctx->lag_table_n = n;
             ctx->lag_table_p0 = p0;
             ctx->lag_table_p1 = p1;
@@ -206,12 +321,13 @@ HbmPlan hbm_plan(pnp_ctx *ctx, uint64_t n) {
         const char *e = getenv("PNP_NTT29");
         return e && atoi(e) != 0;
     }();
-    const uint64_t ntt = 32 * n + 3 * 32 * N8 + (ntt29 ? 36 * n / 2 * 2 + 2 * 36 * N8 : 0);
+    const uint64_t ntt = 32 * n + 3 * 32 * N8 + (ntt29 ? 36 * n / 2 * 2 + 3 * 36 * N8 : 0);
     // (the 8n LDE twist of pnp_coset_lde8 is not a proof's: not counted as held)
     const uint64_t ntt_held = map_bytes(ctx->ntt.fwd) + map_bytes(ctx->ntt.inv) + map_bytes(ctx->ntt.blk_twist) +
                               map_bytes(ctx->ntt.blk_twist_inv) + map_bytes(ctx->ntt.fwd29) +
                               map_bytes(ctx->ntt.inv29) + map_bytes(ctx->ntt.blk_twist29) +
-                              map_bytes(ctx->ntt.blk_twist_inv29) + map_bytes(ctx->ntt.blk_twist32);
+                              map_bytes(ctx->ntt.blk_twist_inv29) + map_bytes(ctx->ntt.blk_twist32) +
+                              map_bytes(ctx->ntt.blk_twist32_29);
     const uint64_t ck_tab = msm_table_bytes(n_tab, n, wk.fold_c);
     const uint64_t msm = msm_work_bytes(per, n, wk.fold_c, 9, wk.v_bytes, world);
     const uint64_t held = work_held + ntt_held + ctx->ck_table.bytes + msm_work_held(wk);
@@ -279,28 +395,45 @@ void hbm_budget(pnp_ctx *ctx) {
     const uint64_t with_lag = p.mandatory + p.lag + std::max(p.t_mand, p.t_lag);
     const uint64_t with_groups = with_lag - std::max(p.t_mand, p.t_lag) + p.groups +
                                  std::max({p.t_mand, p.t_lag, p.t_groups});
-    uint64_t mine[5];
-    mine[0] = base <= budget;
+    // PNP_HBM_BUDGET=0: the mandatory part is an upper bound (up to ~3x the
+    // measured peak, test_gpu_hbm.py), so a caller that knows better lets the
+    // real allocations decide; the optional tables are still sized here
+    static const bool hard = [] {
+        const char *e = getenv("PNP_HBM_BUDGET");
+        return !(e && atoi(e) == 0);
+    }();
+    constexpr int K = 6;
+    uint64_t mine[K];
+    mine[0] = !hard || base <= budget;
     mine[1] = lagrange_enabled() && with_lag <= budget;
     mine[2] = mine[1] && wire_groups_enabled() && with_groups <= budget;
     mine[3] = base;
     mine[4] = budget;
-    std::vector<uint64_t> all(mine, mine + 5);
-    if (W > 1) all = rank_allgather(wk, ctx->stream, mine, 5, PNP_EX_TAG_STATUS);
-    bool ok = true, lag = true, groups = true;
+    // PNP_DEFER_TABLES is read per process: the ranks defer together or not
+    // at all (a deferring rank would skip the table builds' status exchange)
+    mine[5] = ctx->defer_tables;
+    std::vector<uint64_t> all(mine, mine + K);
+    if (W > 1) all = rank_allgather(wk, ctx->stream, mine, K, PNP_EX_TAG_STATUS);
+    bool ok = true, lag = true, groups = true, defer = true;
     int bad = -1;
     for (int r = 0; r < W; r++) {
-        if (!all[5 * r] && bad < 0) bad = r;
-        ok &= all[5 * r] != 0;
-        lag &= all[5 * r + 1] != 0;
-        groups &= all[5 * r + 2] != 0;
+        if (!all[K * r] && bad < 0) bad = r;
+        ok &= all[K * r] != 0;
+        lag &= all[K * r + 1] != 0;
+        groups &= all[K * r + 2] != 0;
+        defer &= all[K * r + 5] != 0;
     }
     ctx->hbm_lag_off = !lag;
     ctx->hbm_groups_off = !groups;
+    if (!defer) {
+        ctx->defer_tables = false;
+        ctx->defer_now = false;
+    }
     if (!ok) {
         set_error("HBM budget: rank %d of %d needs %.2f GiB more for a proof at n = %llu, %.2f GiB free to it "
-                  "(%llu rank(s) on this rank's GPU)", bad, W, all[5 * bad + 3] / 1073741824.0,
-                  (unsigned long long)ctx->pk_n, all[5 * bad + 4] / 1073741824.0, (unsigned long long)share);
+                  "(%llu rank(s) on this rank's GPU; PNP_HBM_BUDGET=0 lets the allocations decide)", bad, W,
+                  all[K * bad + 3] / 1073741824.0, (unsigned long long)ctx->pk_n, all[K * bad + 4] / 1073741824.0,
+                  (unsigned long long)share);
         throw Error(PNP_E_NOMEM);
     }
 }
@@ -424,7 +557,7 @@ int pnp_ctx_create(int device, pnp_ctx **out) {
     try {
         c->device = device;
         if (const char *e = getenv("PNP_FOLD_C")) c->msm.fold_c = atoi(e);  // experiments
-        if (const char *e = getenv("PNP_DEFER_TABLES")) c->defer_tables = atoi(e) != 0;
+        if (const char *e = getenv("PNP_DEFER_TABLES")) c->defer_tables = atoi(e) != 0 ? 1 : 0;
         PNP_HIP(hipSetDevice(device));
         PNP_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     } catch (const Error &e) {
@@ -437,6 +570,8 @@ int pnp_ctx_create(int device, pnp_ctx **out) {
 
 void pnp_ctx_destroy(pnp_ctx *ctx) {
     if (!ctx) return;
+    tables_cancel(ctx);
+    if (ctx->bg_stream) (void)hipStreamDestroy(ctx->bg_stream);
     (void)hipSetDevice(ctx->device);
     (void)hipStreamSynchronize(ctx->stream);
     if (ctx->msm.s2) {
@@ -469,6 +604,11 @@ int pnp_kernel_timing(pnp_ctx *ctx, int enable) {
 
 int pnp_kernel_stats(pnp_ctx *ctx, const char *name, double *total_ms, int *launches) {
     if (!ctx || !name) return PNP_E_ARG;
+    try {
+        ctx->ktimer.collect();  // operator calls leave their events pending
+    } catch (const Error &e) {
+        return e.code;
+    }
     auto it = ctx->ktimer.stats.find(name);
     if (total_ms) *total_ms = it == ctx->ktimer.stats.end() ? 0.0 : it->second.ms;
     if (launches) *launches = it == ctx->ktimer.stats.end() ? 0 : it->second.launches;
@@ -534,12 +674,24 @@ int pnp_ctx_stream(pnp_ctx *ctx, void **stream) {
 }
 
 int pnp_sync(pnp_ctx *ctx) {
-    PNP_TRY(PNP_HIP(hipStreamSynchronize(ctx->stream)));
+    if (!ctx) return PNP_E_ARG;
+    // (and the background table build: pnp_sync waits for all of the context's work)
+    PNP_TRY({
+        tables_wait(ctx);
+        PNP_HIP(hipStreamSynchronize(ctx->stream));
+    });
 }
 
 int pnp_ntt(pnp_ctx *ctx, uint64_t *d, uint32_t lg_n, int inverse, int coset) {
     if (!ctx || !d || lg_n > 28) return PNP_E_ARG;
-    PNP_TRY(ntt_run(ctx->ntt, d, lg_n, inverse != 0, coset != 0, ctx->stream));
+    // timed (pnp_kernel_timing): "ntt", credited 2 x 32 B per element (one
+    // read, one write: SURVEY 8(d)'s algorithmic bytes of a transform)
+    PNP_TRY({
+        hipEvent_t e0 = nullptr;
+        ctx->ktimer.begin("ntt", ctx->stream, e0);
+        ntt_run(ctx->ntt, d, lg_n, inverse != 0, coset != 0, ctx->stream);
+        ctx->ktimer.end("ntt", ctx->stream, e0, 64.0 * (double)(1ULL << lg_n));
+    });
 }
 
 int pnp_coset_lde8(pnp_ctx *ctx, const uint64_t *in, uint64_t *out8, uint32_t lg_n) {
@@ -570,11 +722,21 @@ int pnp_commit_ck(pnp_ctx *ctx, const uint64_t *d_scalars, uint64_t n, Commitmen
                   (unsigned long long)n);
         return PNP_E_ARG;
     }
-    PNP_TRY(commit_affine(ctx, d_scalars, n, out));
+    // timed (pnp_kernel_timing): "msm", the whole MSM (digits, sort,
+    // accumulation, bucket reduction, result), credited n (96 + 32) B (every
+    // point and scalar once); the folded table is built first
+    PNP_TRY({
+        commit_table(ctx, n);
+        hipEvent_t e0 = nullptr;
+        ctx->ktimer.begin("msm", ctx->stream, e0);
+        commit_affine(ctx, d_scalars, n, out);
+        ctx->ktimer.end("msm", ctx->stream, e0, 128.0 * (double)n);
+    });
 }
 
 int pnp_commit_evals(pnp_ctx *ctx, const uint64_t *d_evals, uint64_t n, CommitmentC *out) {
     if (!ctx || !out || !d_evals) return PNP_E_ARG;
+    tables_wait(ctx);  // (a background build of the Lagrange basis finishes first)
     if (!ctx->ck_loaded) {
         set_error("commit key not loaded");
         return PNP_E_NOKEY;
@@ -594,6 +756,7 @@ int pnp_commit_evals(pnp_ctx *ctx, const uint64_t *d_evals, uint64_t n, Commitme
 int pnp_hbm_usage(pnp_ctx *ctx, uint64_t out[6]) {
     if (!out) return PNP_E_ARG;
     PNP_TRY({
+        if (ctx) tables_wait(ctx);
         out[0] = g_dev_live.load();
         out[1] = g_dev_peak.exchange(out[0]);  // the peak since the previous call
         pnp::HbmPlan p;
@@ -745,6 +908,7 @@ extern "C" {
 int pnp_load_prover_key(pnp_ctx *ctx, const ProverKeyC *pk, uint64_t D, int device_ptrs) {
     if (!ctx || !pk || D == 0 || (D & (D - 1)) || D > (1ULL << 25)) return PNP_E_ARG;
     PNP_TRY({
+        tables_wait(ctx);  // a background build reads the key being replaced: let it finish
         PNP_HIP(hipSetDevice(ctx->device));
         ctx->pk_loaded = false;
         ctx->pk_gen++;  // derived groups (wires.hip) re-check sigma
@@ -960,6 +1124,7 @@ extern "C" {
 int pnp_load_commit_key(pnp_ctx *ctx, const CommitKeyC *ck, uint64_t n_points, int device_ptrs) {
     if (!ctx || !ck || !ck->powers_of_g || n_points == 0) return PNP_E_ARG;
     PNP_TRY({
+        tables_wait(ctx);  // a background build reads the SRS being replaced: let it finish
         PNP_HIP(hipSetDevice(ctx->device));
         ctx->ck_loaded = false;
         if (device_ptrs) {
@@ -1001,6 +1166,7 @@ int pnp_load_commit_key_strided(pnp_ctx *ctx, const void *points, uint64_t n_poi
         return PNP_E_ARG;
     }
     PNP_TRY({
+        tables_wait(ctx);
         PNP_HIP(hipSetDevice(ctx->device));
         ctx->ck_loaded = false;
         pnp::DevBuf raw;
@@ -1041,6 +1207,12 @@ int pnp_prove(pnp_ctx *ctx, const CircuitC *cs, int device_ptrs, ProofC *out) {
         return prove_impl(ctx, cs, device_ptrs, out);
     } catch (const Error &e) {
         return e.code;
+    } catch (const std::exception &e) {  // (bad_alloc, system_error: never across the C ABI)
+        set_error("exception: %s", e.what());
+        return PNP_E_DEVICE;
+    } catch (...) {
+        set_error("unknown exception");
+        return PNP_E_DEVICE;
     }
 }
 
@@ -1052,6 +1224,12 @@ int pnp_prove_ex(pnp_ctx *ctx, const CircuitC *cs, int device_ptrs, uint64_t n_p
         return prove_impl(ctx, cs, device_ptrs, out, &o);
     } catch (const Error &e) {
         return e.code;
+    } catch (const std::exception &e) {
+        set_error("exception: %s", e.what());
+        return PNP_E_DEVICE;
+    } catch (...) {
+        set_error("unknown exception");
+        return PNP_E_DEVICE;
     }
 }
 
@@ -1186,7 +1364,10 @@ std::vector<SegHash> hash_segments(const std::vector<Seg> &segs, unsigned cap = 
     if (cap) T = std::min(T, cap);
     T = (unsigned)std::min<size_t>(T, std::max<size_t>(1, jobs.size()));
     std::vector<std::thread> th;
-    for (unsigned t = 1; t < T; t++) th.emplace_back(work);
+    try {
+        for (unsigned t = 1; t < T; t++) th.emplace_back(work);
+    } catch (...) {  // a thread that could not start: the started ones finish the jobs
+    }
     work();
     for (auto &t : th) t.join();
     std::vector<SegHash> out(segs.size());
@@ -1242,8 +1423,11 @@ extern "C" {
 // v1: lib/hello.cu:4-6.  Same contract as the reference (structs by value,
 // synchronous, device 0, keys uploaded per call, print-and-exit on errors,
 // caffe/common.hpp:23-30); see the v1 keys note above for the switches.
+static pnp_ctx *g_v1_ctx = nullptr;  // the v1 symbol's context (pnp_v1_context)
+pnp_ctx *pnp_v1_context(void) { return g_v1_ctx; }
+
 ProofC gen_proof(CircuitC circuit, ProverKeyC pk, CommitKeyC ck) {
-    static pnp_ctx *ctx = nullptr;
+    pnp_ctx *&ctx = g_v1_ctx;
     static bool have_pk = false, have_ck = false;
     static std::array<uint64_t, 2> h_pk{}, h_ck{};
     auto env_on = [](const char *name) {  // read per call: a caller may switch modes
@@ -1283,7 +1467,13 @@ ProofC gen_proof(CircuitC circuit, ProverKeyC pk, CommitKeyC ck) {
                 hash_ok = false;
             }
         });
-        const int prc = pnp_prove(ctx, &circuit, 0, &out);
+        int prc;
+        try {  // (pnp_prove returns codes; the join must happen whatever it does)
+            prc = pnp_prove(ctx, &circuit, 0, &out);
+        } catch (...) {
+            hasher.join();
+            throw;
+        }
         hasher.join();
         if (hash_ok && hp == h_pk && hc == h_ck) {
             if (prc != PNP_OK) die(prc);

@@ -4,7 +4,9 @@
 #pragma once
 #include "pnp_internal.h"
 #include <array>
+#include <atomic>
 #include <memory>
+#include <thread>
 
 struct pnp_ctx {
     int device = 0;
@@ -97,15 +99,25 @@ struct pnp_ctx {
     // optional tables: the prover commits without them (same proof bytes)
     bool hbm_lag_off = false, hbm_groups_off = false;
     bool hbm_checked = false;  // the budget of the loaded keys has been checked (first proof)
-    // PNP_DEFER_TABLES=1: the context's first proof commits without the
+    // Deferred tables: the context's first proof commits without the
     // optional tables it would have to build first (Lagrange basis, copy
-    // groups: ~3.4 s at 2^22), the next proof builds them — for callers that
-    // prove once per process; same proof bytes either way.  Once per context,
-    // so a caller reloading its keys every call (PNP_V1_RELOAD) still gets the
-    // tables from its second proof on
-    bool defer_tables = false;
+    // groups: ~3.4 s at 2^22), so a caller that proves once per process pays
+    // its upload and proof only; same proof bytes either way.  On one GPU the
+    // tables are then built in the background (bg_*: a thread on a
+    // lowest-priority stream, one kernel in flight at a time) while the caller
+    // goes on, and the first proof after the build finished uses them; with
+    // several ranks the next proof builds them (the builds exchange status
+    // with the peers).  PNP_DEFER_TABLES=1 / 0 forces it on / off; default:
+    // on at world 1.  Once per context, so a caller reloading its keys every
+    // call (PNP_V1_RELOAD) still gets the tables from then on
+    int defer_tables = -1;   // -1: the default for the world size (resolved by the first proof)
     bool defer_now = false;  // this proof defers (set per proof)
+    bool tables_wanted = false;  // this deferring proof found a table missing
     uint64_t proofs_started = 0;
+    std::thread bg;
+    std::atomic<int> bg_state{0};  // 0 idle, 1 building, 2 finished (not yet joined)
+    std::atomic<bool> bg_cancel{false};
+    hipStream_t bg_stream = nullptr;
 
     // ---- per-proof working set (sized on first use, reused) ----
     std::map<std::string, pnp::DevBuf> work;
@@ -159,6 +171,24 @@ bool commit_wires_grouped(pnp_ctx *ctx, const uint64_t *const *d_evals, uint64_t
 bool commit_z_grouped(pnp_ctx *ctx, const uint64_t *d_z, uint64_t n, CommitmentC *out);
 // drop the wire groups (a new commit key or Lagrange basis)
 void wire_bases_reset(pnp_ctx *ctx);
+// build the copy-constraint groups now if they are enabled and missing
+// (wires.hip; the background table build)
+void wire_bases_build(pnp_ctx *ctx, uint64_t n);
+// ---- the background table build (abi.cpp; see pnp_ctx::bg) ----
+// start it after a deferring proof (world 1)
+void tables_start_background(pnp_ctx *ctx, uint64_t n);
+// PNP_DEFER_BG (default on): world-1 deferral builds in the background
+bool tables_bg_enabled();
+// true while it runs (joins it once it has finished); a proof then goes
+// without the tables.  Always false on the builder's own thread
+bool tables_busy(pnp_ctx *ctx);
+// wait for it (pnp_sync, key loads, operator calls that need the tables)
+void tables_wait(pnp_ctx *ctx);
+// stop it at its next kernel and wait (context destruction, process exit)
+void tables_cancel(pnp_ctx *ctx);
+// the stream the table builds run on: the background stream on the builder's
+// thread, else the context stream
+hipStream_t tables_stream(pnp_ctx *ctx);
 // B commitments over the resident SRS in one batched MSM
 // local: on a multi-GPU run the scalars hold only this rank's point range
 void commit_affine_batch(pnp_ctx *ctx, const uint64_t *const *d_scalars, int B, uint64_t n,

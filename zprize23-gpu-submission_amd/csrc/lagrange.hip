@@ -218,9 +218,11 @@ bool srs_lagrange(const uint64_t *d_aff, uint64_t n, const Fr &omega_inv, const 
     hipLaunchKernelGGL(k_lag_load, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, s, d_aff, n,
                        static_cast<uint32_t *>(P.p));
     PNP_HIP(hipGetLastError());
+    bg_step(s);
     hipLaunchKernelGGL(k_lag_powers, dim3((uint32_t)((n / 2 + 255) / 256)), dim3(256), 0, s, tw.u64(), n / 2,
                        omega_inv);
     PNP_HIP(hipGetLastError());
+    bg_step(s);
     // lanes: the whole layer when it fits 2^18 lanes (880 MB of window tables)
     const uint64_t lanes = std::min<uint64_t>(n / 2, 1ULL << 18);
     DevBuf scratch(lanes * LAG_TAB * LAG_PT * 4);
@@ -230,11 +232,13 @@ bool srs_lagrange(const uint64_t *d_aff, uint64_t n, const Fr &omega_inv, const 
                            static_cast<uint32_t *>(P.p), n, h, tw.u64(), (n / 2) / h, first ? n_inv : Fr::one(),
                            (int)first, static_cast<uint32_t *>(scratch.p), lanes, bad);
         PNP_HIP(hipGetLastError());
+        bg_step(s);
     }
     DevBuf X(n * 192);
     hipLaunchKernelGGL(k_lag_out, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, s,
                        static_cast<const uint32_t *>(P.p), n, lg, X.u64(), bad);
     PNP_HIP(hipGetLastError());
+    bg_step(s);
     xyzz_to_affine_dev(X.u64(), n, d_out, s);
     uint32_t hbad = 0;
     PNP_HIP(hipMemcpyAsync(&hbad, bad, 4, hipMemcpyDeviceToHost, s));

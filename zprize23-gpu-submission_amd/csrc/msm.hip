@@ -288,17 +288,29 @@ __device__ __forceinline__ void tile_scan(uint32_t *lh, uint32_t *lofs, int nb) 
 }
 
 // rec != nullptr: entries leave as 8-byte records entry | fine key << 32 (the
-// bucket-range exchange format) instead of the ent / fk arrays
+// bucket-range exchange format) instead of the ent / fk arrays.  slot_recs > 0
+// (fixed-slot exchange): destination d's records go to its slot, rec + d
+// slot_recs + hdr_recs, at most `cap` of them (the rest are dropped; the slot
+// header, k_slot_header, flags the overflow and the batch is redone)
 __global__ __launch_bounds__(1024) void k_coarse_scatter(const uint32_t *keys, KeyRows kr, int fb,
                                                          int NBc, uint64_t chunk, int nch,
                                                          const uint32_t *offs, uint32_t *ent,
-                                                         uint16_t *fk, int wmaj = 1, uint64_t *rec = nullptr) {
-    __shared__ uint32_t cur[1 << SORT_CB], lh[1 << SORT_CB], lofs[1 << SORT_CB];
+                                                         uint16_t *fk, int wmaj = 1, uint64_t *rec = nullptr,
+                                                         uint32_t slot_recs = 0, uint32_t hdr_recs = 0,
+                                                         uint32_t cap = 0) {
+    __shared__ uint32_t cur[1 << SORT_CB], lh[1 << SORT_CB], lofs[1 << SORT_CB], lim[1 << SORT_CB];
     __shared__ uint32_t st_e[TILE_K];
     __shared__ uint32_t st_m[TILE_K];
     const int v = blockIdx.y, ch = blockIdx.x;
     for (int b = threadIdx.x; b < NBc; b += blockDim.x) {
         cur[b] = offs[cidx(v, gridDim.y, b, NBc, wmaj, ch, nch)];
+        lim[b] = 0xFFFFFFFFu;
+        if (slot_recs) {  // slot-relative: minus the destination's first record
+            const uint32_t nbl = (uint32_t)NBc / wmaj, d = (uint32_t)b / nbl;
+            const uint32_t at = d * slot_recs + hdr_recs;
+            cur[b] = cur[b] - offs[cidx(0, gridDim.y, d * nbl, NBc, wmaj, 0, nch)] + at;
+            lim[b] = at + cap;
+        }
         lh[b] = 0;
     }
     __syncthreads();
@@ -365,7 +377,7 @@ __global__ __launch_bounds__(1024) void k_coarse_scatter(const uint32_t *keys, K
                 uint32_t mag = st_m[x], bn = mag >> fb;
                 uint32_t pos = cur[bn] + x - lofs[bn];
                 if (rec) {
-                    rec[pos] = st_e[x] | ((uint64_t)(mag & fmask) << 32);
+                    if (pos < lim[bn]) rec[pos] = st_e[x] | ((uint64_t)(mag & fmask) << 32);
                 } else {
                     ent[pos] = st_e[x];
                     fk[pos] = (uint16_t)(mag & fmask);
@@ -551,6 +563,103 @@ __global__ __launch_bounds__(1024) void k_fine_sort_runs(const uint64_t *rec, co
             }
             __syncthreads();
         }
+    }
+}
+
+// ---------------------------------------------------------------- 4b. fixed-slot exchange
+// Slot of destination d in the send buffer (8-byte units): a header of
+// hdr_recs records — u32 [0] magic, [1] this rank's record count for d, [2]
+// this rank overflowed SOME slot, [3] bins per destination, [4 + p] the count
+// of d's bin p (p < per_d: (MSM v, local coarse bin l) v-major) — then up to
+// cap records.  Every receiver sees every sender's overflow word, so all ranks
+// reach the same verdict on the batch without a host exchange.
+constexpr uint32_t SLOT_MAGIC = 0x5107CA90u;
+__host__ __device__ constexpr uint32_t slot_hdr_recs(uint32_t per_d) { return (4 + per_d + 1) / 2; }
+__global__ __launch_bounds__(256) void k_slot_header(const uint32_t *offs, uint32_t per_d, int nch, int W,
+                                                     uint32_t slot_recs, uint32_t cap, uint64_t *send,
+                                                     uint32_t *dest_counts) {
+    const uint32_t d = blockIdx.x;
+    auto bin_off = [&](uint64_t gbin) { return offs[gbin * nch]; };
+    uint32_t over = 0;
+    for (int e = 0; e < W; e++) over |= bin_off((uint64_t)(e + 1) * per_d) - bin_off((uint64_t)e * per_d) > cap;
+    uint32_t *h = reinterpret_cast<uint32_t *>(send + (uint64_t)d * slot_recs);
+    const uint64_t g0 = (uint64_t)d * per_d;
+    if (threadIdx.x == 0) {
+        h[0] = SLOT_MAGIC;
+        h[1] = bin_off(g0 + per_d) - bin_off(g0);
+        h[2] = over;
+        h[3] = per_d;
+        if (dest_counts) dest_counts[d] = h[1];
+    }
+    for (uint32_t p = threadIdx.x; p < per_d; p += blockDim.x) h[4 + p] = bin_off(g0 + p + 1) - bin_off(g0 + p);
+}
+
+// exclusive scan over the block (1024 lanes, one value each); returns the total
+__device__ uint32_t block_scan_1024(uint32_t x, uint32_t &excl, uint32_t *wsum) {
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    uint32_t inc = x;
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t y = __shfl_up(inc, off, 64);
+        if (lane >= off) inc += y;
+    }
+    if (lane == 63) wsum[wv] = inc;
+    __syncthreads();
+    uint32_t pre = 0, tot = 0;
+    for (int j = 0; j < 16; j++) {
+        pre += j < wv ? wsum[j] : 0;
+        tot += wsum[j];
+    }
+    excl = pre + inc - x;
+    __syncthreads();
+    return tot;
+}
+
+// Receiver: from the W slot headers, the run table of k_fine_sort_runs (bin p,
+// source r: {start in v_recv, length}), every bin's output start out0[p],
+// the total in out0[per_d] and bstart_end, and flags = {overflow or a bad
+// header, total}.  Lengths are clamped to the slot so an overflowed batch
+// (redone by the caller) never reads outside it.
+constexpr int SLOT_W_MAX = 64;  // ranks the fixed-slot path supports
+__global__ __launch_bounds__(1024) void k_slot_runs(const uint64_t *recv, int W, uint32_t slot_recs,
+                                                    uint32_t hdr_recs, uint32_t per_d, uint32_t cap, uint2 *runs,
+                                                    uint32_t *out0, uint32_t *bstart_end, uint32_t *flags) {
+    __shared__ uint32_t wsum[16];
+    __shared__ uint32_t rcarry[SLOT_W_MAX];  // records of source r in the bins already done
+    __shared__ uint32_t bad;
+    if (threadIdx.x == 0) bad = 0;
+    if (threadIdx.x < (uint32_t)W) rcarry[threadIdx.x] = 0;
+    __syncthreads();
+    if (threadIdx.x < (uint32_t)W) {
+        const uint32_t *h = reinterpret_cast<const uint32_t *>(recv + (uint64_t)threadIdx.x * slot_recs);
+        if (h[0] != SLOT_MAGIC || h[3] != per_d || h[2]) atomicOr(&bad, 1u);
+    }
+    __syncthreads();
+    uint32_t carry = 0;  // output records of the bins of earlier chunks
+    for (uint32_t p0 = 0; p0 < per_d; p0 += 1024) {
+        const uint32_t p = p0 + threadIdx.x;
+        uint32_t sum = 0;
+        for (int r = 0; r < W; r++) {
+            const uint32_t *h = reinterpret_cast<const uint32_t *>(recv + (uint64_t)r * slot_recs);
+            const uint32_t c = p < per_d ? h[4 + p] : 0;
+            uint32_t pre;
+            const uint32_t tot = block_scan_1024(c, pre, wsum);
+            const uint32_t st = rcarry[r] + pre;  // bin p's run within source r's records
+            const uint32_t len = st >= cap ? 0 : (c < cap - st ? c : cap - st);
+            if (p < per_d) runs[(uint64_t)p * W + r] = make_uint2((uint32_t)r * slot_recs + hdr_recs + st, len);
+            sum += len;
+            __syncthreads();  // every lane has read rcarry[r]
+            if (threadIdx.x == 0) rcarry[r] += tot;
+        }
+        uint32_t pre;
+        const uint32_t tot = block_scan_1024(sum, pre, wsum);
+        if (p < per_d) out0[p] = carry + pre;
+        carry += tot;
+    }
+    if (threadIdx.x == 0) {
+        out0[per_d] = carry;
+        bstart_end[0] = carry;
+        flags[0] = bad;
+        flags[1] = carry;
     }
 }
 
@@ -963,6 +1072,7 @@ void msm_build_table(DevBuf &tab, const uint64_t *d_points, uint64_t n, int c, h
     const dim3 nb((uint32_t)((n + 255) / 256));
     hipLaunchKernelGGL(k_table_to29, nb, dim3(256), 0, s, d_points, n, T29);
     PNP_HIP(hipGetLastError());
+    bg_step(s);
     if (g.W > 1) {
         DevBuf cur(n * 96), nxt(n * 96), xyzz(n * 192), pre(n * 48);
         const uint32_t CH = 64;
@@ -974,11 +1084,14 @@ void msm_build_table(DevBuf &tab, const uint64_t *d_points, uint64_t n, int c, h
             const int dbls = k == g.W - 1 ? g.c - g.top_sh : g.c;
             hipLaunchKernelGGL(k_table_dbl, nb, dim3(256), 0, s, src, n, dbls, xyzz.u64());
             PNP_HIP(hipGetLastError());
+            bg_step(s);
             hipLaunchKernelGGL(k_table_affine, dim3((uint32_t)((lanes + 255) / 256)), dim3(256), 0, s,
                                xyzz.u64(), n, CH, pre.u64(), nxt.u64());
             PNP_HIP(hipGetLastError());
+            bg_step(s);
             hipLaunchKernelGGL(k_table_to29, nb, dim3(256), 0, s, nxt.u64(), n, T29 + (uint64_t)k * n * PT29);
             PNP_HIP(hipGetLastError());
+            bg_step(s);
             std::swap(cur, nxt);
             src = cur.u64();
         }
@@ -1493,12 +1606,116 @@ static bool msm_bucket_batch(MsmWork &wk, const uint64_t *const *sc, int B, uint
         PNP_HIP(hipGetLastError());
     }
     scan_u32(counts, ncount + 1, gb.scan_tmp, s);
+    const uint64_t per_d = (uint64_t)B * nbl;
+    const uint64_t WB = (uint64_t)B * NBloc;
+    const uint64_t lo_w = (uint64_t)wk.rank * NBloc;  // weight offset of this rank's buckets
+    // this batch's slot capacity (the same key, and so the same capacity, on
+    // every rank: the ranks run the same batches in the same order)
+    static const bool slots_on = [] {
+        const char *e = getenv("PNP_MSM_SLOTS");
+        return !(e && atoi(e) == 0);
+    }();
+    if (wk.slot_cap.size() > 1024) wk.slot_cap.clear();  // (operator-API batches never repeat a key)
+    const auto key = std::make_tuple(wk.batch_seq++, B, n_full);
+    const uint32_t hdr = slot_hdr_recs((uint32_t)per_d);
+    auto cap_it = wk.slot_cap.find(key);
+    if (slots_on && W <= SLOT_W_MAX && cap_it != wk.slot_cap.end()) {
+        // ---- fixed slots: no host round trip before the accumulation
+        // (PNP_TEST_SLOT_CAP: a smaller capacity, to exercise the overflow path)
+        static const uint64_t test_cap = [] {
+            const char *e = getenv("PNP_TEST_SLOT_CAP");
+            return e ? strtoull(e, nullptr, 0) : 0ULL;
+        }();
+        const uint64_t cap = test_cap ? std::min(test_cap, cap_it->second) : cap_it->second;
+        const uint64_t slot_recs = hdr + cap;
+        // u32 layout of slot_dev: runs (2 per_d W) | out0 (per_d + 1) | flags (2) | dest counts (W)
+        const uint64_t nruns = 2 * per_d * W;
+        need(wk.slot_dev, (nruns + per_d + 1 + 2 + W) * 4);
+        uint32_t *rt = static_cast<uint32_t *>(wk.slot_dev.p), *o0 = rt + nruns, *flags = o0 + per_d + 1,
+                 *dcnt = flags + 2;
+        hipLaunchKernelGGL(k_slot_header, dim3((uint32_t)W), dim3(256), 0, s, counts, (uint32_t)per_d, nch, W,
+                           (uint32_t)slot_recs, (uint32_t)cap, wk.v_send, dcnt);
+        PNP_HIP(hipGetLastError());
+        if (n) {
+            hipLaunchKernelGGL(k_coarse_scatter, grid, dim3(1024), 0, s, keys, kr, fb, NBc, chunk, nch, counts,
+                               nullptr, nullptr, W, wk.v_send, (uint32_t)slot_recs, hdr, (uint32_t)cap);
+            PNP_HIP(hipGetLastError());
+        }
+        ex_fence(wk, s);
+        std::vector<uint64_t> eq(W, slot_recs * 8);
+        if (int rc = wk.alltoallv(wk.v_user, eq.data(), eq.data())) {
+            set_error("msm bucket shard: slot all-to-all failed (%d)", rc);
+            throw Error(PNP_E_DEVICE);
+        }
+        need(gb.offsets, (WB + 1) * 4);
+        need(gb.sorted, W * cap * 4 + 4);
+        uint32_t *bstart = static_cast<uint32_t *>(gb.offsets.p);
+        hipLaunchKernelGGL(k_slot_runs, dim3(1), dim3(1024), 0, s, wk.v_recv, W, (uint32_t)slot_recs, hdr,
+                           (uint32_t)per_d, (uint32_t)cap, reinterpret_cast<uint2 *>(rt), o0, bstart + WB, flags);
+        PNP_HIP(hipGetLastError());
+        hipLaunchKernelGGL(k_fine_sort_runs, dim3((uint32_t)per_d), dim3(1024), 0, s, wk.v_recv,
+                           reinterpret_cast<const uint2 *>(rt), W, o0, fb, bstart,
+                           static_cast<uint32_t *>(gb.sorted.p));
+        PNP_HIP(hipGetLastError());
+        MsmCfg gl = g;
+        gl.NB = (int)NBloc;
+        GroupPlan gp;
+        gp.kr = kr;
+        gp.nv = B;
+        // (the record count stays on the device: W cap bounds the lanes, the
+        // kernels read the true total from bstart[WB])
+        accumulate_group(wk, gb, gp, gl, nullptr, table, s, W * cap, (double)W * cap * 128.0 / g.W);
+        const uint64_t *res = reduce_group(gb, gp, gl, s, true);
+        std::vector<uint64_t> ts((size_t)B * 48);
+        uint32_t exc = 0, nredo = 0, fl[2] = {0, 0};
+        std::vector<uint32_t> dc(W);
+        PNP_HIP(hipMemcpyAsync(ts.data(), res, ts.size() * 8, hipMemcpyDeviceToHost, s));
+        PNP_HIP(hipMemcpyAsync(&exc, gb.exc.p, 4, hipMemcpyDeviceToHost, s));
+        PNP_HIP(hipMemcpyAsync(&nredo, gb.redo.p, 4, hipMemcpyDeviceToHost, s));
+        PNP_HIP(hipMemcpyAsync(fl, flags, 8, hipMemcpyDeviceToHost, s));
+        PNP_HIP(hipMemcpyAsync(dc.data(), dcnt, 4 * W, hipMemcpyDeviceToHost, s));
+        wctr_fetch(gb, s);
+        PNP_HIP(hipStreamSynchronize(s));
+        wk.slot_runs++;
+        if (fl[0]) {
+            // some rank overflowed some slot (every rank saw its flag): the
+            // variable path below redoes the batch and raises the capacity
+            gb.wctr_live = false;
+            wk.slot_overflows++;
+            if (wk.timer) {
+                wk.timer->credit("msm_slot_overflows", 1);
+                wk.timer->collect();
+            }
+        } else {
+            wctr_credit(wk, gb);
+            if (wk.timer) {
+                wk.timer->credit("msm_slot_batches", 1);
+                wk.timer->credit("msm_redo_lanes", (double)nredo);
+                uint64_t mx = 0, sum = 0;
+                for (uint32_t c : dc) mx = std::max<uint64_t>(mx, c), sum += c;
+                wk.timer->credit("msm_dest_max", (double)mx);
+                wk.timer->credit("msm_dest_sum", (double)sum);
+            }
+            if (exc) {
+                if (wk.timer) wk.timer->credit("msm_exact_fallback", 1);
+                res = reduce_group_exact(gb, gp, gl, s);
+                PNP_HIP(hipMemcpyAsync(ts.data(), res, ts.size() * 8, hipMemcpyDeviceToHost, s));
+                PNP_HIP(hipStreamSynchronize(s));
+            }
+            if (wk.timer) wk.timer->collect();
+            for (int b = 0; b < B; b++) {
+                const Xyzz T = get_xyzz(&ts[24 * (size_t)b]), S = get_xyzz(&ts[24 * ((size_t)B + b)]);
+                put_xyzz(lo_w ? add(T, mul_small(S, lo_w)) : T, part + 24 * (size_t)b);
+            }
+            return true;
+        }
+    }
+    // ---- variable sizes: the counts travel first (host round trips)
     std::vector<uint32_t> offs(ncount + 1);
     PNP_HIP(hipMemcpyAsync(offs.data(), counts, (ncount + 1) * 4, hipMemcpyDeviceToHost, s));
     PNP_HIP(hipStreamSynchronize(s));
     // per destination: its bins' entry counts (B nbl words, bin (v, local) of
     // destination d starts at offs[((d B + v) nbl + l) nch]) and its record bytes
-    const uint64_t per_d = (uint64_t)B * nbl;
     auto bin_off = [&](uint64_t gbin) { return offs[gbin * nch]; };
     std::vector<uint64_t> send_b(W), recv_b(W);
     for (int d = 0; d < W; d++) send_b[d] = 8ULL * (bin_off((d + 1) * per_d) - bin_off(d * per_d));
@@ -1520,10 +1737,30 @@ static bool msm_bucket_batch(MsmWork &wk, const uint64_t *const *sc, int B, uint
         if (wk.timer) wk.timer->credit("msm_bucket_fallback", 1);
         return false;
     }
-    for (int r = 0; r < W; r++) recv_b[r] = cnt(r, wk.rank);
-    // 4. bin counts (u32, B nbl per destination), then the records
     {
-        std::vector<uint32_t> bc((size_t)per_d * W);
+        // the slot capacity of this batch for the next proofs: the largest
+        // (source, destination) count of this run + 3% + 256 records (the
+        // balance over proofs of one circuit is within ~1%)
+        uint64_t mx = 0;
+        for (uint64_t v : all) mx = std::max<uint64_t>(mx, v / 8);
+        const uint64_t cap = ((mx + mx / 32 + 256) + 63) & ~63ULL;
+        if (W <= SLOT_W_MAX && (uint64_t)W * (hdr + cap) * 8 <= wk.v_bytes && cap < (1ULL << 31)) {
+            uint64_t &c = wk.slot_cap[key];
+            c = std::max(c, cap);
+        }
+        if (wk.timer) {
+            uint64_t smx = 0, sum = 0;
+            for (int d = 0; d < W; d++) smx = std::max<uint64_t>(smx, send_b[d] / 8), sum += send_b[d] / 8;
+            wk.timer->credit("msm_dest_max", (double)smx);
+            wk.timer->credit("msm_dest_sum", (double)sum);
+        }
+    }
+    for (int r = 0; r < W; r++) recv_b[r] = cnt(r, wk.rank);
+    // 4. bin counts (u32, B nbl per destination), then the records.  `bc`
+    // lives until the stream synchronisation below: in ordered mode nothing
+    // waits for its upload before then
+    std::vector<uint32_t> bc((size_t)per_d * W);
+    {
         for (uint64_t gbin = 0; gbin < per_d * W; gbin++) bc[gbin] = bin_off(gbin + 1) - bin_off(gbin);
         PNP_HIP(hipMemcpyAsync(wk.v_send, bc.data(), bc.size() * 4, hipMemcpyHostToDevice, s));
         ex_fence(wk, s);
@@ -1572,7 +1809,6 @@ static bool msm_bucket_batch(MsmWork &wk, const uint64_t *const *sc, int B, uint
         out0[per_d] = (uint32_t)o;
     }
     const uint64_t R = out0[per_d];
-    const uint64_t WB = (uint64_t)B * NBloc;
     need(gb.offsets, (WB + 1) * 4);
     need(gb.sorted, R * 4 + 4);
     need(gb.ent, (runs.size() + out0.size()) * 4);  // run table + bin starts (ent is unused on this path)
@@ -1611,10 +1847,9 @@ static bool msm_bucket_batch(MsmWork &wk, const uint64_t *const *sc, int B, uint
         }
         if (wk.timer) wk.timer->collect();
     }
-    const uint64_t lo = (uint64_t)wk.rank * NBloc;
     for (int b = 0; b < B; b++) {
         const Xyzz T = get_xyzz(&ts[24 * (size_t)b]), S = get_xyzz(&ts[24 * ((size_t)B + b)]);
-        put_xyzz(lo ? add(T, mul_small(S, lo)) : T, part + 24 * (size_t)b);
+        put_xyzz(lo_w ? add(T, mul_small(S, lo_w)) : T, part + 24 * (size_t)b);
     }
     return true;
 }
@@ -1669,6 +1904,7 @@ void msm_run_batch(MsmWork &wk, const uint64_t *d_points, const uint64_t *const 
         set_error("msm: point segments need a folded table and at most %d MSMs", MSM_BATCH_MAX);
         throw Error(PNP_E_ARG);
     }
+    if (wk.timer) wk.timer->credit("msm_scalar_bytes", 32.0 * (double)B * n / wk.world);  // (this rank's scalars)
     if (wk.world == 1) {
         if (segs)
             msm_local_batch(wk, nullptr, d_scalars, B, n, h_xyzz, s, table, segs->n_table, 0, segs->off, segs->c);

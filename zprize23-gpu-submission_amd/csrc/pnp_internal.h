@@ -5,6 +5,7 @@
 #include <stdio.h>
 #include <map>
 #include <string>
+#include <tuple>
 #include <vector>
 #include "field.cuh"
 #include "../../include/pnp_plonk.h"
@@ -61,8 +62,8 @@ struct NttTables {
     // the same twiddles / twists times 2^261 in radix 2^29 (9 u32 per entry)
     // for the radix-2^29 passes (fr29.cuh)
     std::map<uint32_t, DevBuf> fwd29, inv29, blk_twist29, blk_twist_inv29;
-    // the forward block twists times 32 (lde_blocks form29)
-    std::map<uint32_t, DevBuf> blk_twist32;
+    // the forward block twists times 32 (lde_blocks form29), and their 2^261 form
+    std::map<uint32_t, DevBuf> blk_twist32, blk_twist32_29;
 };
 const uint64_t *ntt_twiddles(NttTables &t, uint32_t lg, bool inverse, hipStream_t s);
 void ntt_prepare_coset(NttTables &t, hipStream_t s);
@@ -119,6 +120,14 @@ struct KernelTimer {
     }
 };
 
+// Background table builds (abi.cpp tables_start_background): on the builder's
+// thread every build kernel is followed by bg_step, which waits for it (one
+// build kernel in flight at a time, so a proof's streams never queue behind
+// more than one of them on a shared hardware queue) and stops the build when
+// it is cancelled.  A no-op on every other thread.
+extern thread_local bool t_bg_build;
+void bg_step(hipStream_t s);
+
 // ---- MSM (msm.hip) ----
 // buffers of one group of an MSM batch: counts (coarse-bin counts -> offsets,
 // scan_tmp), ent/fkey (pass-A entries and fine keys), offsets (bucket
@@ -173,6 +182,18 @@ struct MsmWork {
     // the folded table covers ALL n points (bucket ranges gather any point)
     bool full_table() const { return world > 1 && alltoallv != nullptr; }
     DevBuf part_counts, rec_counts;  // bucket-range pass counts
+    // Fixed-slot bucket exchange (msm.hip msm_bucket_batch): every rank sends
+    // every peer one slot of `cap` records with the bin counts in the slot's
+    // header, so the records move in one equal-size all-to-all with no host
+    // round trip to size it.  cap is per batch of a proof (its ordinal since
+    // the proof began, B, the table's n), set from the all-gathered counts of
+    // that batch's first variable-size run (the same on every rank); a batch
+    // whose counts outgrow it is redone on the variable path, which raises it.
+    // PNP_MSM_SLOTS=0: always the variable path.
+    std::map<std::tuple<uint32_t, int, uint64_t>, uint64_t> slot_cap;
+    uint32_t batch_seq = 0;  // bucket-range batches since the proof began
+    DevBuf slot_dev;         // run table, bin starts, flags, per-destination counts
+    unsigned long long slot_runs = 0, slot_overflows = 0;  // slotted batches / redone ones
 };
 // before an exchange callback: the data on the stream is complete
 inline void ex_fence(const MsmWork &wk, hipStream_t s) {

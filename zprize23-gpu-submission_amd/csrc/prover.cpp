@@ -78,29 +78,34 @@ std::vector<uint64_t> shard_allgather(pnp_ctx *ctx, const uint64_t *mine, int k,
     return rank_allgather(ctx->msm, ctx->stream, mine, k, tag);
 }
 
-// In place p <- p / (X - z) (kzg10.cu:87-99) where this rank holds the
-// coefficient range [a, a + len) of p.  Quotient coefficient
-// q_i = sum_(k > i) p_k z^(k-i-1) = (division of the local slice) +
-// z^(a+len-1-i) C with C = sum_(k >= a+len) p_k z^(k-a-len): every rank
-// shares the value E_r of its slice at z, C follows from the E of the ranks
-// above.
-void div_linear_range(pnp_ctx *ctx, uint64_t *d, uint64_t len, const Fr &z, bool dist) {
+// In place p_k <- p_k / (X - z_k) (kzg10.cu:87-99) for the K polynomials of
+// round 6, where this rank holds the coefficient range [a, a + len) of each.
+// Quotient coefficient q_i = sum_(k > i) p_k z^(k-i-1) = (division of the
+// local slice) + z^(a+len-1-i) C with C = sum_(k >= a+len) p_k z^(k-a-len):
+// every rank shares the value E_r of its slice at z, C follows from the E of
+// the ranks above — both polynomials' values in ONE all-gather.
+void div_linear_range(pnp_ctx *ctx, uint64_t *const *d, const Fr *z, int K, uint64_t len, bool dist) {
     hipStream_t s = ctx->stream;
     if (!dist) {
-        k_poly_div_linear(d, len, z, ctx->scratch_a, s);
+        for (int k = 0; k < K; k++) k_poly_div_linear(d[k], len, z[k], ctx->scratch_a, s);
         return;
     }
     const int world = ctx->msm.world, rank = ctx->msm.rank;
-    Fr e;
-    k_poly_eval(d, len, z, ctx->scratch_a, &e, s);
-    uint64_t mine[4];
-    to_u64_limbs(e, mine);
-    std::vector<uint64_t> all = shard_allgather(ctx, mine, 4, PNP_EX_TAG_DIV_CARRY);
+    std::vector<uint64_t> mine(4 * K);
+    for (int k = 0; k < K; k++) {
+        Fr e;
+        k_poly_eval(d[k], len, z[k], ctx->scratch_a, &e, s);
+        to_u64_limbs(e, &mine[4 * k]);
+    }
+    std::vector<uint64_t> all = shard_allgather(ctx, mine.data(), 4 * K, PNP_EX_TAG_DIV_CARRY);
     const uint64_t n = len * world;  // equal ranges (world divides 8 and n)
-    Fr c = Fr::zero();
-    for (int r = world - 1; r > rank; r--) c = c * pow_u64(z, n / world) + from_u64_limbs<FrP>(&all[4 * r]);
-    k_poly_div_linear(d, len, z, ctx->scratch_a, s);
-    if (rank < world - 1) k_add_powers(d, len, c, z, s);
+    for (int k = 0; k < K; k++) {
+        Fr c = Fr::zero();
+        const Fr zl = pow_u64(z[k], n / world);
+        for (int r = world - 1; r > rank; r--) c = c * zl + from_u64_limbs<FrP>(&all[4 * (K * r + k)]);
+        k_poly_div_linear(d[k], len, z[k], ctx->scratch_a, s);
+        if (rank < world - 1) k_add_powers(d[k], len, c, z[k], s);
+    }
 }
 
 }  // namespace
@@ -159,17 +164,35 @@ int prove_impl(pnp_ctx *ctx, const CircuitC *cs, int device_ptrs, ProofC *out, c
             pi_val.push_back(v[k].second);
         }
     }
-    // the context's first proof may go without the optional tables (every
-    // rank: the same call sequence)
-    ctx->defer_now = ctx->defer_tables && ctx->proofs_started++ == 0;
+    // Deferred tables (context.h): a proof that finds the optional tables
+    // missing goes without them.  One GPU: on by default, the tables are only
+    // built in the background, started when such a proof returns; several
+    // ranks: off by default, the context's first proof only (every rank: the
+    // same call sequence; hbm_budget checks the ranks agree)
+    if (ctx->defer_tables < 0) ctx->defer_tables = ctx->msm.world <= 1 ? 1 : 0;
+    const bool bg_mode = ctx->msm.world <= 1 && tables_bg_enabled();
+    ctx->defer_now = ctx->defer_tables == 1 && (bg_mode || ctx->proofs_started == 0);
+    ctx->proofs_started++;
+    ctx->tables_wanted = false;
+    struct DeferScope {  // the deferral is this proof's only, on every exit
+        pnp_ctx *c;
+        ~DeferScope() { c->defer_now = false; }
+    } defer_scope{ctx};
     if (!ctx->hbm_checked) {  // the first proof after a key load: the HBM budget (every rank)
         hbm_budget(ctx);
         ctx->hbm_checked = true;
     }
+    ctx->msm.batch_seq = 0;  // the fixed-slot exchange keys its capacities by batch ordinal
     const uint64_t N8 = 8 * n, ng = cs->n;
     const ProverKeyC &pk = ctx->pk_dev;
     Timer tm(ctx);
     auto &nt = ctx->ntt;
+    // The proof's algorithmic HBM bytes (the whole-proof GB/s
+    // beside the wall-clock): every op below credits its minimal reads and
+    // writes in Fr elements (32 B); the MSMs credit their scalars and the
+    // accumulation its device-counted entries in msm.hip (bench.py adds them
+    // up; DESIGN.md 5 states the tally)
+    auto alg = [&](double elems) { ctx->ktimer.credit("proof_alg_bytes", 32.0 * elems); };
     k_proof_marker(s);
     // the twiddle / twist tables are built lazily; build them here, on the main
     // stream, so the side-stream LDEs (after fork()) and the main-stream LDEs
@@ -238,6 +261,7 @@ int prove_impl(pnp_ctx *ctx, const CircuitC *cs, int device_ptrs, ProofC *out, c
     }
     uint64_t *qlk = ctx->buf("qlk", n);
     PNP_HIP(hipMemcpyAsync(qlk, cs->q_lookup, 32 * ng, kind, s));
+    alg(4.0 * (2 * ng + (n - ng)) + 2.0 * ng);
     tm.mark("inputs");
 
     Transcript tr(opt ? opt->label : "Merkle tree");
@@ -264,13 +288,16 @@ int prove_impl(pnp_ctx *ctx, const CircuitC *cs, int device_ptrs, ProofC *out, c
         for (int j = 0; j < 4; j++) ntt_run(nt, wpoly[j], lg, true, false, s_lo, wsc[j]);
         for (int j = 0; j < 4; j++) lde_on(s_lo, wpoly[j], w8buf[j], q29);
         if (overlap) PNP_HIP(hipEventRecord(ctx->ev_w8, s_lo));
+        alg(4.0 * 2 * n + 4.0 * (1 + nbq) * n);  // 4 iNTTs, 4 LDEs onto nbq blocks
         tm.mark("r1_intt");
         // over the copy-constraint groups when the key has them and the
         // witness keeps them (wires.hip), else row by row
         const uint64_t *sc[4] = {wsc[0], wsc[1], wsc[2], wsc[3]};
-        if (!commit_wires_grouped(ctx, sc, n, wc)) commit_evals_batch(ctx, sc, 4, n, wc);
+        if (commit_wires_grouped(ctx, sc, n, wc)) alg(4.0 * n * 72 / 32);  // row, group, representative
+        else commit_evals_batch(ctx, sc, 4, n, wc);
     } else {
         for (int j = 0; j < 4; j++) ntt_run(nt, wpoly[j], lg, true, false, s, wsc[j]);
+        alg(4.0 * 2 * n + 4.0 * (1 + nbq) * n);
         tm.mark("r1_intt");
         fork();
         for (int j = 0; j < 4; j++) lde_on(s_lo, wpoly[j], w8buf[j], q29);
@@ -294,6 +321,7 @@ int prove_impl(pnp_ctx *ctx, const CircuitC *cs, int device_ptrs, ProofC *out, c
     const uint64_t *wconst[4] = {wsc[0], wsc[1], wsc[2], wsc[3]};
     k_query_f(fc, qlk, ng, wconst, tc, zeta, n, s);
     const bool f_zero = !k_any_nonzero(fc, 4 * n, ctx->scratch_b, s);
+    alg(5.0 * n + n + ng + n + n);  // compress, its check, query (q_lookup in, f out), its check
     // (zero f / table: their polynomials are never read)
     if (!table_zero) ntt_run(nt, table_poly, lg, true, false, s, tc);
     if (!f_zero) ntt_run(nt, f_poly, lg, true, false, s, fc);
@@ -317,6 +345,7 @@ int prove_impl(pnp_ctx *ctx, const CircuitC *cs, int device_ptrs, ProofC *out, c
         if (h_zero) {
             PNP_HIP(hipMemsetAsync(h1, 0, 32 * n, s));
             PNP_HIP(hipMemsetAsync(h2, 0, 32 * n, s));
+            alg(2.0 * n);
             set_infinity(&out->h_1_comm);
             set_infinity(&out->h_2_comm);
         } else {
@@ -371,6 +400,8 @@ int prove_impl(pnp_ctx *ctx, const CircuitC *cs, int device_ptrs, ProofC *out, c
     k_batch_inverse(den, n, ctx->scratch_a, s);
     k_mul_inplace(num, den, n, s);
     k_prefix_product(num, n, ctx->scratch_a, s);
+    alg(10.0 * n + 2.0 * n + 3.0 * n + 2.0 * n);  // numerators / denominators, inverse, product, scan
+    alg(2.0 * n + (1.0 + nbq) * n);               // z's iNTT and LDE
     uint64_t *z8 = ctx->buf("z8", NB);
     if (lag) {  // z from its evaluations; its iNTT joins its LDE on the side stream
         fork();
@@ -382,7 +413,8 @@ int prove_impl(pnp_ctx *ctx, const CircuitC *cs, int device_ptrs, ProofC *out, c
         CommitmentC *oc[1] = {&out->z_comm};
         // z is constant over runs of rows sigma fixes (the padding): one
         // scalar per run (wires.hip), else row by row
-        if (!commit_z_grouped(ctx, num, n, &out->z_comm)) commit_evals_batch(ctx, sc, 1, n, oc);
+        if (commit_z_grouped(ctx, num, n, &out->z_comm)) alg(1.0 * n * 72 / 32);
+        else commit_evals_batch(ctx, sc, 1, n, oc);
     } else {
         ntt_run(nt, z_poly, lg, true, false, s, num);
         tm.mark("r3_z");
@@ -630,6 +662,7 @@ int prove_impl(pnp_ctx *ctx, const CircuitC *cs, int device_ptrs, ProofC *out, c
             int nread = 0;
             for (const uint64_t *a : arrs) nread += a != nullptr;
             ctx->ktimer.end("quotient", s, qe0, 32.0 * (double)NBq * (nread + 1));
+            alg((double)NBq * (nread + 1));
         }
         tm.mark("r4_quotient");
         ctx->ktimer.collect();
@@ -640,6 +673,7 @@ int prove_impl(pnp_ctx *ctx, const CircuitC *cs, int device_ptrs, ProofC *out, c
         // this rank's coefficient range [q0, q0 + len): t_poly[k len + u]; with
         // nbq < 8 blocks the chunks from t_(nbq+1) on are zero
         intt_blocks(nt, t_blk, lg, mb0, nbq, s);
+        alg(2.0 * NBq + 2.0 * NBq);  // the block iNTTs and the combine
         uint64_t *t_poly = ctx->buf("t_poly", 8 * len);
         const int npieces = dist ? 8 : nbq;
         unsigned *t_nz = reinterpret_cast<unsigned *>(ctx->buf("t_nz", 1));  // bit k: chunk k != 0
@@ -751,6 +785,7 @@ int prove_impl(pnp_ctx *ctx, const CircuitC *cs, int device_ptrs, ProofC *out, c
             const uint64_t *pw[4] = {z_poly + eo, wpoly[0] + eo, wpoly[1] + eo, wpoly[3] + eo};
             Fr rw[4];
             k_poly_eval_multi(pw, 4, len, zw, ctx->scratch_a, rw, s);
+            alg(18.0 * len);
             if (dist) {
                 Fr *vals[18];
                 for (int k = 0; k < 12; k++) vals[k] = &rz[k];
@@ -890,6 +925,7 @@ int prove_impl(pnp_ctx *ctx, const CircuitC *cs, int device_ptrs, ProofC *out, c
         }
         uint64_t *lin = ctx->buf("lin", len);
         k_lincomb(la, len, lin, s);
+        alg((la.k + 1.0) * len);
         if (!dist && nbq < 8) {
             // the verifier's equation (proof.rs:433-494, oracle/verifier.c): for the
             // true quotient lin(z) = -r_0; otherwise the witness does not satisfy
@@ -979,7 +1015,7 @@ int prove_impl(pnp_ctx *ctx, const CircuitC *cs, int device_ptrs, ProofC *out, c
                 p = p * aw;
             }
             k_lincomb(oa, len, comb, s);
-            div_linear_range(ctx, comb, len, zc, dist);
+            alg((oa.k + 1.0) * len);
         }
         {
             const uint64_t *sawp[7] = {z_poly, wpoly[0], wpoly[1], wpoly[3], h1_poly, z2_poly, table_poly};
@@ -996,7 +1032,12 @@ int prove_impl(pnp_ctx *ctx, const CircuitC *cs, int device_ptrs, ProofC *out, c
                 p = p * saw;
             }
             k_lincomb(oa, len, comb2, s);
-            div_linear_range(ctx, comb2, len, zw, dist);
+            alg((oa.k + 1.0) * len + 4.0 * len);  // + both divisions
+        }
+        {
+            uint64_t *dd[2] = {comb, comb2};
+            const Fr zz[2] = {zc, zw};
+            div_linear_range(ctx, dd, zz, 2, len, dist);
         }
         tm.mark("r6_witness");
         {
@@ -1007,6 +1048,8 @@ int prove_impl(pnp_ctx *ctx, const CircuitC *cs, int device_ptrs, ProofC *out, c
         tm.mark("r6_commit");
         break;
     }
+    // the tables this proof went without: built in the background from now
+    if (bg_mode && ctx->defer_now && ctx->tables_wanted) tables_start_background(ctx, n);
     return PNP_OK;
 }
 

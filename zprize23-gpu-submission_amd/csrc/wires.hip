@@ -161,21 +161,58 @@ __global__ __launch_bounds__(256) void k_wb_chunks(const uint64_t *L, const uint
 }
 
 // level 2: group g = the pieces ending at the chunk boundaries inside its run
-// and at its last position; *bad when a base is infinity (a degenerate key)
+// and at its last position; *bad when a base is infinity (a degenerate key).
+// A group of more than WB_HEAVY pieces (z's run over the 1M padding rows of
+// the HEIGHT = 15 circuit: 32K pieces, 0.68 s in one lane) is queued in
+// heavy[1..] instead and summed by a whole workgroup (k_wb_final_heavy)
+constexpr uint64_t WB_HEAVY = 256;
+__device__ __forceinline__ uint64_t wb_piece_end(uint64_t t0, uint64_t t1, uint32_t C, uint64_t k) {
+    const uint64_t e = (t0 / C + 1 + k) * C;
+    return (e < t1 ? e : t1) - 1;  // last position of piece k
+}
 __global__ __launch_bounds__(256) void k_wb_final(const uint64_t *part, const uint32_t *gstart, uint64_t g_cnt,
-                                                  uint64_t n, uint32_t C, uint64_t *out, uint32_t *bad) {
+                                                  uint64_t n, uint32_t C, uint64_t *out, uint32_t *bad,
+                                                  uint32_t *heavy) {
     const uint64_t g = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
     if (g >= g_cnt) return;
     const uint64_t t0 = gstart[g], t1 = g + 1 < g_cnt ? gstart[g + 1] : n;
+    const uint64_t np = (t1 - 1) / C - t0 / C + 1;  // pieces of the run
+    if (np > WB_HEAVY) {
+        heavy[1 + atomicAdd(heavy, 1u)] = (uint32_t)g;
+        return;
+    }
     Xyzz acc = Xyzz::inf();
 #pragma unroll 1
-    for (uint64_t e = (t0 / C + 1) * C; ; e += C) {
-        const uint64_t last = (e < t1 ? e : t1) - 1;
-        acc = add(acc, load_xyzz(part + 24 * last));
-        if (e >= t1) break;
-    }
+    for (uint64_t k = 0; k < np; k++) acc = add(acc, load_xyzz(part + 24 * wb_piece_end(t0, t1, C, k)));
     if (acc.is_inf()) atomicOr(bad, 1u);
     store_xyzz(out + 24 * (uint64_t)wb_slot(g, g_cnt, n), acc);
+}
+// the queued heavy groups, one workgroup each (strided partial sums, then a
+// tree in LDS); the grid strides over the queue, whose length stays on the device
+__global__ __launch_bounds__(256) void k_wb_final_heavy(const uint64_t *part, const uint32_t *gstart, uint64_t g_cnt,
+                                                        uint64_t n, uint32_t C, uint64_t *out, uint32_t *bad,
+                                                        const uint32_t *heavy) {
+    __shared__ Xyzz red[256];
+    for (uint32_t q = blockIdx.x; q < heavy[0]; q += gridDim.x) {
+        const uint64_t g = heavy[1 + q];
+        const uint64_t t0 = gstart[g], t1 = g + 1 < g_cnt ? gstart[g + 1] : n;
+        const uint64_t np = (t1 - 1) / C - t0 / C + 1;
+        Xyzz acc = Xyzz::inf();
+#pragma unroll 1
+        for (uint64_t k = threadIdx.x; k < np; k += blockDim.x)
+            acc = add(acc, load_xyzz(part + 24 * wb_piece_end(t0, t1, C, k)));
+        red[threadIdx.x] = acc;
+        __syncthreads();
+        for (uint32_t h = blockDim.x / 2; h > 0; h /= 2) {
+            if (threadIdx.x < h) red[threadIdx.x] = add(red[threadIdx.x], red[threadIdx.x + h]);
+            __syncthreads();
+        }
+        if (threadIdx.x == 0) {
+            if (red[0].is_inf()) atomicOr(bad, 1u);
+            store_xyzz(out + 24 * (uint64_t)wb_slot(g, g_cnt, n), red[0]);
+        }
+        __syncthreads();
+    }
 }
 
 // z's runs: z_(i+1) = z_i ratio_i and ratio_i = 1 exactly when sigma fixes
@@ -253,7 +290,7 @@ void *cub_tmp(DevBuf &b, size_t bytes) {
 // size n present); sets wb.ok
 void build_wire_bases(pnp_ctx *ctx, uint64_t n) {
     auto &wb = ctx->wb;
-    hipStream_t s = ctx->stream;
+    hipStream_t s = tables_stream(ctx);
     wb = pnp_ctx::WireBases{};
     wb.built = true;
     wb.n = n;
@@ -279,6 +316,7 @@ void build_wire_bases(pnp_ctx *ctx, uint64_t n) {
         hipLaunchKernelGGL(k_wb_keys, dim3(nblk(N)), dim3(256), 0, s, idv.u64(), N, key.u64(),
                            static_cast<uint32_t *>(pos.p));
         PNP_HIP(hipGetLastError());
+        bg_step(s);
         size_t tb = 0;
         PNP_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, key.u64(), key2.u64(),
                                                    static_cast<uint32_t *>(pos.p), static_cast<uint32_t *>(pos2.p),
@@ -291,6 +329,7 @@ void build_wire_bases(pnp_ctx *ctx, uint64_t n) {
         hipLaunchKernelGGL(k_wb_next, dim3(nblk(N)), dim3(256), 0, s, sg, n, key2.u64(),
                            static_cast<const uint32_t *>(pos2.p), idv.u64(), static_cast<uint32_t *>(next.p), bad);
         PNP_HIP(hipGetLastError());
+        bg_step(s);
     }
     // 2. cycle labels (the jumps run on a copy: `next` stays the successor,
     // z's runs below read it)
@@ -301,9 +340,11 @@ void build_wire_bases(pnp_ctx *ctx, uint64_t n) {
         uint32_t *na = static_cast<uint32_t *>(nx1.p), *nb = static_cast<uint32_t *>(nx2.p);
         hipLaunchKernelGGL(k_wb_iota, dim3(nblk(N)), dim3(256), 0, s, la, N);
         PNP_HIP(hipGetLastError());
+        bg_step(s);
         for (uint64_t span = 1; span < N; span *= 2) {
             hipLaunchKernelGGL(k_wb_jump, dim3(nblk(N)), dim3(256), 0, s, la, na, lb, nb, N);
             PNP_HIP(hipGetLastError());
+            bg_step(s);
             std::swap(la, lb);
             std::swap(na, nb);
         }
@@ -315,6 +356,8 @@ void build_wire_bases(pnp_ctx *ctx, uint64_t n) {
     std::vector<DevBuf> bx(5);
     {
         DevBuf srt(n * 4), srow(n * 4), row(n * 4), head(n * 4), gid(n * 4), gstart(n * 4), part(n * 192);
+        // (at most n / (C WB_HEAVY) groups have more than WB_HEAVY pieces)
+        DevBuf heavy((n / (32 * WB_HEAVY) + 2) * 4);
         uint32_t *srt_p = static_cast<uint32_t *>(srt.p), *srow_p = static_cast<uint32_t *>(srow.p);
         uint32_t *head_p = static_cast<uint32_t *>(head.p), *gid_p = static_cast<uint32_t *>(gid.p);
         const int bits = (int)lg + 2;  // labels < 4n
@@ -328,22 +371,33 @@ void build_wire_bases(pnp_ctx *ctx, uint64_t n) {
                                static_cast<uint32_t *>(wb.grp[j].p), static_cast<uint32_t *>(wb.rep[j].p),
                                static_cast<uint32_t *>(gstart.p));
             PNP_HIP(hipGetLastError());
+            bg_step(s);
             hipLaunchKernelGGL(k_wb_chunks, dim3(nblk((n + C - 1) / C)), dim3(256), 0, s, L, srow_p, gid_p, n, C,
                                part.u64());
             PNP_HIP(hipGetLastError());
+            bg_step(s);
             // the n slots: valid points everywhere (the empty slots' are never
             // read, their scalars stay zero), the group sums at the group slots
             bx[j].alloc(n * 192);
             hipLaunchKernelGGL(k_wb_lift, dim3(nblk(n)), dim3(256), 0, s, L, n, bx[j].u64());
             PNP_HIP(hipGetLastError());
+            bg_step(s);
+            PNP_HIP(hipMemsetAsync(heavy.p, 0, 4, s));
             hipLaunchKernelGGL(k_wb_final, dim3(nblk(g)), dim3(256), 0, s, part.u64(),
-                               static_cast<const uint32_t *>(gstart.p), (uint64_t)g, n, C, bx[j].u64(), bad);
+                               static_cast<const uint32_t *>(gstart.p), (uint64_t)g, n, C, bx[j].u64(), bad,
+                               static_cast<uint32_t *>(heavy.p));
             PNP_HIP(hipGetLastError());
+            hipLaunchKernelGGL(k_wb_final_heavy, dim3(64), dim3(256), 0, s, part.u64(),
+                               static_cast<const uint32_t *>(gstart.p), (uint64_t)g, n, C, bx[j].u64(), bad,
+                               static_cast<const uint32_t *>(heavy.p));
+            PNP_HIP(hipGetLastError());
+            bg_step(s);
         };
         for (int j = 0; j < 4; j++) {
             const uint32_t *labj = static_cast<const uint32_t *>(lab.p) + (uint64_t)j * n;
             hipLaunchKernelGGL(k_wb_iota, dim3(nblk(n)), dim3(256), 0, s, static_cast<uint32_t *>(row.p), n);
             PNP_HIP(hipGetLastError());
+            bg_step(s);
             size_t tb = 0;
             PNP_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, labj, srt_p, static_cast<uint32_t *>(row.p),
                                                        srow_p, (int)n, 0, bits, s));
@@ -351,6 +405,7 @@ void build_wire_bases(pnp_ctx *ctx, uint64_t n) {
                                                        static_cast<uint32_t *>(row.p), srow_p, (int)n, 0, bits, s));
             hipLaunchKernelGGL(k_wb_heads, dim3(nblk(n)), dim3(256), 0, s, srt_p, n, head_p);
             PNP_HIP(hipGetLastError());
+            bg_step(s);
             tb = 0;
             PNP_HIP(hipcub::DeviceScan::InclusiveSum(nullptr, tb, head_p, gid_p, (int)n, s));
             PNP_HIP(hipcub::DeviceScan::InclusiveSum(cub_tmp(tmp, tb), tb, head_p, gid_p, (int)n, s));
@@ -364,6 +419,7 @@ void build_wire_bases(pnp_ctx *ctx, uint64_t n) {
                 bx[j].alloc(n * 192);
                 hipLaunchKernelGGL(k_wb_lift, dim3(nblk(n)), dim3(256), 0, s, L, n, bx[j].u64());
                 PNP_HIP(hipGetLastError());
+                bg_step(s);
                 continue;
             }
             bases(j, g);
@@ -373,6 +429,7 @@ void build_wire_bases(pnp_ctx *ctx, uint64_t n) {
             hipLaunchKernelGGL(k_wb_zheads, dim3(nblk(n)), dim3(256), 0, s, static_cast<const uint32_t *>(next.p), n,
                                head_p, srow_p);
             PNP_HIP(hipGetLastError());
+            bg_step(s);
             size_t tb = 0;
             PNP_HIP(hipcub::DeviceScan::InclusiveSum(nullptr, tb, head_p, gid_p, (int)n, s));
             PNP_HIP(hipcub::DeviceScan::InclusiveSum(cub_tmp(tmp, tb), tb, head_p, gid_p, (int)n, s));
@@ -449,18 +506,25 @@ void build_wire_bases(pnp_ctx *ctx, uint64_t n) {
 
 // the groups for domain n, (re)built when the keys changed
 bool wire_bases_ready(pnp_ctx *ctx, uint64_t n) {
+    if (tables_busy(ctx)) return false;  // being built in the background: commit without them
     auto &wb = ctx->wb;
     if (wb.built && wb.n == n && wb.pk_gen != ctx->pk_gen) {
         // the prover key was loaded again (the v1 symbol does it every call):
         // same sigma, same groups
+        DevBuf own;  // (the builder's thread keeps off the proof's scratch)
+        DevBuf &scr = t_bg_build ? own : ctx->scratch_b;
         bool same = wb.sigma.p != nullptr;
         for (int j = 0; j < 4 && same; j++)
-            same = !k_any_diff(wb.sigma.u64() + 4 * (uint64_t)j * n, ctx->pk_sigma_n[j].u64(), 4 * n, ctx->scratch_b,
-                               ctx->stream);
+            same = !k_any_diff(wb.sigma.u64() + 4 * (uint64_t)j * n, ctx->pk_sigma_n[j].u64(), 4 * n, scr,
+                               tables_stream(ctx));
         if (same) wb.pk_gen = ctx->pk_gen;
         else wb.built = false;
     }
-    if ((!wb.built || wb.n != n) && ctx->defer_now) return false;  // PNP_DEFER_TABLES: next proof
+    // a deferring proof goes without them (built in the background or by the next proof)
+    if ((!wb.built || wb.n != n) && ctx->defer_now && !t_bg_build) {
+        ctx->tables_wanted = true;
+        return false;
+    }
     if (!wb.built || wb.n != n) {
         // built on the same call on every rank; a rank whose HBM cannot hold
         // the groups makes every rank commit without them
@@ -492,6 +556,9 @@ bool wire_bases_ready(pnp_ctx *ctx, uint64_t n) {
 }  // namespace
 
 void wire_bases_reset(pnp_ctx *ctx) { ctx->wb = pnp_ctx::WireBases{}; }
+void wire_bases_build(pnp_ctx *ctx, uint64_t n) {
+    if (groups_enabled() && !ctx->hbm_groups_off) wire_bases_ready(ctx, n);
+}
 bool wire_groups_enabled() { return groups_enabled(); }
 
 bool commit_wires_grouped(pnp_ctx *ctx, const uint64_t *const *d_evals, uint64_t n, CommitmentC *const *out) {

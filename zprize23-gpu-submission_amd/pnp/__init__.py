@@ -36,7 +36,7 @@ SYMBOLS = ("gen_proof", "pnp_last_error", "pnp_ctx_create", "pnp_ctx_destroy",
            "pnp_synth_random_fr", "pnp_synth_srs", "pnp_synth_coset_consts", "pnp_synth_circuit",
            "pnp_synth_merkle", "pnp_load_commit_key_strided", "pnp_proof_infinity_mask",
            "pnp_set_exchange_v", "pnp_commit_segments", "pnp_hbm_usage",
-           "pnp_ctx_stream", "pnp_set_exchange_ordered")
+           "pnp_ctx_stream", "pnp_set_exchange_ordered", "pnp_v1_context")
 
 
 # int allgather(void *user, uint64_t bytes_per_rank) — pnp_set_msm_shard
@@ -70,6 +70,7 @@ def load(path: str = LIB_PATH):
     vp, u64, i32 = C.c_void_p, C.c_uint64, C.c_int
     lib.gen_proof.argtypes = [abi.CircuitC, abi.ProverKeyC, abi.CommitKeyC]
     lib.gen_proof.restype = abi.ProofC
+    lib.pnp_v1_context.restype = vp
     lib.pnp_last_error.restype = C.c_char_p
     lib.pnp_ctx_create.argtypes = [i32, C.POINTER(vp)]
     lib.pnp_ctx_destroy.argtypes = [vp]
@@ -111,7 +112,7 @@ def load(path: str = LIB_PATH):
     lib.pnp_load_commit_key_strided.argtypes = [vp, vp, u64, C.POINTER(abi.AffineLayout), i32]
     lib.pnp_proof_infinity_mask.argtypes = [C.POINTER(abi.ProofC)]
     for name in SYMBOLS:
-        if name.startswith("pnp_") and name not in ("pnp_last_error", "pnp_ctx_destroy"):
+        if name.startswith("pnp_") and name not in ("pnp_last_error", "pnp_ctx_destroy", "pnp_v1_context"):
             getattr(lib, name).restype = C.c_int if name != "pnp_last_error" else C.c_char_p
     lib.pnp_proof_infinity_mask.restype = C.c_uint32
     _LIB = lib
