@@ -41,6 +41,7 @@ def _launch(world, args, tmp_path, timeout, **extra_env):
         import time
         hb_dir = os.path.join(os.path.dirname(HERE), "gpurun_out")
         t0 = last = time.time()
+        cpu0 = _cpu_snapshot(procs)
         while any(p.poll() is None for p in procs) and time.time() - t0 < timeout:
             time.sleep(1)
             if time.time() - last >= 30:
@@ -53,8 +54,11 @@ def _launch(world, args, tmp_path, timeout, **extra_env):
                         free = f", HBM free {f_ / 2**30:.1f} of {t_ / 2**30:.0f} GiB"
                 except Exception:
                     pass
+                cpu1 = _cpu_snapshot(procs)
                 line = (f"[{time.strftime('%H:%M:%S')}] {world} ranks ({' '.join(args[:1])}): "
-                        f"{sum(p.poll() is None for p in procs)} running, {last - t0:.0f} s{free}\n")
+                        f"{sum(p.poll() is None for p in procs)} running, {last - t0:.0f} s{free}; "
+                        f"{_cpu_delta(cpu0, cpu1)}\n")
+                cpu0 = cpu1
                 for r in range(world):  # each rank's last progress line
                     try:
                         tail = (tmp_path / f"rank{r}.log").read_bytes().decode(errors="replace").strip()
@@ -73,6 +77,47 @@ def _launch(world, args, tmp_path, timeout, **extra_env):
                 p.kill()
     for p, o in zip(procs, outs):
         assert p.returncode == 0, o[-3000:]
+
+
+def _cpu_snapshot(procs):
+    """CPU evidence for the heartbeat: the cgroup's bandwidth throttling
+    counters (cpu.stat), the load average, the ranks' and this process's CPU
+    seconds and thread counts"""
+    snap = {"t": __import__("time").time()}
+    try:
+        with open("/sys/fs/cgroup/cpu.stat") as f:
+            for line in f:
+                k, v = line.split()
+                snap[k] = int(v)
+    except OSError:
+        pass
+    try:
+        with open("/proc/loadavg") as f:
+            snap["load"] = f.read().split()[0]
+    except OSError:
+        pass
+    cpu, thr = 0.0, 0
+    tick = os.sysconf("SC_CLK_TCK")
+    for pid in [p.pid for p in procs if p.poll() is None] + [os.getpid()]:
+        try:
+            with open(f"/proc/{pid}/stat") as f:
+                fs = f.read().rsplit(")", 1)[1].split()
+            cpu += (int(fs[11]) + int(fs[12])) / tick
+            thr += int(fs[17])
+        except (OSError, IndexError, ValueError):
+            pass
+    snap["cpu_s"], snap["threads"] = cpu, thr
+    return snap
+
+
+def _cpu_delta(a, b):
+    dt = max(b["t"] - a["t"], 1e-3)
+    out = f"cpu {(b['cpu_s'] - a['cpu_s']) / dt:.1f} cores busy, {b['threads']} threads, load {b.get('load')}"
+    if "nr_throttled" in a and "nr_throttled" in b:
+        out += (f", cgroup throttled {b['nr_throttled'] - a['nr_throttled']} of "
+                f"{b['nr_periods'] - a['nr_periods']} periods "
+                f"({(b['throttled_usec'] - a['throttled_usec']) / 1e6:.1f} s)")
+    return out
 
 
 def test_window_exchange_gloo_world2(tmp_path):
@@ -147,13 +192,17 @@ def test_sharded_full_size_matches_golden(tmp_path, golden, world, shard):
         torch.cuda.synchronize()
         torch.cuda.empty_cache()
     prefix = str(tmp_path / "full")
-    # 4 and 8 ranks on one GPU at 2^22: no copy-constraint wire groups (in
-    # bucket-range mode every rank holds their full folded table, 5 segments x
-    # n x 13 windows x 128 B = 35 GB at 2^22, plus its build scratch: 8 ranks
-    # would need ~300 GB of this one GPU's 288; one rank per GPU has room) —
-    # test_sharded_merkle_h13_groups_on runs the production default with the
-    # groups at 4 and 8 ranks at 2^20
-    extra = {"PNP_WIRE_GROUPS": "0"} if world >= 4 else {}
+    # 4 and 8 ranks on one GPU at 2^22 in bucket-range mode: no copy-constraint
+    # wire groups (every rank holds their full folded table, 5 segments x n x
+    # 13 windows x 128 B = 35 GB at 2^22, plus its build scratch: 8 ranks would
+    # need ~300 GB of this one GPU's 288; one rank per GPU has room) —
+    # test_sharded_merkle_h13_groups_on runs that default at 4 and 8 ranks at 2^20
+    # In point-range mode each rank builds only its 1/world slice of the group
+    # table, so the 8 ranks of the Merkle case hold the
+    # production default, groups on, and must really commit over them
+    extra = {"PNP_WIRE_GROUPS": "0"} if world >= 4 and shard == "buckets" else {}
+    if shard == "points" and g.get("circuit") == "merkle":
+        extra["PNP_EXPECT_GROUPS"] = "1"
     _launch(world, ["full", prefix, str(g["lg"]), str(g["gates"]), str(g["seed"]), g.get("circuit", "arith")],
             tmp_path, 900, PNP_TEST_MSM_SHARD=shard, PNP_EXPECT_BUCKETS="1" if shard == "buckets" else "0",
             PNP_MSM_BUCKETS_MIN_WORLD="2", **extra)

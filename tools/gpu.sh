@@ -14,7 +14,8 @@
 #   stats[=STEPS]    rocprofv3 --kernel-trace --stats over a short bench
 #   trace=ARGS       the same over bench.py ARGS ('+'-separated, e.g. --solo+7/8+--steps+2)
 #   pmc[=COUNTERS]   one rocprofv3 --pmc pass over one bench proof (counters
-#                    '+'-separated; default the SQ issue / VALU group)
+#                    '+'-separated; default the SQ issue / VALU group);
+#                    PMC_BENCH_ARGS: other bench.py arguments (e.g. --op ntt --lg 20)
 #   traffic          FETCH_SIZE and WRITE_SIZE passes (two runs)
 #   solo[=R/W,...]   bench.py --solo for each R/W (default 0/2,0/4,0/8,7/8)
 #   ab=N:V1,V2,...   tools/abn.sh N rounds over the variants
@@ -25,7 +26,7 @@ R=$(pwd)
 TAG=${1:?tag}; shift
 OUT=$R/gpurun_out/$TAG
 mkdir -p "$OUT"
-RX='k_accumulate29|k_ntt_pass|k_quotient|k_coarse_scatter|k_fine_sort|k_tree_level|k_t_combine|k_merge_tails29|k_tree_leafw29|k_digits_hist|k_count_pieces'
+RX='k_accumulate29|k_ntt_pass|k_bitrev|k_quotient|k_coarse_scatter|k_fine_sort|k_tree_level|k_t_combine|k_merge_tails29|k_tree_leafw29|k_digits_hist|k_count_pieces'
 BENCH1="--steps 1 --warmup 0 --cpu-lg 0 --drop-in '' --no-verify"
 
 run_step() {
@@ -54,7 +55,7 @@ run_step() {
       local d=$OUT/pmc_$(echo "$c" | tr '+' '_' | cut -c1-40)
       (cd /tmp && export TMPDIR=/tmp && timeout -s KILL 200 rocprofv3 --pmc ${c//+/ } --kernel-include-regex "$RX" -f csv \
           -d "$d" -o run -- python3 "$R/bench.py" --steps 1 --warmup 0 --cpu-lg 0 --drop-in "" --no-verify \
-          > "$d.log" 2>&1) ;;
+          ${PMC_BENCH_ARGS:-} > "$d.log" 2>&1) ;;
     traffic)
       run_step pmc=FETCH_SIZE && run_step pmc=WRITE_SIZE ;;
     solo*)

@@ -268,7 +268,40 @@ static void scan_u32(uint32_t *d, uint64_t n, DevBuf &scratch, hipStream_t s) {
 constexpr int TILE_K = PNP_TILE_K;
 constexpr int KPT = TILE_K / 1024;  // keys per lane per tile
 static_assert(TILE_K % 4096 == 0 && TILE_K <= 16384, "PNP_TILE_K: a multiple of 4096 up to 16384");
-__device__ __forceinline__ void tile_scan(uint32_t *lh, uint32_t *lofs, int nb) {
+// exclusive scan of lh[0..nb) into lofs by the whole workgroup: each lane
+// sums its run of ceil(nb / blockDim) bins, one wave-level scan, the wave
+// totals through LDS (wsum: blockDim / 64 words).  Every lane must call it; the
+// caller synchronises after it.  (PNP_SORT_SCAN=0: wave 0 alone, 32 bins per
+// lane in sequence at 2048 fine bins while 15 waves wait at the barrier)
+#ifndef PNP_SORT_SCAN
+#define PNP_SORT_SCAN 1
+#endif
+__device__ __forceinline__ void tile_scan_wave0(uint32_t *lh, uint32_t *lofs, int nb);
+__device__ __forceinline__ void tile_scan(uint32_t *lh, uint32_t *lofs, int nb, uint32_t *wsum) {
+#if PNP_SORT_SCAN
+    const int per = (nb + (int)blockDim.x - 1) / (int)blockDim.x, b0 = (int)threadIdx.x * per;
+    uint32_t loc = 0;
+    for (int b = b0; b < b0 + per && b < nb; b++) loc += lh[b];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    uint32_t x = loc;
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t y = __shfl_up(x, off, 64);
+        if (lane >= off) x += y;
+    }
+    if (lane == 63) wsum[wv] = x;
+    __syncthreads();
+    uint32_t run = x - loc;
+    for (int j = 0; j < wv; j++) run += wsum[j];
+    for (int b = b0; b < b0 + per && b < nb; b++) {
+        lofs[b] = run;
+        run += lh[b];
+    }
+#else
+    (void)wsum;
+    tile_scan_wave0(lh, lofs, nb);
+#endif
+}
+__device__ __forceinline__ void tile_scan_wave0(uint32_t *lh, uint32_t *lofs, int nb) {
     // exclusive scan of lh[0..nb) into lofs by wave 0
     if (threadIdx.x < 64) {
         const int per = (nb + 63) / 64, b0 = threadIdx.x * per;
@@ -298,7 +331,7 @@ __global__ __launch_bounds__(1024) void k_coarse_scatter(const uint32_t *keys, K
                                                          uint16_t *fk, int wmaj = 1, uint64_t *rec = nullptr,
                                                          uint32_t slot_recs = 0, uint32_t hdr_recs = 0,
                                                          uint32_t cap = 0) {
-    __shared__ uint32_t cur[1 << SORT_CB], lh[1 << SORT_CB], lofs[1 << SORT_CB], lim[1 << SORT_CB];
+    __shared__ uint32_t cur[1 << SORT_CB], lh[1 << SORT_CB], lofs[1 << SORT_CB], lim[1 << SORT_CB], wsum[16];
     __shared__ uint32_t st_e[TILE_K];
     __shared__ uint32_t st_m[TILE_K];
     const int v = blockIdx.y, ch = blockIdx.x;
@@ -361,7 +394,7 @@ __global__ __launch_bounds__(1024) void k_coarse_scatter(const uint32_t *keys, K
             for (int j = 0; j < KPT; j++)
                 if (key[j] != KEY_ZERO) rank[j] = atomicAdd(&lh[(key[j] & 0x7FFFFFFFu) >> fb], 1u);
             __syncthreads();
-            tile_scan(lh, lofs, NBc);
+            tile_scan(lh, lofs, NBc, wsum);
             __syncthreads();
 #pragma unroll
             for (int j = 0; j < KPT; j++) {
@@ -414,7 +447,7 @@ static_assert(TILE_F % 1024 == 0 && TILE_F >= 1024 && TILE_F <= 16384,
 __global__ __launch_bounds__(1024) void k_fine_sort(const uint32_t *ent, const uint16_t *fk,
                                                     const uint32_t *coffs, int nch, int fb,
                                                     uint32_t *bstart, uint32_t *sorted) {
-    __shared__ uint32_t h[1 << SORT_FB_MAX], lh[1 << SORT_FB_MAX], lofs[1 << SORT_FB_MAX];
+    __shared__ uint32_t h[1 << SORT_FB_MAX], lh[1 << SORT_FB_MAX], lofs[1 << SORT_FB_MAX], wsum[16];
     __shared__ uint32_t st_e[TILE_F];
     __shared__ uint16_t st_f[TILE_F];
     const uint64_t p = blockIdx.x;
@@ -434,7 +467,7 @@ __global__ __launch_bounds__(1024) void k_fine_sort(const uint32_t *ent, const u
     for (uint32_t k = ps + threadIdx.x; k < a; k += blockDim.x) atomicAdd(&h[fk[k]], 1u);
     for (uint32_t k = b + threadIdx.x; k < pe; k += blockDim.x) atomicAdd(&h[fk[k]], 1u);
     __syncthreads();
-    tile_scan(h, lofs, NF);
+    tile_scan(h, lofs, NF, wsum);
     __syncthreads();
     for (int f = threadIdx.x; f < NF; f += blockDim.x) h[f] = ps + lofs[f];  // cursor of fine bin f
     __syncthreads();
@@ -467,7 +500,7 @@ __global__ __launch_bounds__(1024) void k_fine_sort(const uint32_t *ent, const u
         for (int j = 0; j < PER; j++)
             if (tb + threadIdx.x + j * 1024 < pe) rank[j] = atomicAdd(&lh[f[j]], 1u);
         __syncthreads();
-        tile_scan(lh, lofs, NF);
+        tile_scan(lh, lofs, NF, wsum);
         __syncthreads();
 #pragma unroll
         for (int j = 0; j < PER; j++) {
@@ -503,7 +536,7 @@ __global__ __launch_bounds__(1024) void k_fine_sort(const uint32_t *ent, const u
 __global__ __launch_bounds__(1024) void k_fine_sort_runs(const uint64_t *rec, const uint2 *runs, int W,
                                                          const uint32_t *out0, int fb, uint32_t *bstart,
                                                          uint32_t *sorted) {
-    __shared__ uint32_t h[1 << SORT_FB_MAX], lh[1 << SORT_FB_MAX], lofs[1 << SORT_FB_MAX];
+    __shared__ uint32_t h[1 << SORT_FB_MAX], lh[1 << SORT_FB_MAX], lofs[1 << SORT_FB_MAX], wsum[16];
     __shared__ uint32_t st_e[TILE_F];
     __shared__ uint16_t st_f[TILE_F];
     const uint64_t p = blockIdx.x;
@@ -516,7 +549,7 @@ __global__ __launch_bounds__(1024) void k_fine_sort_runs(const uint64_t *rec, co
             atomicAdd(&h[(uint32_t)(rec[run.x + k] >> 32) & 0xFFFFu], 1u);
     }
     __syncthreads();
-    tile_scan(h, lofs, NF);
+    tile_scan(h, lofs, NF, wsum);
     __syncthreads();
     const uint32_t ps = out0[p];
     for (int f = threadIdx.x; f < NF; f += blockDim.x) h[f] = ps + lofs[f];  // cursor of fine bin f
@@ -539,7 +572,7 @@ __global__ __launch_bounds__(1024) void k_fine_sort_runs(const uint64_t *rec, co
                 }
             }
             __syncthreads();
-            tile_scan(lh, lofs, NF);
+            tile_scan(lh, lofs, NF, wsum);
             __syncthreads();
 #pragma unroll
             for (int j = 0; j < PER; j++) {
