@@ -55,9 +55,11 @@ def _launch(world, args, tmp_path, timeout, **extra_env):
                 except Exception:
                     pass
                 cpu1 = _cpu_snapshot(procs)
+                qs = kfd_queue_census()
                 line = (f"[{time.strftime('%H:%M:%S')}] {world} ranks ({' '.join(args[:1])}): "
                         f"{sum(p.poll() is None for p in procs)} running, {last - t0:.0f} s{free}; "
-                        f"{_cpu_delta(cpu0, cpu1)}\n")
+                        f"{_cpu_delta(cpu0, cpu1)}; GPU queues {sum(qs.values())} in {len(qs)} processes "
+                        f"(this one {qs.get(os.getpid(), 0)})\n")
                 cpu0 = cpu1
                 for r in range(world):  # each rank's last progress line
                     try:
@@ -77,6 +79,25 @@ def _launch(world, args, tmp_path, timeout, **extra_env):
                 p.kill()
     for p, o in zip(procs, outs):
         assert p.returncode == 0, o[-3000:]
+
+
+def kfd_queue_census():
+    """{pid: hardware queues} of every process with GPU queues, from the KFD's
+    sysfs (/sys/class/kfd/kfd/proc/<pid>/queues/<id>); {} where unreadable.
+    (Processes sharing the GPU past the scheduler's queue capacity are
+    time-sliced: DESIGN.md §4, the shard-test crawl.)"""
+    out = {}
+    base = "/sys/class/kfd/kfd/proc"
+    try:
+        pids = os.listdir(base)
+    except OSError:
+        return out
+    for pid in pids:
+        try:
+            out[int(pid)] = len(os.listdir(os.path.join(base, pid, "queues")))
+        except (OSError, ValueError):
+            pass
+    return out
 
 
 def _cpu_snapshot(procs):

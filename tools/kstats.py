@@ -7,7 +7,7 @@ import csv
 import sys
 
 rows = list(csv.DictReader(open(sys.argv[1])))
-proofs = sum(int(r["Calls"]) for r in rows if r["Name"].startswith("pnp::k_quotient_"))
+proofs = sum(int(r["Calls"]) for r in rows if r["Name"].startswith(("pnp::k_quotient_", "pnp::k_quotient29_")))
 setup = ("k_srs_", "k_table_", "k_synth", "k_coset_consts", "k_powers_table", "k_to_blocks", "k_fermat_inv")
 tot = 0.0
 print(f"{proofs} proofs")

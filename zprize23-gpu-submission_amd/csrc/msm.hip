@@ -457,12 +457,30 @@ __global__ __launch_bounds__(1024) void k_fine_sort(const uint32_t *ent, const u
     __syncthreads();
     // [a, b): 4-aligned body read as 4 x u16; the rest one by one
     const uint32_t a = std::min((ps + 3) & ~3u, pe), b = std::max(pe & ~3u, a);
-    for (uint32_t k = a + 4 * threadIdx.x; k < b; k += 4 * blockDim.x) {
-        uint2 q = *reinterpret_cast<const uint2 *>(fk + k);
-        atomicAdd(&h[q.x & 0xFFFF], 1u);
-        atomicAdd(&h[q.x >> 16], 1u);
-        atomicAdd(&h[q.y & 0xFFFF], 1u);
-        atomicAdd(&h[q.y >> 16], 1u);
+    {
+        // four loads in flight per lane before their atomics (the loop is
+        // latency-bound: ~26 steps per bin at 2^22)
+        const uint32_t step = 4 * blockDim.x;
+        uint32_t k = a + 4 * threadIdx.x;
+        for (; k + 3 * step < b; k += 4 * step) {
+            uint2 q[4];
+#pragma unroll
+            for (int u = 0; u < 4; u++) q[u] = *reinterpret_cast<const uint2 *>(fk + k + u * step);
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                atomicAdd(&h[q[u].x & 0xFFFF], 1u);
+                atomicAdd(&h[q[u].x >> 16], 1u);
+                atomicAdd(&h[q[u].y & 0xFFFF], 1u);
+                atomicAdd(&h[q[u].y >> 16], 1u);
+            }
+        }
+        for (; k < b; k += step) {
+            const uint2 q = *reinterpret_cast<const uint2 *>(fk + k);
+            atomicAdd(&h[q.x & 0xFFFF], 1u);
+            atomicAdd(&h[q.x >> 16], 1u);
+            atomicAdd(&h[q.y & 0xFFFF], 1u);
+            atomicAdd(&h[q.y >> 16], 1u);
+        }
     }
     for (uint32_t k = ps + threadIdx.x; k < a; k += blockDim.x) atomicAdd(&h[fk[k]], 1u);
     for (uint32_t k = b + threadIdx.x; k < pe; k += blockDim.x) atomicAdd(&h[fk[k]], 1u);
@@ -886,7 +904,7 @@ __global__ __launch_bounds__(256, PNP_ACC_WAVES) void k_accumulate29(const uint3
                                                       const uint32_t *offs, uint64_t U, uint32_t S,
                                                       uint32_t *buckets, uint32_t *head,
                                                       uint32_t *tail, uint32_t *tailb, uint32_t *redo,
-                                                      uint32_t *nredo) {
+                                                      uint32_t *nredo, uint32_t *tlist) {
 #if PNP_ACC_GLDS
     // per wave: the staged point (7 x 64 x 16 B) and the staged next index
     // (64 x 4 B); both arrive by LDS-DMA, so no ordinary global load result is
@@ -961,6 +979,18 @@ __global__ __launch_bounds__(256, PNP_ACC_WAVES) void k_accumulate29(const uint3
     const bool to_tail = !first && next > hi;
     ok &= store29(first ? head + 56 * t : (to_tail ? tail + 56 * t : buckets + 56 * cur), acc);
     tailb[t] = to_tail ? (uint32_t)cur : NO_TAIL;
+    // the lanes with a tail, compacted (tlist[0] = count, then lane ids; one
+    // atomic per wave): the merge runs one lane per listed tail instead of one
+    // per accumulation lane, ~2/3 of which have none
+    const uint64_t m = __ballot(to_tail);
+    if (to_tail) {
+        const int leader = __ffsll((unsigned long long)m) - 1;
+        const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+        uint32_t base = 0;
+        if (below == 0) base = atomicAdd(tlist, (uint32_t)__popcll(m));
+        base = __shfl(base, leader);
+        tlist[1 + base + below] = (uint32_t)t;
+    }
     if (!ok) redo[atomicAdd(nredo, 1u)] = (uint32_t)t;
 }
 
@@ -1232,7 +1262,13 @@ static uint32_t acc_segment(uint64_t nent, bool folded) {
         slots = (uint64_t)cus * 4 * PNP_ACC_WAVES * 64;
     }
     const uint64_t per = (nent + slots - 1) / slots;  // entries per lane in one round
-    const uint64_t rounds = std::max<uint64_t>(1, per / S);
+    // PNP_ACC_ROUNDS=R: at most R rounds (longer segments, fewer split buckets
+    // to merge; experiments)
+    static const uint64_t max_rounds = [] {
+        const char *e = getenv("PNP_ACC_ROUNDS");
+        return e && atoi(e) > 0 ? (uint64_t)atoi(e) : ~0ULL;
+    }();
+    const uint64_t rounds = std::min(max_rounds, std::max<uint64_t>(1, per / S));
     // a batch smaller than one round at S = 64 (one MSM of a 2^19-point rank
     // range: ~35 entries per lane) takes shorter segments and fills the chip
     // instead of leaving part of it idle (more bucket pieces to merge, a few %
@@ -1263,16 +1299,18 @@ static void accumulate_group(MsmWork &wk, MsmGroup &gb, const GroupPlan &gp, con
     const uint64_t nthr = (nent + S - 1) / S;
     if (table) {
         // raw radix-2^29 pieces: buckets inside one segment, then heads, tails
-        need(gb.seg, (WB + 2 * nthr) * 224 + nthr * 4);
+        need(gb.seg, (WB + 2 * nthr) * 224 + nthr * 4 + (nthr + 1) * 4);
         uint32_t *bk29 = static_cast<uint32_t *>(gb.seg.p);
         uint32_t *head = bk29 + 56 * WB, *tail = head + 56 * nthr, *tailb = tail + 56 * nthr;
+        uint32_t *tlist = tailb + nthr;  // [0] count, then the lanes with a tail
+        PNP_HIP(hipMemsetAsync(tlist, 0, 4, s));
         need(gb.redo, nthr * 4 + 16);
         uint32_t *nredo = static_cast<uint32_t *>(gb.redo.p), *redo = nredo + 4;
         PNP_HIP(hipMemsetAsync(nredo, 0, 4, s));
         const uint32_t *t29 = reinterpret_cast<const uint32_t *>(table);
         const uint32_t blocks = (uint32_t)((nthr + 255) / 256);
         hipLaunchKernelGGL(k_accumulate29, dim3(blocks), dim3(256), 0, s, t29, sorted, bstart, WB, S, bk29,
-                           head, tail, tailb, redo, nredo);
+                           head, tail, tailb, redo, nredo, tlist);
         PNP_HIP(hipGetLastError());
         // equal / opposite points or infinity inside a piece: exact recomputation
         // of the flagged lanes (the count stays on the device: no host sync)
@@ -1286,7 +1324,7 @@ static void accumulate_group(MsmWork &wk, MsmGroup &gb, const GroupPlan &gp, con
         gb.pieces = (uint32_t)(nent / WB / S + 1);
         gb.nthr = nthr;
         need(gb.heavy, (WB + 1) * 4);
-        msm_merge_pieces29(bstart, WB, S, nthr, tailb, bk29, head, tail, static_cast<uint32_t *>(gb.exc.p),
+        msm_merge_pieces29(bstart, WB, S, nthr, tailb, tlist, bk29, head, tail, static_cast<uint32_t *>(gb.exc.p),
                            static_cast<uint32_t *>(gb.heavy.p), s);
     } else {
         need(gb.seg, nthr * 2 * 24 * 8);

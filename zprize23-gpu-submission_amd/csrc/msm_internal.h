@@ -51,7 +51,8 @@ void msm_merge_pieces(const uint32_t *offs, int nch, uint64_t U, uint32_t S, uin
 
 // the same over raw radix-2^29 pieces (folded layout, 56 u32 each, ec29.cuh),
 // one merge lane per accumulation lane t whose segment ended inside bucket
-// tailb[t] (NO_TAIL otherwise): bk29 holds the buckets inside one lane's
+// tailb[t] (NO_TAIL otherwise; tlist: [0] the count, then those lanes t,
+// compacted by the accumulation): bk29 holds the buckets inside one lane's
 // segment on entry and every NON-EMPTY bucket (F29) on exit; empty buckets
 // (offs[u] = offs[u + 1]) are left unwritten and read as infinity by
 // msm_reduce29.  (An equal / opposite pair of operands sets *exc: see
@@ -59,7 +60,7 @@ void msm_merge_pieces(const uint32_t *offs, int nch, uint64_t U, uint32_t S, uin
 // buckets of > 64 pieces).
 constexpr uint32_t NO_TAIL = 0xFFFFFFFFu;
 void msm_merge_pieces29(const uint32_t *offs, uint64_t U, uint32_t S, uint64_t nthr, const uint32_t *tailb,
-                        uint32_t *bk29, const uint32_t *head, const uint32_t *tail, uint32_t *exc,
+                        const uint32_t *tlist, uint32_t *bk29, const uint32_t *head, const uint32_t *tail, uint32_t *exc,
                         uint32_t *heavy, hipStream_t s);
 // exact fallback: the same pieces summed in 32-bit Fq into bk (R384)
 void msm_merge_pieces29_exact(const uint32_t *offs, uint64_t U, uint32_t S, uint32_t pieces,

@@ -131,9 +131,7 @@ void msm_merge_pieces(const uint32_t *offs, int nch, uint64_t U, uint32_t S, uin
 // the 32-bit Fq products, no per-piece conversion).  A bucket inside one
 // lane's segment is already bk29[u].  A bucket u split across lanes t0 < t1 is
 // tail29[t0] + head29[t0+1] + ... + head29[t1]; its merge lane is accumulation
-// lane t0, which recorded u in tailb[t0].  (One lane per BUCKET, the first
-// version, left ~2/3 of every wave idle: with ~3 buckets per accumulation
-// segment only one bucket in three is split.)  Empty buckets are not written
+// lane t0, which recorded u in tailb[t0] and listed itself in tlist.  Empty buckets are not written
 // (msm_reduce29 reads them as infinity).  A bucket of more than MERGE_HEAVY
 // pieces (clustered or repeated scalars, a short top window) is not summed
 // here, where one lane would add its pieces one after another, but queued
@@ -142,14 +140,17 @@ void msm_merge_pieces(const uint32_t *offs, int nch, uint64_t U, uint32_t S, uin
 #define PNP_MERGE_HEAVY 64
 #endif
 constexpr uint32_t MERGE_HEAVY = PNP_MERGE_HEAVY;
-__global__ __launch_bounds__(256) void k_merge_tails29(const uint32_t *offs, uint64_t U, uint32_t S, uint64_t nthr,
-                                                       const uint32_t *tailb, uint32_t *bk29, const uint32_t *head,
+// One merge lane per listed tail (tlist: the accumulation lanes that left
+// one, compacted by k_accumulate29): a wave is 64 merges, where one lane per
+// accumulation lane ran ~1 in 3 of its lanes (a segment of ~3 buckets splits one)
+__global__ __launch_bounds__(256) void k_merge_tails29(const uint32_t *offs, uint32_t S, const uint32_t *tailb,
+                                                       const uint32_t *tlist, uint32_t *bk29, const uint32_t *head,
                                                        const uint32_t *tail, uint32_t *exc, uint32_t *heavy,
                                                        uint32_t *nheavy) {
-    const uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
-    if (t >= nthr || t * S >= offs[U]) return;  // no segment: tailb[t] never written
+    const uint64_t q = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    if (q >= tlist[0]) return;
+    const uint64_t t = tlist[1 + q];
     const uint32_t u = tailb[t];
-    if (u == NO_TAIL) return;
     const uint32_t t1 = (offs[u + 1] - 1) / S;
     if (t1 - (uint32_t)t >= MERGE_HEAVY) {
         heavy[atomicAdd(nheavy, 1u)] = u;
@@ -188,12 +189,15 @@ __global__ __launch_bounds__(256) void k_merge_heavy29(const uint32_t *offs, uin
 }
 
 void msm_merge_pieces29(const uint32_t *offs, uint64_t U, uint32_t S, uint64_t nthr, const uint32_t *tailb,
-                        uint32_t *bk29, const uint32_t *head, const uint32_t *tail, uint32_t *exc,
-                        uint32_t *heavy, hipStream_t s) {
+                        const uint32_t *tlist, uint32_t *bk29, const uint32_t *head, const uint32_t *tail,
+                        uint32_t *exc, uint32_t *heavy, hipStream_t s) {
+    (void)U;
     uint32_t *nheavy = heavy, *list = heavy + 1;
     PNP_HIP(hipMemsetAsync(nheavy, 0, 4, s));
-    hipLaunchKernelGGL(k_merge_tails29, dim3((uint32_t)((nthr + 255) / 256)), dim3(256), 0, s, offs, U, S, nthr,
-                       tailb, bk29, head, tail, exc, list, nheavy);
+    // (the count stays on the device: a grid for every accumulation lane, the
+    // waves past the count exit at once)
+    hipLaunchKernelGGL(k_merge_tails29, dim3((uint32_t)((nthr + 255) / 256)), dim3(256), 0, s, offs, S, tailb, tlist,
+                       bk29, head, tail, exc, list, nheavy);
     PNP_HIP(hipGetLastError());
     // a small grid: it exits at once when nothing was queued
     hipLaunchKernelGGL(k_merge_heavy29, dim3(256), dim3(256), 0, s, offs, S, bk29, head, tail, exc, list,
