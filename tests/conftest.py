@@ -12,11 +12,19 @@ def pytest_configure(config):
 
 
 def pytest_collection_modifyitems(session, config, items):
-    """The multi-process tests (tests/test_shard.py: ranks that share the one
-    GPU) run first, while this pytest process holds no GPU state of its own:
-    after the in-process GPU tests, 8 rank processes sharing the GPU next to
-    it were measured to crawl (instance generation 4 s -> > 300 s; no memory
-    pressure), in isolation they finish in seconds."""
+    """The multi-process tests (tests/test_shard.py: up to 8 rank processes
+    sharing the one GPU) run first, while this pytest process holds no GPU
+    state.  Measured cause (tools/crawl_probe.py, DESIGN.md 4 "The shard-test
+    crawl"): a bystander process on the same GPU that has run a pnp proof —
+    even after closing its context, even limited to one hardware queue — or
+    that has used four torch streams makes the 8 ranks time-share the GPU
+    (they advance one or two at a time: a 10 s job takes > 150 s); a bystander
+    that only holds a HIP context, one extra stream of any priority, or an
+    unused pnp context does not, nor do 9 ranks alone, and the CPU (no cgroup
+    throttling) and HBM are not involved.  A process cannot hand its HIP state
+    back without exiting, so the in-process GPU tests come after the ranks;
+    tests/test_shard.py refuses (fails at once, with this reason) to start 4 or
+    more ranks beside a pytest process that has loaded the library."""
     if os.environ.get("PNP_TEST_ORDER") == "natural":  # (the crawl experiment)
         return
     first = [it for it in items if it.nodeid.startswith("tests/test_shard.py")]

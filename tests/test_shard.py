@@ -23,7 +23,21 @@ def _free_port():
         return s.getsockname()[1]
 
 
+def _bystander_state():
+    """GPU state of this (pytest) process that makes co-resident rank
+    processes time-share the GPU (conftest.py): the library
+    loaded here, i.e. an in-process GPU test ran before the ranks"""
+    pnp = sys.modules.get("pnp")
+    if pnp is not None and getattr(pnp, "_LIB", None) is not None:
+        return "this pytest process has loaded libpnp_plonk.so (an in-process GPU test ran first)"
+    return None
+
+
 def _launch(world, args, tmp_path, timeout, **extra_env):
+    why = _bystander_state() if args[0] != "cpu" else None
+    if why and world >= 4 and os.environ.get("PNP_TEST_ORDER") != "natural":
+        pytest.fail(f"{world} ranks would share the GPU with a bystander: {why}; they would time-share it "
+                    "and crawl (DESIGN.md 4) — run tests/test_shard.py first (conftest.py does by default)")
     port = _free_port()
     procs = []
     for r in range(world):
@@ -79,6 +93,34 @@ def _launch(world, args, tmp_path, timeout, **extra_env):
                 p.kill()
     for p, o in zip(procs, outs):
         assert p.returncode == 0, o[-3000:]
+
+
+def kfd_queue_census_by_gpu():
+    """{gpu_id: {pid: [queue types]}} from the KFD's sysfs
+    (/sys/class/kfd/kfd/proc/<pid>/queues/<id>/{gpuid,type}): every process on
+    the machine, grouped by the GPU its queues are on; {} where unreadable"""
+    out = {}
+    base = "/sys/class/kfd/kfd/proc"
+    try:
+        pids = os.listdir(base)
+    except OSError:
+        return out
+    for pid in pids:
+        qdir = os.path.join(base, pid, "queues")
+        try:
+            qids = os.listdir(qdir)
+        except OSError:
+            continue
+        for q in qids:
+            try:
+                with open(os.path.join(qdir, q, "gpuid")) as f:
+                    gid = f.read().strip()
+                with open(os.path.join(qdir, q, "type")) as f:
+                    typ = f.read().strip()
+            except OSError:
+                continue
+            out.setdefault(gid, {}).setdefault(pid, []).append(typ)
+    return out
 
 
 def kfd_queue_census():

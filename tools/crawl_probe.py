@@ -14,8 +14,13 @@ in one of these ways, each in a fresh process, one JSON line each:
   lo8        parent holds torch + ONE lowest-priority stream that ran a kernel
   norm8      parent holds torch + three normal-priority streams that ran kernels
   hi8        parent holds torch + ONE highest-priority stream that ran a kernel
+  low8       parent holds torch + ONE stream at HIP's least priority (ctypes)
+  pnpctx8    parent holds torch + a pnp context that did nothing yet
+  pnphi8     as pnp8 with the side stream at the highest priority and no
+             deferred table build (so no least-priority stream at all)
 
-CRAWL_RANK_QUEUES=Q starts the ranks with GPU_MAX_HW_QUEUES=Q.  Every line
+CRAWL_RANK_QUEUES=Q starts the ranks with GPU_MAX_HW_QUEUES=Q, CRAWL_PARENT_QUEUES=Q
+sets it for the parent alone (the ranks keep the box's value).  Every line
 carries the peak KFD queue census (sysfs) seen while the ranks ran.
 
     python tools/crawl_probe.py [config ...]   (default: the first four)
@@ -61,16 +66,19 @@ def run(name, world):
     peak = {"total": 0, "procs": 0, "parent": 0}
     stop = threading.Event()
 
-    def sample():  # the KFD queue census while the ranks live
+    def sample():  # the KFD queue census while the ranks live, per GPU
         while not stop.is_set():
             qs = test_shard.kfd_queue_census()
             if sum(qs.values()) > peak["total"]:
                 peak.update(total=sum(qs.values()), procs=len(qs), parent=qs.get(os.getpid(), 0),
                             per_process=sorted(qs.values()))
+                byg = test_shard.kfd_queue_census_by_gpu()
+                # per GPU: each process's queue types (the GPU with the ranks is the busy one)
+                peak["by_gpu"] = {g: sorted(",".join(sorted(t)) for t in pq.values()) for g, pq in byg.items()}
             stop.wait(1.0)
     th = threading.Thread(target=sample, daemon=True)
     th.start()
-    extra = {"GPU_MAX_HW_QUEUES": os.environ["CRAWL_RANK_QUEUES"]} if os.environ.get("CRAWL_RANK_QUEUES") else {}
+    extra = {"GPU_MAX_HW_QUEUES": os.environ.get("CRAWL_RANK_QUEUES", os.environ.get("CRAWL_QUEUES0", "4"))}
     with open(os.path.join(REPO, "tests", "golden", "merkle_h13_seed1.json")) as f:
         g = json.load(f)
     tmp = pathlib.Path(tempfile.mkdtemp(prefix=f"crawl_{name}_"))
@@ -85,6 +93,7 @@ def run(name, world):
     except Exception as e:  # a rank that failed or passed the limit
         ok, err = False, repr(e)[-400:]
     dt = time.time() - t0
+    print(json.dumps({"config": name, "ranks_done_s": round(dt, 1), "ok": ok, "error": err[-200:]}), flush=True)
     stop.set()
     th.join()
     lines = {}
@@ -94,6 +103,7 @@ def run(name, world):
         except OSError:
             pass
     rec = {"config": name, "ranks": world, "rank_hw_queues_env": extra.get("GPU_MAX_HW_QUEUES"),
+           "parent_hw_queues_env": os.environ.get("CRAWL_PARENT_QUEUES"),
            "queue_census_peak": peak, "seconds": round(dt, 1), "ok": ok, "crawled": dt >= LIMIT - 5,
            "kfd_processes_after": kfd_holders(), "error": err, "rank_tail": {0: lines.get(0), world - 1: lines.get(world - 1)}}
     print(json.dumps(rec), flush=True)
@@ -102,6 +112,8 @@ def run(name, world):
 
 def one(c):
     """set this (fresh) process up as configuration c, then run the ranks"""
+    if os.environ.get("CRAWL_PARENT_QUEUES"):  # this process only; the ranks get theirs below
+        os.environ["GPU_MAX_HW_QUEUES"] = os.environ["CRAWL_PARENT_QUEUES"]
     if c not in ("clean8", "clean9"):
         import torch
         torch.cuda.init()
@@ -120,7 +132,24 @@ def one(c):
             globals()["_streams"] = streams
             print(json.dumps({"config": c, "priority_range": [lo, hi], "priorities": prios}), flush=True)
         torch.cuda.synchronize()
-    if c in ("pnp8", "closed8"):
+    if c == "low8":  # one stream at HIP's LEAST priority (torch's range stops at normal)
+        import ctypes
+        hip = ctypes.CDLL("libamdhip64.so")
+        lo, hi = ctypes.c_int(), ctypes.c_int()
+        hip.hipDeviceGetStreamPriorityRange(ctypes.byref(lo), ctypes.byref(hi))
+        st = ctypes.c_void_p()
+        assert hip.hipStreamCreateWithPriority(ctypes.byref(st), 1, lo) == 0
+        assert hip.hipMemsetAsync(ctypes.c_void_p(x.data_ptr()), 0, 1 << 20, st) == 0
+        assert hip.hipStreamSynchronize(st) == 0
+        globals()["_lo_stream"] = st
+        print(json.dumps({"config": c, "hip_priority_range": [lo.value, hi.value], "priority": lo.value}), flush=True)
+    if c == "pnphi8":  # the pnp context without a least-priority stream
+        os.environ["PNP_SIDE_PRIORITY"] = "hi"
+        os.environ["PNP_DEFER_TABLES"] = "0"
+    if c == "pnpctx8":  # a pnp context and nothing else (one stream)
+        import pnp
+        globals()["_keep"] = pnp.Context(0)
+    if c in ("pnp8", "closed8", "pnphi8"):
         import pnp
         from pnp_testlib import Inputs
         inp = Inputs(10, 3)
@@ -133,16 +162,29 @@ def one(c):
             ctx.close()
         else:
             globals()["_keep"] = ctx  # held like a test's context until the process ends
+    print(json.dumps({"config": c, "parent_set_up": True}), flush=True)
     return 0 if run(c, 9 if c == "clean9" else 8) else 1
 
 
+def one_logged(c):
+    import traceback
+    try:
+        return one(c)
+    except BaseException:
+        print(json.dumps({"config": c, "exception": traceback.format_exc()[-1500:]}), flush=True)
+        raise
+
+
 def main():
+    # the ranks' default: this process's own setting before any knob (4 on the box)
+    os.environ.setdefault("CRAWL_QUEUES0", os.environ.get("GPU_MAX_HW_QUEUES", "4"))
     if len(sys.argv) > 2 and sys.argv[1] == "--one":
-        return one(sys.argv[2])
+        return one_logged(sys.argv[2])
     configs = sys.argv[1:] or ["clean8", "clean9", "ctx8", "pnp8"]
     for c in configs:
-        rc = subprocess.run([sys.executable, "-u", os.path.abspath(__file__), "--one", c],
+        rc = subprocess.run([sys.executable, "-u", "-X", "faulthandler", os.path.abspath(__file__), "--one", c],
                             timeout=LIMIT + 240).returncode
+        print(json.dumps({"config": c, "child_rc": rc}), flush=True)
         if rc and os.environ.get("CRAWL_GO_ON") != "1":
             print(json.dumps({"stopped_after": c}), flush=True)
             return 1

@@ -48,15 +48,18 @@ constexpr uint32_t KEY_ZERO = 0xFFFFFFFFu;
 // KEY_ZERO for a zero digit), row w of keys at keys[w n + i]; fn(key) per digit
 // top_sh (folded tables, MsmCfg::top_sh): the top window's digit d becomes
 // magnitude d 2^top_sh (its table level is divided by 2^top_sh)
-template <class F>
-__device__ __forceinline__ void scalar_digits(const uint64_t *scalars, uint64_t i, uint64_t n, int c, int W,
-                                              int top_sh, uint32_t *keys, F fn) {
-    Fr s = from_mont(load_fr(scalars, i));
+// C > 0: the window width known at compile time (c = 20, every folded MSM
+// from 2^19 points): the limb index and shift of every window fold to
+// constants, no selects (~20 VALU per digit less)
+template <int C, class E>
+__device__ __forceinline__ void digits_of(const Fr &s, int c_rt, int W_rt, int top_sh, E emit) {
+    const int c = C > 0 ? C : c_rt;
+    const int W = C > 0 ? (255 + C) / C : W_rt;
     const uint32_t NB = 1u << (c - 1);
     uint32_t carry = 0;
-    for (int w = 0; w < W; w++) {
-        int bit = w * c;
-        int li = bit >> 5, sh = bit & 31;
+    auto digit = [&](int w) {
+        const int bit = w * c;
+        const int li = bit >> 5, sh = bit & 31;
         // limbs li, li + 1 by selects (a dynamic register index would go to scratch)
         uint32_t lo32 = 0, hi32 = 0;
 #pragma unroll
@@ -64,12 +67,12 @@ __device__ __forceinline__ void scalar_digits(const uint64_t *scalars, uint64_t 
             lo32 = li == k ? s.v[k] : lo32;
             hi32 = li + 1 == k ? s.v[k] : hi32;
         }
-        uint64_t word = lo32 | ((uint64_t)hi32 << 32);
+        const uint64_t word = lo32 | ((uint64_t)hi32 << 32);
         uint32_t raw = (uint32_t)(word >> sh) & ((1u << c) - 1);
         raw += carry;
         uint32_t key = KEY_ZERO;
         if (raw > NB) {
-            uint32_t mag = (NB << 1) - raw;  // |raw - 2^c|, 0 when raw = 2^c
+            const uint32_t mag = (NB << 1) - raw;  // |raw - 2^c|, 0 when raw = 2^c
             carry = 1;
             if (mag) key = (mag - 1) | 0x80000000u;
         } else {
@@ -77,9 +80,27 @@ __device__ __forceinline__ void scalar_digits(const uint64_t *scalars, uint64_t 
             if (raw) key = (w == W - 1 ? raw << top_sh : raw) - 1;
         }
         // the top window never carries: W c >= 255 + 1 for the configured c (scalars < 2^255)
+        emit(w, key);
+    };
+    if constexpr (C > 0) {
+#pragma unroll
+        for (int w = 0; w < (255 + C) / C; w++) digit(w);
+    } else {
+        for (int w = 0; w < W; w++) digit(w);
+    }
+}
+template <class F>
+__device__ __forceinline__ void scalar_digits(const uint64_t *scalars, uint64_t i, uint64_t n, int c, int W,
+                                              int top_sh, uint32_t *keys, F fn) {
+    const Fr s = from_mont(load_fr(scalars, i));
+    auto emit = [&](int w, uint32_t key) {
         keys[(uint64_t)w * n + i] = key;
         fn(key);
-    }
+    };
+    if (c == 20 && W == 13)
+        digits_of<20>(s, c, W, top_sh, emit);
+    else
+        digits_of<0>(s, c, W, top_sh, emit);
 }
 __global__ void k_digits(const uint64_t *scalars, uint64_t n, int c, int W, int top_sh, uint32_t *keys) {
     uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
