@@ -294,9 +294,31 @@ static_assert(TILE_K % 4096 == 0 && TILE_K <= 16384, "PNP_TILE_K: a multiple of 
 // totals through LDS (wsum: blockDim / 64 words).  Every lane must call it; the
 // caller synchronises after it.  (PNP_SORT_SCAN=0: wave 0 alone, 32 bins per
 // lane in sequence at 2048 fine bins while 15 waves wait at the barrier)
+// (PNP_SORT_SCAN=1: the wave scan by __shfl_up, ds_bpermute through the LDS
+// crossbar, and the wave totals summed one LDS read after another; 2: DPP
+// row shifts / broadcasts in the VALU, and the totals of the <= 16 waves read
+// once per lane and scanned the same way)
 #ifndef PNP_SORT_SCAN
-#define PNP_SORT_SCAN 1
+#define PNP_SORT_SCAN 2
 #endif
+// inclusive scan over the 64 lanes of a wave by DPP: row_shr 1, 2, 4, 8 inside
+// each row of 16 lanes, then row_bcast:15 and row_bcast:31 carry the row totals
+__device__ __forceinline__ uint32_t wave_scan_incl(uint32_t x) {
+    const uint32_t lane = threadIdx.x & 63, rl = lane & 15;
+    uint32_t t = (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x111, 0xf, 0xf, false);  // row_shr:1
+    if (rl >= 1) x += t;
+    t = (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x112, 0xf, 0xf, false);  // row_shr:2
+    if (rl >= 2) x += t;
+    t = (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x114, 0xf, 0xf, false);  // row_shr:4
+    if (rl >= 4) x += t;
+    t = (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x118, 0xf, 0xf, false);  // row_shr:8
+    if (rl >= 8) x += t;
+    t = (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x142, 0xf, 0xf, false);  // row_bcast:15
+    if ((lane & 31) >= 16) x += t;
+    t = (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x143, 0xf, 0xf, false);  // row_bcast:31
+    if (lane >= 32) x += t;
+    return x;
+}
 __device__ __forceinline__ void tile_scan_wave0(uint32_t *lh, uint32_t *lofs, int nb);
 __device__ __forceinline__ void tile_scan(uint32_t *lh, uint32_t *lofs, int nb, uint32_t *wsum) {
 #if PNP_SORT_SCAN
@@ -304,6 +326,16 @@ __device__ __forceinline__ void tile_scan(uint32_t *lh, uint32_t *lofs, int nb, 
     uint32_t loc = 0;
     for (int b = b0; b < b0 + per && b < nb; b++) loc += lh[b];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+#if PNP_SORT_SCAN == 2
+    const uint32_t x = wave_scan_incl(loc);
+    if (lane == 63) wsum[wv] = x;
+    __syncthreads();
+    // the waves before this one: every lane reads one wave total, one more scan
+    const int nw = (int)blockDim.x >> 6;
+    const uint32_t wt = wave_scan_incl(lane < nw ? wsum[lane] : 0u);
+    const int wsrc = __builtin_amdgcn_readfirstlane(wv) - 1;
+    uint32_t run = x - loc + (wsrc >= 0 ? (uint32_t)__builtin_amdgcn_readlane((int)wt, wsrc) : 0u);
+#else
     uint32_t x = loc;
     for (int off = 1; off < 64; off <<= 1) {
         const uint32_t y = __shfl_up(x, off, 64);
@@ -313,6 +345,7 @@ __device__ __forceinline__ void tile_scan(uint32_t *lh, uint32_t *lofs, int nb, 
     __syncthreads();
     uint32_t run = x - loc;
     for (int j = 0; j < wv; j++) run += wsum[j];
+#endif
     for (int b = b0; b < b0 + per && b < nb; b++) {
         lofs[b] = run;
         run += lh[b];
