@@ -328,3 +328,20 @@ def test_hbm_short_rank_fails_every_load(tmp_path, world):
     _launch(world, ["hbm", prefix, "10", "5"], tmp_path, 300, PNP_TEST_SHORT_RANK=str(world - 1))
     for r in range(world):
         assert open(f"{prefix}.{r}").read() == "ok", f"rank {r}"
+
+
+def test_bystander_guard(tmp_path, monkeypatch):
+    """4+ ranks beside a pytest process that has loaded the library fail at
+    once with the reason (the shard-test crawl), instead of
+    time-sharing the GPU into a timeout; fewer ranks, the CPU exchange test
+    and the crawl experiment's natural order are let through."""
+    import types
+    fake = types.ModuleType("pnp")
+    fake._LIB = object()
+    monkeypatch.setitem(sys.modules, "pnp", fake)
+    monkeypatch.delenv("PNP_TEST_ORDER", raising=False)
+    assert "loaded libpnp_plonk.so" in _bystander_state()
+    with pytest.raises(pytest.fail.Exception, match="bystander"):
+        _launch(4, ["gpu", str(tmp_path / "x"), "13", "3"], tmp_path, 5)
+    fake._LIB = None
+    assert _bystander_state() is None
