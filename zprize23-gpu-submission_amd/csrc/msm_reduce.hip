@@ -136,8 +136,12 @@ void msm_merge_pieces(const uint32_t *offs, int nch, uint64_t U, uint32_t S, uin
 // pieces (clustered or repeated scalars, a short top window) is not summed
 // here, where one lane would add its pieces one after another, but queued
 // for k_merge_heavy29.
+// (16, not 64: a bucket of 16-63 pieces was one lane's chain of dependent
+// additions — at 8 ranks the wires' repeated values made round 1's merge a
+// 0.85 ms chain; same box, solo rank 0 of 8: 30.2 -> 29.5 ms per proof, one
+// GPU neutral, profiles/r05_ab_merge_heavy.txt)
 #ifndef PNP_MERGE_HEAVY
-#define PNP_MERGE_HEAVY 64
+#define PNP_MERGE_HEAVY 16
 #endif
 constexpr uint32_t MERGE_HEAVY = PNP_MERGE_HEAVY;
 // One merge lane per listed tail (tlist: the accumulation lanes that left
@@ -163,7 +167,8 @@ __global__ __launch_bounds__(256) void k_merge_tails29(const uint32_t *offs, uin
 }
 
 // the queued heavy buckets, one workgroup each (grid-stride over the queue):
-// 256 lanes sum every 256th piece, then an 8-level LDS tree
+// 256 lanes sum every 256th piece, then an LDS tree of log2 of the lanes that
+// hold a piece (8 levels from 128 pieces on, 4 for a bucket of 16)
 __global__ __launch_bounds__(256) void k_merge_heavy29(const uint32_t *offs, uint32_t S, uint32_t *bk29,
                                                        const uint32_t *head, const uint32_t *tail, uint32_t *exc,
                                                        const uint32_t *heavy, const uint32_t *nheavy) {
@@ -177,7 +182,11 @@ __global__ __launch_bounds__(256) void k_merge_heavy29(const uint32_t *offs, uin
 #pragma unroll 1
         for (uint32_t k = threadIdx.x; k <= t1 - t0; k += blockDim.x)
             acc = xadd29_inf(acc, load_xyzz29(k == 0 ? tail + 56ULL * t0 : head + 56ULL * (t0 + k)), exc);
-        for (uint32_t h = blockDim.x / 2; h >= 1; h /= 2) {
+        // lanes >= the piece count hold infinity: the tree starts at the
+        // power of two that covers the pieces
+        uint32_t h0 = 1;
+        while (2 * h0 < t1 - t0 + 1 && 2 * h0 < blockDim.x) h0 *= 2;
+        for (uint32_t h = h0; h >= 1; h /= 2) {
             store_xyzz29(mine, acc);
             __syncthreads();
             if (threadIdx.x < h) acc = xadd29_inf(acc, load_xyzz29(mine + 56 * h), exc);
