@@ -302,13 +302,84 @@ __device__ __forceinline__ Fr mont_mul2_dev(const Fr &a, const Fr &b, const Fr &
 }
 #endif
 
-// Montgomery product, "no-carry" CIOS on 32-bit limbs (requires the top word
-// of P below 2^31 - 1, true for r and q).  2N^2 v_mad_u64_u32.  Host path;
-// the device uses mont_mul_dev above.
+#ifndef __HIP_DEVICE_COMPILE__
+// Host Montgomery product: CIOS on 64-bit words with 128-bit products (the
+// x86-64 mul gives the full 64x64 product).  The prover's host work between
+// device round trips (challenge arithmetic, the commitments' affine
+// conversion) sits on the proof's critical path: the 32-bit-limb form below
+// cost 121 ns per Fr product, 185 us per Fq inversion.
+template <class P>
+constexpr uint64_t mont_inv64() {  // -P^-1 mod 2^64 (Newton: each step doubles the bits)
+    const uint64_t p0 = (uint64_t)P::P[0] | (uint64_t)P::P[1] << 32;
+    uint64_t x = 1;
+    for (int i = 0; i < 7; i++) x *= 2 - p0 * x;
+    return 0 - x;
+}
+template <class P>
+inline Fp<P> mont_mul_host(const Fp<P> &a, const Fp<P> &b) {
+    constexpr int M = P::N / 2;
+    constexpr uint64_t INV = mont_inv64<P>();
+    typedef unsigned __int128 u128;
+    uint64_t A[M], B[M], Q[M], t[M + 2];
+#pragma unroll
+    for (int j = 0; j < M; j++) {
+        A[j] = (uint64_t)a.v[2 * j] | (uint64_t)a.v[2 * j + 1] << 32;
+        B[j] = (uint64_t)b.v[2 * j] | (uint64_t)b.v[2 * j + 1] << 32;
+        Q[j] = (uint64_t)P::P[2 * j] | (uint64_t)P::P[2 * j + 1] << 32;
+        t[j] = 0;
+    }
+    t[M] = t[M + 1] = 0;
+#pragma unroll
+    for (int i = 0; i < M; i++) {
+        u128 c = 0;
+#pragma unroll
+        for (int j = 0; j < M; j++) {
+            c = (u128)A[j] * B[i] + t[j] + (uint64_t)(c >> 64);
+            t[j] = (uint64_t)c;
+        }
+        c = (u128)t[M] + (uint64_t)(c >> 64);
+        t[M] = (uint64_t)c;
+        t[M + 1] = (uint64_t)(c >> 64);
+        const uint64_t m = t[0] * INV;
+        c = (u128)m * Q[0] + t[0];
+#pragma unroll
+        for (int j = 1; j < M; j++) {
+            c = (u128)m * Q[j] + t[j] + (uint64_t)(c >> 64);
+            t[j - 1] = (uint64_t)c;
+        }
+        c = (u128)t[M] + (uint64_t)(c >> 64);
+        t[M - 1] = (uint64_t)c;
+        t[M] = t[M + 1] + (uint64_t)(c >> 64);
+    }
+    // CIOS leaves [0, 2P) (t[M] = 0 for a, b < P < R / 4): one conditional
+    // subtraction, on the 64-bit words
+    uint64_t d[M], br = 0;
+#pragma unroll
+    for (int j = 0; j < M; j++) {
+        const u128 x = (u128)t[j] - Q[j] - br;
+        d[j] = (uint64_t)x;
+        br = (uint64_t)(x >> 64) & 1;
+    }
+    Fp<P> r;
+#pragma unroll
+    for (int j = 0; j < M; j++) {
+        const uint64_t w = br ? t[j] : d[j];
+        r.v[2 * j] = (uint32_t)w;
+        r.v[2 * j + 1] = (uint32_t)(w >> 32);
+    }
+    return r;
+}
+#endif
+
+// Montgomery product: mont_mul_dev on the device, mont_mul_host on the host.
+// (The "no-carry" CIOS on 32-bit limbs after the return was the host path;
+// it is kept only for host builds without a 128-bit integer type.)
 template <class P>
 PNP_HD Fp<P> operator*(const Fp<P> &a, const Fp<P> &b) {
 #ifdef __HIP_DEVICE_COMPILE__
     return mont_mul_dev(a, b);
+#elif defined(__SIZEOF_INT128__)
+    return mont_mul_host(a, b);
 #endif
     constexpr int N = P::N;
     uint32_t t[N];
@@ -390,9 +461,104 @@ PNP_HD Fp<P> pow_u64(Fp<P> base, uint64_t e) {
     return acc;
 }
 
-// Fermat inverse a^(P-2); inv(0) = 0 (inv_mod_kernel_, mont_arithmetic.cu:73)
+#ifndef __HIP_DEVICE_COMPILE__
+// Host inverse by the binary extended Euclidean algorithm on 64-bit words
+// (~2 log2 P shift / subtract steps instead of Fermat's ~1.5 log2 P dependent
+// products: an Fq inverse in a few us, not ~65).  The host inverts public
+// values only (challenge arithmetic, the commitments' affine conversion), so
+// its data-dependent time leaks nothing.  Montgomery form in and out: the
+// plain inverse of aR is a^-1 R^-1, and one product by R^3 gives a^-1 R.
+template <class P>
+inline Fp<P> inverse_host(const Fp<P> &a) {
+    constexpr int M = P::N / 2;
+    typedef unsigned __int128 u128;
+    if (a.is_zero()) return a;
+    uint64_t u[M], v[M], x1[M], x2[M], q[M];
+    for (int j = 0; j < M; j++) {
+        u[j] = (uint64_t)a.v[2 * j] | (uint64_t)a.v[2 * j + 1] << 32;
+        q[j] = v[j] = (uint64_t)P::P[2 * j] | (uint64_t)P::P[2 * j + 1] << 32;
+        x1[j] = x2[j] = 0;
+    }
+    x1[0] = 1;
+    auto is_one = [](const uint64_t *w) {
+        uint64_t acc = w[0] ^ 1;
+        for (int j = 1; j < M; j++) acc |= w[j];
+        return acc == 0;
+    };
+    auto shr1 = [](uint64_t *w, uint64_t top) {  // w = (top:w) >> 1
+        for (int j = 0; j < M - 1; j++) w[j] = (w[j] >> 1) | (w[j + 1] << 63);
+        w[M - 1] = (w[M - 1] >> 1) | (top << 63);
+    };
+    auto halve = [&](uint64_t *x) {  // x / 2 mod P (x < P)
+        uint64_t c = 0;
+        if (x[0] & 1) {
+            u128 t = 0;
+            for (int j = 0; j < M; j++) {
+                t = (u128)x[j] + q[j] + (uint64_t)(t >> 64);
+                x[j] = (uint64_t)t;
+            }
+            c = (uint64_t)(t >> 64);
+        }
+        shr1(x, c);
+    };
+    auto sub = [](uint64_t *r, const uint64_t *b) {  // r -= b, borrow out
+        uint64_t br = 0;
+        for (int j = 0; j < M; j++) {
+            const u128 t = (u128)r[j] - b[j] - br;
+            r[j] = (uint64_t)t;
+            br = (uint64_t)(t >> 64) & 1;
+        }
+        return br;
+    };
+    auto geq = [](const uint64_t *x, const uint64_t *y) {
+        for (int j = M - 1; j >= 0; j--)
+            if (x[j] != y[j]) return x[j] > y[j];
+        return true;
+    };
+    auto sub_mod = [&](uint64_t *r, const uint64_t *b) {  // r = r - b mod P
+        if (sub(r, b)) {
+            u128 t = 0;
+            for (int j = 0; j < M; j++) {
+                t = (u128)r[j] + q[j] + (uint64_t)(t >> 64);
+                r[j] = (uint64_t)t;
+            }
+        }
+    };
+    while (!is_one(u) && !is_one(v)) {
+        while (!(u[0] & 1)) {
+            shr1(u, 0);
+            halve(x1);
+        }
+        while (!(v[0] & 1)) {
+            shr1(v, 0);
+            halve(x2);
+        }
+        if (geq(u, v)) {
+            sub(u, v);
+            sub_mod(x1, x2);
+        } else {
+            sub(v, u);
+            sub_mod(x2, x1);
+        }
+    }
+    const uint64_t *x = is_one(u) ? x1 : x2;
+    Fp<P> r;
+    for (int j = 0; j < M; j++) {
+        r.v[2 * j] = (uint32_t)x[j];
+        r.v[2 * j + 1] = (uint32_t)(x[j] >> 32);
+    }
+    const Fp<P> r3 = mont_mul_host(Fp<P>::r2(), Fp<P>::r2());  // R^3 mod P
+    return mont_mul_host(r, r3);
+}
+#endif
+
+// Fermat inverse a^(P-2); inv(0) = 0 (inv_mod_kernel_, mont_arithmetic.cu:73).
+// The host takes inverse_host above.
 template <class P>
 PNP_HD Fp<P> inverse(const Fp<P> &a) {
+#if !defined(__HIP_DEVICE_COMPILE__) && defined(__SIZEOF_INT128__)
+    return inverse_host(a);
+#endif
     Fp<P> acc = Fp<P>::one();
     for (int w = P::N - 1; w >= 0; w--) {
         uint32_t e = P::PM2[w];

@@ -263,6 +263,14 @@ void k_poly_eval(const uint64_t *d, uint64_t n, const Fr &x, DevBuf &scratch, Fr
 // several polys (same n) at the same point in one launch
 void k_poly_eval_multi(const uint64_t *const *polys, int npolys, uint64_t n, const Fr &x,
                        DevBuf &scratch, Fr *out, hipStream_t s);
+// several such sets (each its own point), one host round trip for all
+struct EvalSet {
+    const uint64_t *const *polys;
+    int np;
+    Fr x;
+    Fr *out;
+};
+void k_poly_eval_sets(const EvalSet *sets, int nsets, uint64_t n, DevBuf &scratch, hipStream_t s);
 void k_poly_div_linear(uint64_t *d, uint64_t n, const Fr &z, DevBuf &scratch, hipStream_t s);
 // d[i] += c z^(len-1-i)
 void k_add_powers(uint64_t *d, uint64_t len, const Fr &c, const Fr &z, hipStream_t s);

@@ -220,8 +220,11 @@ void k_poly_div_linear(uint64_t *d, uint64_t n, const Fr &z, DevBuf &scratch, hi
 // lane instead of the full x^lo power per 32-coefficient chunk of the
 // previous layout (which cost more products than the Horner steps).
 static constexpr int EV_K = 32;
+struct EvalPtrs {  // up to 8 polys, by value in the kernel arguments (no upload)
+    const uint64_t *p[8];
+};
 template <int NP>
-__global__ __launch_bounds__(256) void k_eval_partial(const uint64_t *const *polys, uint64_t n, Fr x,
+__global__ __launch_bounds__(256) void k_eval_partial(EvalPtrs polys, uint64_t n, Fr x,
                                                       Fr x256, Fr xblk, uint64_t *partial) {
     __shared__ uint4 red_lo[256], red_hi[256];
     const uint64_t base = (uint64_t)blockIdx.x * 256 * EV_K + threadIdx.x;
@@ -233,7 +236,7 @@ __global__ __launch_bounds__(256) void k_eval_partial(const uint64_t *const *pol
         const uint64_t i = base + 256ull * k;
         if (i < n) {
 #pragma unroll
-            for (int p = 0; p < NP; p++) h[p] = h[p] * x256 + load_fr(polys[p], i);
+            for (int p = 0; p < NP; p++) h[p] = h[p] * x256 + load_fr(polys.p[p], i);
         } else {
 #pragma unroll
             for (int p = 0; p < NP; p++) h[p] = h[p] * x256;
@@ -293,38 +296,54 @@ __global__ __launch_bounds__(256) void k_sum_partials(const uint64_t *partial, u
     }
 }
 
-void k_poly_eval_multi(const uint64_t *const *polys, int npolys, uint64_t n, const Fr &x,
-                       DevBuf &scratch, Fr *out, hipStream_t s) {
-    if (npolys <= 0) return;
+void k_poly_eval_sets(const EvalSet *sets, int nsets, uint64_t n, DevBuf &scratch, hipStream_t s) {
+    int total = 0;
+    for (int k = 0; k < nsets; k++) total += std::max(sets[k].np, 0);
+    if (total == 0) return;
     const uint32_t nb = (uint32_t)std::max<uint64_t>(1, (n + 256 * EV_K - 1) / (256 * EV_K));
-    const Fr x256 = pow_u64(x, 256), xblk = pow_u64(x, 256ull * EV_K);
-    // layout: [8 poly pointers][partials np*nb][results np]
-    size_t need = 64 * 8 + (size_t)npolys * nb * 32 + (size_t)npolys * 32 + 64;
+    // layout: [partials total*nb][results total]: every group of up to 8 polys
+    // has its own slice, so all launch back to back and ONE copy and ONE
+    // synchronisation return every value (round 5 evaluates 18 polys at two
+    // points: four host round trips before)
+    size_t need = (size_t)total * nb * 32 + (size_t)total * 32 + 64;
     if (scratch.bytes < need) scratch.alloc(need);
-    uint64_t *base = scratch.u64();
-    const uint64_t **dptrs = reinterpret_cast<const uint64_t **>(base);
-    uint64_t *partial = base + 64;
-    uint64_t *res = partial + (size_t)npolys * nb * 4;
-    std::vector<Fr> host((size_t)npolys);
-    for (int p0 = 0; p0 < npolys; p0 += 8) {
-        int np = npolys - p0 < 8 ? npolys - p0 : 8;
-        PNP_HIP(hipMemcpyAsync(dptrs, polys + p0, sizeof(void *) * np, hipMemcpyHostToDevice, s));
-        uint64_t *pt = partial;
-        switch (np) {
+    uint64_t *partial = scratch.u64();
+    uint64_t *res = partial + (size_t)total * nb * 4;
+    int q = 0;  // polys launched so far
+    for (int k = 0; k < nsets; k++) {
+        const Fr &x = sets[k].x;
+        const Fr x256 = pow_u64(x, 256), xblk = pow_u64(x, 256ull * EV_K);
+        for (int p0 = 0; p0 < sets[k].np; p0 += 8) {
+            const int np = std::min(sets[k].np - p0, 8);
+            EvalPtrs ptrs = {};
+            for (int j = 0; j < np; j++) ptrs.p[j] = sets[k].polys[p0 + j];
+            uint64_t *pt = partial + (size_t)q * nb * 4;
+            switch (np) {
 #define PNP_EV(K)                                                                                 \
     case K:                                                                                       \
-        hipLaunchKernelGGL(k_eval_partial<K>, dim3(nb), dim3(256), 0, s, dptrs, n, x, x256, xblk, pt); \
+        hipLaunchKernelGGL(k_eval_partial<K>, dim3(nb), dim3(256), 0, s, ptrs, n, x, x256, xblk, pt); \
         break;
-            PNP_EV(1) PNP_EV(2) PNP_EV(3) PNP_EV(4) PNP_EV(5) PNP_EV(6) PNP_EV(7) PNP_EV(8)
+                PNP_EV(1) PNP_EV(2) PNP_EV(3) PNP_EV(4) PNP_EV(5) PNP_EV(6) PNP_EV(7) PNP_EV(8)
 #undef PNP_EV
+            }
+            PNP_HIP(hipGetLastError());
+            hipLaunchKernelGGL(k_sum_partials, dim3(np), dim3(256), 0, s, pt, (uint64_t)nb, res + 4 * q);
+            PNP_HIP(hipGetLastError());
+            q += np;
         }
-        PNP_HIP(hipGetLastError());
-        hipLaunchKernelGGL(k_sum_partials, dim3(np), dim3(256), 0, s, pt, (uint64_t)nb, res);
-        PNP_HIP(hipGetLastError());
-        PNP_HIP(hipMemcpyAsync(host.data() + p0, res, 32 * np, hipMemcpyDeviceToHost, s));
-        PNP_HIP(hipStreamSynchronize(s));  // dptrs / partial reused by the next group
     }
-    for (int p = 0; p < npolys; p++) out[p] = host[p];
+    std::vector<Fr> host((size_t)total);
+    PNP_HIP(hipMemcpyAsync(host.data(), res, 32 * (size_t)total, hipMemcpyDeviceToHost, s));
+    PNP_HIP(hipStreamSynchronize(s));
+    q = 0;
+    for (int k = 0; k < nsets; k++)
+        for (int p = 0; p < sets[k].np; p++) sets[k].out[p] = host[q++];
+}
+
+void k_poly_eval_multi(const uint64_t *const *polys, int npolys, uint64_t n, const Fr &x,
+                       DevBuf &scratch, Fr *out, hipStream_t s) {
+    const EvalSet set = {polys, npolys, x, out};
+    k_poly_eval_sets(&set, 1, n, scratch, s);
 }
 
 void k_poly_eval(const uint64_t *d, uint64_t n, const Fr &x, DevBuf &scratch, Fr *out,

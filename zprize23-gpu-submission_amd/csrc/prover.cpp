@@ -92,11 +92,11 @@ void div_linear_range(pnp_ctx *ctx, uint64_t *const *d, const Fr *z, int K, uint
     }
     const int world = ctx->msm.world, rank = ctx->msm.rank;
     std::vector<uint64_t> mine(4 * K);
-    for (int k = 0; k < K; k++) {
-        Fr e;
-        k_poly_eval(d[k], len, z[k], ctx->scratch_a, &e, s);
-        to_u64_limbs(e, &mine[4 * k]);
-    }
+    std::vector<Fr> e(K);
+    std::vector<EvalSet> sets(K);
+    for (int k = 0; k < K; k++) sets[k] = {d + k, 1, z[k], &e[k]};
+    k_poly_eval_sets(sets.data(), K, len, ctx->scratch_a, s);
+    for (int k = 0; k < K; k++) to_u64_limbs(e[k], &mine[4 * k]);
     std::vector<uint64_t> all = shard_allgather(ctx, mine.data(), 4 * K, PNP_EX_TAG_DIV_CARRY);
     const uint64_t n = len * world;  // equal ranges (world divides 8 and n)
     for (int k = 0; k < K; k++) {
@@ -777,14 +777,13 @@ int prove_impl(pnp_ctx *ctx, const CircuitC *cs, int device_ptrs, ProofC *out, c
                                       pk.out_sigma_coeffs + eo, pk.q_arith_coeffs + eo, pk.q_c_coeffs + eo,
                                       pk.q_l_coeffs + eo, pk.q_r_coeffs + eo, pk.q_hl_coeffs + eo};
             Fr rz[12];
-            k_poly_eval_multi(pz, 12, len, zc, ctx->scratch_a, rz, s);
             const uint64_t *pz2[2] = {pk.q_hr_coeffs + eo, pk.q_h4_coeffs + eo};
             Fr rz2[2];
-            k_poly_eval_multi(pz2, 2, len, zc, ctx->scratch_a, rz2, s);
             // evaluations at z * omega
             const uint64_t *pw[4] = {z_poly + eo, wpoly[0] + eo, wpoly[1] + eo, wpoly[3] + eo};
             Fr rw[4];
-            k_poly_eval_multi(pw, 4, len, zw, ctx->scratch_a, rw, s);
+            const EvalSet sets[3] = {{pz, 12, zc, rz}, {pz2, 2, zc, rz2}, {pw, 4, zw, rw}};
+            k_poly_eval_sets(sets, 3, len, ctx->scratch_a, s);  // one host round trip
             alg(18.0 * len);
             if (dist) {
                 Fr *vals[18];
