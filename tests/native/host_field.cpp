@@ -2,7 +2,9 @@
 // arithmetic and the commitments' affine conversion run on the host): prints
 // seeded operands with their Montgomery product and inverse, one line each,
 // for tests/test_host_field.py to check with Python integers.
-//   host_field <count>   ->  "r|q a b a*b inv(a)" (hex limbs, Montgomery form)
+//   host_field <count>   ->  "r|q a b a*b inv(a)" (hex limbs, Montgomery form),
+//                            then "b a fr_inverse_bin(a)" (the device's batch-
+//                            inverse base case, same source on the host)
 #include "field.cuh"
 #include <cstdio>
 #include <cstdlib>
@@ -47,5 +49,11 @@ int main(int argc, char **argv) {
     const int count = argc > 1 ? atoi(argv[1]) : 200;
     run<FrP>("r", count);
     run<FqP>("q", count);
+    for (int k = 0; k < count; k++) {
+        const Fr a = draw<FrP>(k);
+        printf("b");
+        hex(a), hex(fr_inverse_bin(a));
+        printf("\n");
+    }
     return 0;
 }

@@ -8,6 +8,8 @@ Euclidean inverse (mont_mul_host / inverse_host).  tests/native/host_field.cpp
 prints seeded operands (zero, one, -1, the raw integer 1, P - 2 and random
 residues) with a*b and inv(a); here each line is checked exactly:
 a*b == a b R^-1 mod P and a * inv(a) == R^2 mod P (Montgomery forms), inv(0) = 0.
+fr_inverse_bin (the device's batch-inverse base case, poly.hip k_inv_small)
+is the same host/device source and is checked the same way.
 The golden proofs on the GPU cover the same code end to end."""
 import os
 import shutil
@@ -45,6 +47,18 @@ def test_host_mont_product_and_inverse(lines, field):
     for a, b, ab, inv in ([int(x, 16) for x in row] for row in rows):
         assert a < p and b < p
         assert ab == a * b * rinv % p
+        if a == 0:
+            assert inv == 0
+        else:
+            assert inv < p and a * inv % p == R * R % p
+
+
+def test_fr_inverse_bin(lines):
+    p, bits = MOD["r"]
+    R = 1 << bits
+    rows = [[int(x, 16) for x in ln[1:]] for ln in lines if ln[0] == "b"]
+    assert len(rows) == 300
+    for a, inv in rows:
         if a == 0:
             assert inv == 0
         else:

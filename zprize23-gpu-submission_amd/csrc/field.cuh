@@ -570,6 +570,102 @@ PNP_HD Fp<P> inverse(const Fp<P> &a) {
     return acc;
 }
 
+// Fr inverse by the binary extended Euclidean algorithm on 32-bit words, for
+// the device where ONE inversion's latency is the cost (the batch inverse's
+// base case, poly.hip k_inv_small): ~2 log2 r steps of a few 8-word shifts /
+// subtractions instead of Fermat's ~380 dependent products of ~300 VALU.
+// Variable time; it inverts the product of a batch, not a key.  Halving x
+// (mod r) by 2^k at once: r = 1 mod 2^32, so x + ((-x) mod 2^k) r is
+// divisible by 2^k.
+PNP_HD void inv_shr(uint32_t *w, int k) {  // w >>= k, 0 < k < 32
+#pragma unroll
+    for (int j = 0; j < 7; j++) w[j] = (w[j] >> k) | (w[j + 1] << (32 - k));
+    w[7] >>= k;
+}
+PNP_HD void inv_halve(uint32_t *x, int k) {  // x 2^-k mod r (x < r), 0 < k < 32
+    const uint32_t m = (0u - x[0]) & ((1u << k) - 1);
+    uint64_t c = 0;
+    uint32_t top;
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+        c += (uint64_t)m * FrP::P[j] + x[j];
+        x[j] = (uint32_t)c;
+        c >>= 32;
+    }
+    top = (uint32_t)c;  // x + m r < 2^(256 + k)
+#pragma unroll
+    for (int j = 0; j < 7; j++) x[j] = (x[j] >> k) | (x[j + 1] << (32 - k));
+    x[7] = (x[7] >> k) | (top << (32 - k));
+    // (x + m r) / 2^k < r / 2^k + r: one conditional subtraction
+    uint32_t t[8], br = 0;
+#pragma unroll
+    for (int j = 0; j < 8; j++) t[j] = __builtin_subc(x[j], FrP::P[j], br, &br);
+#pragma unroll
+    for (int j = 0; j < 8; j++) x[j] = br ? x[j] : t[j];
+}
+PNP_HD Fr fr_inverse_bin(const Fr &a) {
+    if (a.is_zero()) return a;
+    uint32_t u[8], v[8], x1[8], x2[8];
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+        u[j] = a.v[j];
+        v[j] = FrP::P[j];
+        x1[j] = x2[j] = 0;
+    }
+    x1[0] = 1;
+    auto is_one = [](const uint32_t *w) {
+        uint32_t acc = w[0] ^ 1u;
+#pragma unroll
+        for (int j = 1; j < 8; j++) acc |= w[j];
+        return acc == 0;
+    };
+    auto strip = [](uint32_t *w, uint32_t *x) {  // w odd, x / 2^k (w != 0)
+        while (!(w[0] & 1)) {
+            const int k = w[0] ? __builtin_ctz(w[0]) : 31;
+            inv_shr(w, k);
+            inv_halve(x, k);
+        }
+    };
+    strip(u, x1);
+    while (!is_one(u) && !is_one(v)) {
+        strip(v, x2);
+        bool ge = true;  // u >= v
+#pragma unroll
+        for (int j = 7; j >= 0; j--)
+            if (u[j] != v[j]) {
+                ge = u[j] > v[j];
+                break;
+            }
+        // keep u >= v: swapping the pairs (u, x1), (v, x2) keeps x1 a = u,
+        // x2 a = v (mod r); selects, not pointers (registers, no scratch)
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            const uint32_t tu = u[j], tx = x1[j];
+            u[j] = ge ? tu : v[j];
+            v[j] = ge ? v[j] : tu;
+            x1[j] = ge ? tx : x2[j];
+            x2[j] = ge ? x2[j] : tx;
+        }
+        uint32_t br = 0;
+#pragma unroll
+        for (int j = 0; j < 8; j++) u[j] = __builtin_subc(u[j], v[j], br, &br);
+        br = 0;
+#pragma unroll
+        for (int j = 0; j < 8; j++) x1[j] = __builtin_subc(x1[j], x2[j], br, &br);
+        if (br) {
+            uint32_t c = 0;
+#pragma unroll
+            for (int j = 0; j < 8; j++) x1[j] = __builtin_addc(x1[j], FrP::P[j], c, &c);
+        }
+        strip(u, x1);  // the difference of two odd numbers is even (and not 0)
+    }
+    Fr r;
+    const uint32_t *x = is_one(u) ? x1 : x2;
+#pragma unroll
+    for (int j = 0; j < 8; j++) r.v[j] = x[j];
+    // the plain inverse of a R is a^-1 R^-1: times R^3 (= R2 R2 / R) gives a^-1 R
+    return r * (Fr::r2() * Fr::r2());
+}
 // canonical compare a > b (gt_zkp, zk_function.cu:3-22)
 template <class P>
 PNP_HD bool gt(const Fp<P> &a, const Fp<P> &b) {

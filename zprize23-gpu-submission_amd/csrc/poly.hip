@@ -126,13 +126,17 @@ __global__ void k_binv_down(uint64_t *d, uint64_t n, const uint64_t *pre, const 
         acc = acc * x;
     }
 }
-__global__ void k_fermat_inv(uint64_t *d, uint64_t n) {
+// The batch inverse's base case: <= 4096 independent inversions, one per
+// lane, so its time is ONE inversion's latency: field.cuh fr_inverse_bin
+// (binary extended Euclid) instead of Fermat's ~380 dependent products
+// (0.3 ms, exposed at 8 ranks).
+__global__ void k_inv_small(uint64_t *d, uint64_t n) {
     uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
-    if (i < n) store_fr(d, i, inverse(load_fr(d, i)));
+    if (i < n) store_fr(d, i, fr_inverse_bin(load_fr(d, i)));
 }
 static void binv_rec(uint64_t *d, uint64_t n, uint64_t *scratch, hipStream_t s) {
     if (n <= 4096) {
-        hipLaunchKernelGGL(k_fermat_inv, dim3(nblk(n, 64)), dim3(64), 0, s, d, n);
+        hipLaunchKernelGGL(k_inv_small, dim3(nblk(n, 64)), dim3(64), 0, s, d, n);
         PNP_HIP(hipGetLastError());
         return;
     }
