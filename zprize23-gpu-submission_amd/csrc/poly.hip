@@ -100,30 +100,31 @@ void k_prefix_product(uint64_t *d, uint64_t n, DevBuf &scratch, hipStream_t s) {
 }
 
 // ---------------------------------------------------------------- batch inverse
-__global__ void k_binv_up(const uint64_t *d, uint64_t n, uint64_t *pre, uint64_t *tot) {
+// Chunk c of nc holds the elements c, c + nc, c + 2 nc, ... (any partition
+// serves a batch inverse): a wave's loads and stores are 64 consecutive
+// elements, not 64 elements a chunk (1 KB) apart as with contiguous chunks.
+__global__ void k_binv_up(const uint64_t *d, uint64_t n, uint64_t nc, uint64_t *pre, uint64_t *tot) {
     uint64_t c = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
-    uint64_t lo = c * CHUNK;
-    if (lo >= n) return;
-    uint64_t hi = lo + CHUNK < n ? lo + CHUNK : n;
+    if (c >= nc) return;
     Fr acc = Fr::one();
-    for (uint64_t i = lo; i < hi; i++) {
+    for (uint64_t i = c; i < n; i += nc) {
         store_fr(pre, i, acc);
         Fr x = load_fr(d, i);
         if (!x.is_zero()) acc = acc * x;
     }
     store_fr(tot, c, acc);
 }
-__global__ void k_binv_down(uint64_t *d, uint64_t n, const uint64_t *pre, const uint64_t *tinv) {
+__global__ void k_binv_down(uint64_t *d, uint64_t n, uint64_t nc, const uint64_t *pre, const uint64_t *tinv) {
     uint64_t c = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
-    uint64_t lo = c * CHUNK;
-    if (lo >= n) return;
-    uint64_t hi = lo + CHUNK < n ? lo + CHUNK : n;
+    if (c >= nc || c >= n) return;
     Fr acc = load_fr(tinv, c);
-    for (uint64_t i = hi; i-- > lo;) {
+    for (uint64_t i = c + (n - 1 - c) / nc * nc;; i -= nc) {
         Fr x = load_fr(d, i);
-        if (x.is_zero()) continue;
-        store_fr(d, i, acc * load_fr(pre, i));
-        acc = acc * x;
+        if (!x.is_zero()) {
+            store_fr(d, i, acc * load_fr(pre, i));
+            acc = acc * x;
+        }
+        if (i < nc) break;
     }
 }
 // The batch inverse's base case: <= 4096 independent inversions, one per
@@ -142,10 +143,10 @@ static void binv_rec(uint64_t *d, uint64_t n, uint64_t *scratch, hipStream_t s) 
     }
     uint64_t nc = (n + CHUNK - 1) / CHUNK;
     uint64_t *pre = scratch, *tot = scratch + 4 * n;
-    hipLaunchKernelGGL(k_binv_up, dim3(nblk(nc)), dim3(256), 0, s, d, n, pre, tot);
+    hipLaunchKernelGGL(k_binv_up, dim3(nblk(nc)), dim3(256), 0, s, d, n, nc, pre, tot);
     PNP_HIP(hipGetLastError());
     binv_rec(tot, nc, tot + 4 * nc, s);
-    hipLaunchKernelGGL(k_binv_down, dim3(nblk(nc)), dim3(256), 0, s, d, n, pre, tot);
+    hipLaunchKernelGGL(k_binv_down, dim3(nblk(nc)), dim3(256), 0, s, d, n, nc, pre, tot);
     PNP_HIP(hipGetLastError());
 }
 void k_batch_inverse(uint64_t *d, uint64_t n, DevBuf &scratch, hipStream_t s) {
@@ -284,20 +285,21 @@ __global__ __launch_bounds__(256) void k_sum_partials(const uint64_t *partial, u
     const uint64_t *pp = partial + 4 * (uint64_t)blockIdx.x * nb;
     Fr acc = Fr::zero();
     for (uint64_t i = threadIdx.x; i < nb; i += 256) acc = acc + load_fr(pp, i);
-    red_lo[threadIdx.x] = make_uint4(acc.v[0], acc.v[1], acc.v[2], acc.v[3]);
-    red_hi[threadIdx.x] = make_uint4(acc.v[4], acc.v[5], acc.v[6], acc.v[7]);
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        Fr tot = Fr::zero();
-        for (int k = 0; k < 256; k++) {
-            Fr a;
-            uint4 a0 = red_lo[k], a1 = red_hi[k];
-            a.v[0] = a0.x; a.v[1] = a0.y; a.v[2] = a0.z; a.v[3] = a0.w;
-            a.v[4] = a1.x; a.v[5] = a1.y; a.v[6] = a1.z; a.v[7] = a1.w;
-            tot = tot + a;
+    // a tree over the 256 lane sums (8 dependent additions, not 256 on one lane)
+    for (int st = 128; st > 0; st >>= 1) {
+        red_lo[threadIdx.x] = make_uint4(acc.v[0], acc.v[1], acc.v[2], acc.v[3]);
+        red_hi[threadIdx.x] = make_uint4(acc.v[4], acc.v[5], acc.v[6], acc.v[7]);
+        __syncthreads();
+        if ((int)threadIdx.x < st) {
+            Fr b;
+            const uint4 b0 = red_lo[threadIdx.x + st], b1 = red_hi[threadIdx.x + st];
+            b.v[0] = b0.x; b.v[1] = b0.y; b.v[2] = b0.z; b.v[3] = b0.w;
+            b.v[4] = b1.x; b.v[5] = b1.y; b.v[6] = b1.z; b.v[7] = b1.w;
+            acc = acc + b;
         }
-        store_fr(out, blockIdx.x, tot);
+        __syncthreads();
     }
+    if (threadIdx.x == 0) store_fr(out, blockIdx.x, acc);
 }
 
 void k_poly_eval_sets(const EvalSet *sets, int nsets, uint64_t n, DevBuf &scratch, hipStream_t s) {
