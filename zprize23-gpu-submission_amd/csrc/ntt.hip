@@ -698,44 +698,50 @@ __device__ __forceinline__ Fr apply_scale(const Scale &s, Fr x, uint64_t i) {
     return x * f;
 }
 
-// lg >= 10: index = hi5 | mid | lo5; tile(mid) <-> tile(rev(mid)) transposed.
+// lg >= 2 TB: index = hi | mid | lo (TB bits each end); tile(mid) <->
+// tile(rev(mid)) transposed.  TB = 4 (default): 16 x 16 tiles, 17 KB of LDS
+// per workgroup, one element per lane per tile; TB = 5 (32 x 32, 68 KB: two
+// workgroups per CU) moved 256 MB in ~0.3 ms at 2^22, ~0.9 TB/s.  Rows of a
+// tile are 2^TB consecutive elements (512 B at TB = 4: four whole lines).
+template <int TB>
 __global__ __launch_bounds__(256) void k_bitrev_tiles(uint64_t *data, uint32_t lg, Scale sc) {
-    __shared__ uint4 t0l[32 * 33], t0h[32 * 33], t1l[32 * 33], t1h[32 * 33];
+    constexpr int T = 1 << TB, TP = T + 1;
+    __shared__ uint4 t0l[T * TP], t0h[T * TP], t1l[T * TP], t1h[T * TP];
     data += ((uint64_t)blockIdx.y << lg) * 4;  // independent transforms of 2^lg side by side
-    const uint32_t midbits = lg - 10;
+    const uint32_t midbits = lg - 2 * TB;
     const uint32_t mid = blockIdx.x;
     const uint32_t rmid = midbits ? brev(mid, midbits) : 0;
     if (rmid < mid) return;  // each pair handled once
     const bool self = rmid == mid;
-    // load tile(mid): rows hi (0..31), cols lo (0..31) contiguous
-    for (int e = threadIdx.x; e < 1024; e += 256) {
-        uint32_t h = e >> 5, l = e & 31;
-        uint64_t i0 = ((uint64_t)h << (lg - 5)) | ((uint64_t)mid << 5) | l;
+    // load tile(mid): rows hi, cols lo contiguous
+    for (int e = threadIdx.x; e < T * T; e += 256) {
+        uint32_t h = e >> TB, l = e & (T - 1);
+        uint64_t i0 = ((uint64_t)h << (lg - TB)) | ((uint64_t)mid << TB) | l;
         const uint4 *s0 = reinterpret_cast<const uint4 *>(data + 4 * i0);
-        t0l[h * 33 + l] = s0[0];
-        t0h[h * 33 + l] = s0[1];
+        t0l[h * TP + l] = s0[0];
+        t0h[h * TP + l] = s0[1];
         if (!self) {
-            uint64_t i1 = ((uint64_t)h << (lg - 5)) | ((uint64_t)rmid << 5) | l;
+            uint64_t i1 = ((uint64_t)h << (lg - TB)) | ((uint64_t)rmid << TB) | l;
             const uint4 *s1 = reinterpret_cast<const uint4 *>(data + 4 * i1);
-            t1l[h * 33 + l] = s1[0];
-            t1h[h * 33 + l] = s1[1];
+            t1l[h * TP + l] = s1[0];
+            t1h[h * TP + l] = s1[1];
         }
     }
     __syncthreads();
-    // element at (h, mid, l) goes to (rev5(l), rev(mid), rev5(h)).
-    // write tile position rmid: dest (h', rmid, l') gets source (rev5(l'), mid, rev5(h'))
-    for (int e = threadIdx.x; e < 1024; e += 256) {
-        uint32_t h2 = e >> 5, l2 = e & 31;
-        uint32_t sh = brev(l2, 5), sl = brev(h2, 5);
-        uint64_t d0 = ((uint64_t)h2 << (lg - 5)) | ((uint64_t)rmid << 5) | l2;
+    // element at (h, mid, l) goes to (rev(l), rev(mid), rev(h)).
+    // write tile position rmid: dest (h', rmid, l') gets source (rev(l'), mid, rev(h'))
+    for (int e = threadIdx.x; e < T * T; e += 256) {
+        uint32_t h2 = e >> TB, l2 = e & (T - 1);
+        uint32_t sh = brev(l2, TB), sl = brev(h2, TB);
+        uint64_t d0 = ((uint64_t)h2 << (lg - TB)) | ((uint64_t)rmid << TB) | l2;
         Fr x;
-        uint4 lo = t0l[sh * 33 + sl], hi = t0h[sh * 33 + sl];
+        uint4 lo = t0l[sh * TP + sl], hi = t0h[sh * TP + sl];
         x.v[0] = lo.x; x.v[1] = lo.y; x.v[2] = lo.z; x.v[3] = lo.w;
         x.v[4] = hi.x; x.v[5] = hi.y; x.v[6] = hi.z; x.v[7] = hi.w;
         store_fr(data, d0, apply_scale(sc, x, d0));
         if (!self) {
-            uint64_t d1 = ((uint64_t)h2 << (lg - 5)) | ((uint64_t)mid << 5) | l2;
-            uint4 lo1 = t1l[sh * 33 + sl], hi1 = t1h[sh * 33 + sl];
+            uint64_t d1 = ((uint64_t)h2 << (lg - TB)) | ((uint64_t)mid << TB) | l2;
+            uint4 lo1 = t1l[sh * TP + sl], hi1 = t1h[sh * TP + sl];
             Fr y;
             y.v[0] = lo1.x; y.v[1] = lo1.y; y.v[2] = lo1.z; y.v[3] = lo1.w;
             y.v[4] = hi1.x; y.v[5] = hi1.y; y.v[6] = hi1.z; y.v[7] = hi1.w;
@@ -960,10 +966,13 @@ static void dif(NttTables &t, uint64_t *d, uint32_t lg, bool inverse, hipStream_
 }
 
 static void bitrev(uint64_t *d, uint32_t lg, const Scale &sc, hipStream_t s, uint32_t nblocks = 1) {
+    static const int tb = getenv("PNP_BITREV_TB") && atoi(getenv("PNP_BITREV_TB")) == 5 ? 5 : 4;  // A/B
     if (lg < 10) {
         hipLaunchKernelGGL(k_bitrev_small, dim3(1, nblocks), dim3(256), 0, s, d, lg, sc);
+    } else if (tb == 5) {
+        hipLaunchKernelGGL(k_bitrev_tiles<5>, dim3(1u << (lg - 10), nblocks), dim3(256), 0, s, d, lg, sc);
     } else {
-        hipLaunchKernelGGL(k_bitrev_tiles, dim3(1u << (lg - 10), nblocks), dim3(256), 0, s, d, lg, sc);
+        hipLaunchKernelGGL(k_bitrev_tiles<4>, dim3(1u << (lg - 8), nblocks), dim3(256), 0, s, d, lg, sc);
     }
     PNP_HIP(hipGetLastError());
 }
