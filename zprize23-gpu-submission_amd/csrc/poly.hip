@@ -224,27 +224,30 @@ void k_poly_div_linear(uint64_t *d, uint64_t n, const Fr &z, DevBuf &scratch, hi
 // product by x^(base + t) = (x^(256 EV_K))^b x^t: a 9- and an 8-bit power per
 // lane instead of the full x^lo power per 32-coefficient chunk of the
 // previous layout (which cost more products than the Horner steps).
-static constexpr int EV_K = 32;
+// EV_K coefficients a lane (a template argument: PNP_EV_K = 16 or 32, A/B)
 struct EvalPtrs {  // up to 8 polys, by value in the kernel arguments (no upload)
     const uint64_t *p[8];
 };
-template <int NP>
+// Two Horner steps at a time, h <- h X^2 + c_k X + c_(k-1) (X = x^256): the
+// two products share one Montgomery reduction (fr_mul2).
+template <int NP, int EV_K>
 __global__ __launch_bounds__(256) void k_eval_partial(EvalPtrs polys, uint64_t n, Fr x,
                                                       Fr x256, Fr xblk, uint64_t *partial) {
+    static_assert(EV_K % 2 == 0, "Horner steps in pairs");
     __shared__ uint4 red_lo[256], red_hi[256];
     const uint64_t base = (uint64_t)blockIdx.x * 256 * EV_K + threadIdx.x;
+    const Fr x512 = x256 * x256;
     Fr h[NP];
 #pragma unroll
     for (int p = 0; p < NP; p++) h[p] = Fr::zero();
 #pragma unroll 1
-    for (int k = EV_K - 1; k >= 0; k--) {
-        const uint64_t i = base + 256ull * k;
-        if (i < n) {
+    for (int k = EV_K - 1; k >= 1; k -= 2) {
+        const uint64_t i1 = base + 256ull * k, i0 = i1 - 256;  // i0 < i1
 #pragma unroll
-            for (int p = 0; p < NP; p++) h[p] = h[p] * x256 + load_fr(polys.p[p], i);
-        } else {
-#pragma unroll
-            for (int p = 0; p < NP; p++) h[p] = h[p] * x256;
+        for (int p = 0; p < NP; p++) {
+            const Fr c1 = i1 < n ? load_fr(polys.p[p], i1) : Fr::zero();
+            const Fr c0 = i0 < n ? load_fr(polys.p[p], i0) : Fr::zero();
+            h[p] = fr_mul2(h[p], x512, c1, x256) + c0;
         }
     }
     const Fr sc = pow_u64(xblk, blockIdx.x) * pow_u64(x, threadIdx.x);  // x^(base)
@@ -306,6 +309,7 @@ void k_poly_eval_sets(const EvalSet *sets, int nsets, uint64_t n, DevBuf &scratc
     int total = 0;
     for (int k = 0; k < nsets; k++) total += std::max(sets[k].np, 0);
     if (total == 0) return;
+    static const int EV_K = getenv("PNP_EV_K") && atoi(getenv("PNP_EV_K")) == 32 ? 32 : 16;
     const uint32_t nb = (uint32_t)std::max<uint64_t>(1, (n + 256 * EV_K - 1) / (256 * EV_K));
     // layout: [partials total*nb][results total]: every group of up to 8 polys
     // has its own slice, so all launch back to back and ONE copy and ONE
@@ -327,7 +331,10 @@ void k_poly_eval_sets(const EvalSet *sets, int nsets, uint64_t n, DevBuf &scratc
             switch (np) {
 #define PNP_EV(K)                                                                                 \
     case K:                                                                                       \
-        hipLaunchKernelGGL(k_eval_partial<K>, dim3(nb), dim3(256), 0, s, ptrs, n, x, x256, xblk, pt); \
+        if (EV_K == 32)                                                                           \
+            hipLaunchKernelGGL((k_eval_partial<K, 32>), dim3(nb), dim3(256), 0, s, ptrs, n, x, x256, xblk, pt); \
+        else                                                                                      \
+            hipLaunchKernelGGL((k_eval_partial<K, 16>), dim3(nb), dim3(256), 0, s, ptrs, n, x, x256, xblk, pt); \
         break;
                 PNP_EV(1) PNP_EV(2) PNP_EV(3) PNP_EV(4) PNP_EV(5) PNP_EV(6) PNP_EV(7) PNP_EV(8)
 #undef PNP_EV

@@ -497,8 +497,12 @@ void k_widgets(const WidgetArgs &g, uint64_t N8, uint64_t *out, hipStream_t s) {
 __global__ __launch_bounds__(256) void k_lincomb_(LinArgs a, uint64_t n, uint64_t *out) {
     uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
     if (i >= n) return;
+    // terms in pairs sharing one Montgomery reduction (fr_mul2: 3/5 of the
+    // VALU of two products)
     Fr acc = Fr::zero();
-    for (int k = 0; k < a.k; k++) acc += load_fr(a.p[k], i) * a.s[k];
+    int k = 0;
+    for (; k + 1 < a.k; k += 2) acc += fr_mul2(load_fr(a.p[k], i), a.s[k], load_fr(a.p[k + 1], i), a.s[k + 1]);
+    if (k < a.k) acc += load_fr(a.p[k], i) * a.s[k];
     store_fr(out, i, acc);
 }
 void k_lincomb(const LinArgs &a, uint64_t n, uint64_t *out, hipStream_t s) {
