@@ -272,6 +272,9 @@ struct EvalSet {
 };
 void k_poly_eval_sets(const EvalSet *sets, int nsets, uint64_t n, DevBuf &scratch, hipStream_t s);
 void k_poly_div_linear(uint64_t *d, uint64_t n, const Fr &z, DevBuf &scratch, hipStream_t s);
+// several divisions d_k / (X - z_k) sharing every launch
+void k_poly_div_linear_batch(uint64_t *const *d, const Fr *z, int K, uint64_t n, DevBuf &scratch,
+                             hipStream_t s);
 // d[i] += c z^(len-1-i)
 void k_add_powers(uint64_t *d, uint64_t len, const Fr &c, const Fr &z, hipStream_t s);
 void k_random_fr(uint64_t *d, uint64_t n, uint64_t seed, hipStream_t s);

@@ -160,22 +160,34 @@ void k_batch_inverse(uint64_t *d, uint64_t n, DevBuf &scratch, hipStream_t s) {
 
 // ---------------------------------------------------------------- suffix Horner
 // H[k] = sum_{j >= k} v_j z^(j-k).  Chunk value L_c = H restricted to the chunk.
-__global__ void k_horner_chunk(const uint64_t *v, uint64_t n, Fr z, uint64_t *L) {
+// Up to HB_MAX independent polys (each its own z) share every launch
+// (blockIdx.y): the levels above the first are latency-bound chains of CHUNK
+// dependent products, so the round-6 pair of divisions costs one chain, not two.
+constexpr int HB_MAX = 4;
+struct HornerSet {
+    uint64_t *v[HB_MAX];
+    Fr z[HB_MAX];
+};
+__global__ void k_horner_chunk(HornerSet hs, uint64_t n, uint64_t *L, uint64_t nc) {
     uint64_t c = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
     uint64_t lo = c * CHUNK;
     if (lo >= n) return;
+    const uint64_t *v = hs.v[blockIdx.y];
+    const Fr z = hs.z[blockIdx.y];
     uint64_t hi = lo + CHUNK < n ? lo + CHUNK : n;
     Fr acc = Fr::zero();
     for (uint64_t i = hi; i-- > lo;) acc = acc * z + load_fr(v, i);
-    store_fr(L, c, acc);
+    store_fr(L + 4 * nc * blockIdx.y, c, acc);
 }
 // H at chunk starts is in Hc (inclusive); write H[k] for every k of the chunk
 // (mode 0) or the shifted quotient q[k] = H[k+1] (mode 1: poly division)
-__global__ void k_horner_apply(uint64_t *v, uint64_t n, Fr z, const uint64_t *Hc, uint64_t nc,
-                               int shift) {
+__global__ void k_horner_apply(HornerSet hs, uint64_t n, const uint64_t *Hc, uint64_t nc, int shift) {
     uint64_t c = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
     uint64_t lo = c * CHUNK;
     if (lo >= n) return;
+    uint64_t *v = hs.v[blockIdx.y];
+    const Fr z = hs.z[blockIdx.y];
+    Hc += 4 * nc * blockIdx.y;
     uint64_t hi = lo + CHUNK < n ? lo + CHUNK : n;
     Fr acc = c + 1 < nc ? load_fr(Hc, c + 1) : Fr::zero();  // H[hi]
     for (uint64_t i = hi; i-- > lo;) {
@@ -185,7 +197,9 @@ __global__ void k_horner_apply(uint64_t *v, uint64_t n, Fr z, const uint64_t *Hc
         if (!shift) store_fr(v, i, acc);
     }
 }
-__global__ void k_seq_horner(uint64_t *v, uint64_t n, Fr z, int shift) {
+__global__ void k_seq_horner(HornerSet hs, uint64_t n, int shift) {
+    uint64_t *v = hs.v[blockIdx.y];
+    const Fr z = hs.z[blockIdx.y];
     Fr acc = Fr::zero();
     for (uint64_t i = n; i-- > 0;) {
         Fr x = load_fr(v, i);
@@ -194,27 +208,42 @@ __global__ void k_seq_horner(uint64_t *v, uint64_t n, Fr z, int shift) {
         if (!shift) store_fr(v, i, acc);
     }
 }
-static void horner_rec(uint64_t *v, uint64_t n, const Fr &z, int shift, uint64_t *scratch,
-                       hipStream_t s) {
+static void horner_rec(const HornerSet &hs, int K, uint64_t n, int shift, uint64_t *scratch, hipStream_t s) {
     if (n <= CHUNK) {
-        hipLaunchKernelGGL(k_seq_horner, dim3(1), dim3(1), 0, s, v, n, z, shift);
+        hipLaunchKernelGGL(k_seq_horner, dim3(1, K), dim3(1), 0, s, hs, n, shift);
         PNP_HIP(hipGetLastError());
         return;
     }
     uint64_t nc = (n + CHUNK - 1) / CHUNK;
-    uint64_t *L = scratch;
-    hipLaunchKernelGGL(k_horner_chunk, dim3(nblk(nc)), dim3(256), 0, s, v, n, z, L);
+    uint64_t *L = scratch;  // K x nc
+    hipLaunchKernelGGL(k_horner_chunk, dim3(nblk(nc), K), dim3(256), 0, s, hs, n, L, nc);
     PNP_HIP(hipGetLastError());
-    Fr zK = pow_u64(z, CHUNK);
-    horner_rec(L, nc, zK, 0, scratch + 4 * nc, s);  // L <- inclusive H at chunk starts
-    hipLaunchKernelGGL(k_horner_apply, dim3(nblk(nc)), dim3(256), 0, s, v, n, z, L, nc, shift);
+    HornerSet up = {};
+    for (int k = 0; k < K; k++) {
+        up.v[k] = L + 4 * nc * k;
+        up.z[k] = pow_u64(hs.z[k], CHUNK);
+    }
+    horner_rec(up, K, nc, 0, scratch + 4 * nc * K, s);  // L <- inclusive H at chunk starts
+    hipLaunchKernelGGL(k_horner_apply, dim3(nblk(nc), K), dim3(256), 0, s, hs, n, L, nc, shift);
     PNP_HIP(hipGetLastError());
 }
-void k_poly_div_linear(uint64_t *d, uint64_t n, const Fr &z, DevBuf &scratch, hipStream_t s) {
+void k_poly_div_linear_batch(uint64_t *const *d, const Fr *z, int K, uint64_t n, DevBuf &scratch,
+                             hipStream_t s) {
     if (!n) return;
-    size_t need = rec_scratch_elems(n) * 32;
-    if (scratch.bytes < need) scratch.alloc(need);
-    horner_rec(d, n, z, 1, scratch.u64(), s);
+    for (int k0 = 0; k0 < K; k0 += HB_MAX) {
+        const int kb = std::min(K - k0, HB_MAX);
+        size_t need = rec_scratch_elems(n) * 32 * kb;
+        if (scratch.bytes < need) scratch.alloc(need);
+        HornerSet hs = {};
+        for (int k = 0; k < kb; k++) {
+            hs.v[k] = d[k0 + k];
+            hs.z[k] = z[k0 + k];
+        }
+        horner_rec(hs, kb, n, 1, scratch.u64(), s);
+    }
+}
+void k_poly_div_linear(uint64_t *d, uint64_t n, const Fr &z, DevBuf &scratch, hipStream_t s) {
+    k_poly_div_linear_batch(&d, &z, 1, n, scratch, s);
 }
 
 // ---------------------------------------------------------------- evaluation
@@ -224,13 +253,16 @@ void k_poly_div_linear(uint64_t *d, uint64_t n, const Fr &z, DevBuf &scratch, hi
 // product by x^(base + t) = (x^(256 EV_K))^b x^t: a 9- and an 8-bit power per
 // lane instead of the full x^lo power per 32-coefficient chunk of the
 // previous layout (which cost more products than the Horner steps).
-// EV_K coefficients a lane (a template argument: PNP_EV_K = 16 or 32, A/B)
+// 32 coefficients a lane: 16 (4 waves a SIMD at 2^22 instead of 2) measured
+// slower, 1.06 vs 0.91 ms per proof: the lane's two powers (~25 products)
+// are spread over half the coefficients (profiles/r05_ab_mul2_lincomb_eval.txt)
+static constexpr int EV_K = 32;
 struct EvalPtrs {  // up to 8 polys, by value in the kernel arguments (no upload)
     const uint64_t *p[8];
 };
 // Two Horner steps at a time, h <- h X^2 + c_k X + c_(k-1) (X = x^256): the
 // two products share one Montgomery reduction (fr_mul2).
-template <int NP, int EV_K>
+template <int NP>
 __global__ __launch_bounds__(256) void k_eval_partial(EvalPtrs polys, uint64_t n, Fr x,
                                                       Fr x256, Fr xblk, uint64_t *partial) {
     static_assert(EV_K % 2 == 0, "Horner steps in pairs");
@@ -309,7 +341,6 @@ void k_poly_eval_sets(const EvalSet *sets, int nsets, uint64_t n, DevBuf &scratc
     int total = 0;
     for (int k = 0; k < nsets; k++) total += std::max(sets[k].np, 0);
     if (total == 0) return;
-    static const int EV_K = getenv("PNP_EV_K") && atoi(getenv("PNP_EV_K")) == 32 ? 32 : 16;
     const uint32_t nb = (uint32_t)std::max<uint64_t>(1, (n + 256 * EV_K - 1) / (256 * EV_K));
     // layout: [partials total*nb][results total]: every group of up to 8 polys
     // has its own slice, so all launch back to back and ONE copy and ONE
@@ -331,10 +362,7 @@ void k_poly_eval_sets(const EvalSet *sets, int nsets, uint64_t n, DevBuf &scratc
             switch (np) {
 #define PNP_EV(K)                                                                                 \
     case K:                                                                                       \
-        if (EV_K == 32)                                                                           \
-            hipLaunchKernelGGL((k_eval_partial<K, 32>), dim3(nb), dim3(256), 0, s, ptrs, n, x, x256, xblk, pt); \
-        else                                                                                      \
-            hipLaunchKernelGGL((k_eval_partial<K, 16>), dim3(nb), dim3(256), 0, s, ptrs, n, x, x256, xblk, pt); \
+        hipLaunchKernelGGL(k_eval_partial<K>, dim3(nb), dim3(256), 0, s, ptrs, n, x, x256, xblk, pt); \
         break;
                 PNP_EV(1) PNP_EV(2) PNP_EV(3) PNP_EV(4) PNP_EV(5) PNP_EV(6) PNP_EV(7) PNP_EV(8)
 #undef PNP_EV

@@ -87,7 +87,7 @@ std::vector<uint64_t> shard_allgather(pnp_ctx *ctx, const uint64_t *mine, int k,
 void div_linear_range(pnp_ctx *ctx, uint64_t *const *d, const Fr *z, int K, uint64_t len, bool dist) {
     hipStream_t s = ctx->stream;
     if (!dist) {
-        for (int k = 0; k < K; k++) k_poly_div_linear(d[k], len, z[k], ctx->scratch_a, s);
+        k_poly_div_linear_batch(d, z, K, len, ctx->scratch_a, s);  // one chain of launches for all K
         return;
     }
     const int world = ctx->msm.world, rank = ctx->msm.rank;
@@ -99,11 +99,11 @@ void div_linear_range(pnp_ctx *ctx, uint64_t *const *d, const Fr *z, int K, uint
     for (int k = 0; k < K; k++) to_u64_limbs(e[k], &mine[4 * k]);
     std::vector<uint64_t> all = shard_allgather(ctx, mine.data(), 4 * K, PNP_EX_TAG_DIV_CARRY);
     const uint64_t n = len * world;  // equal ranges (world divides 8 and n)
+    k_poly_div_linear_batch(d, z, K, len, ctx->scratch_a, s);
     for (int k = 0; k < K; k++) {
         Fr c = Fr::zero();
         const Fr zl = pow_u64(z[k], n / world);
         for (int r = world - 1; r > rank; r--) c = c * zl + from_u64_limbs<FrP>(&all[4 * (K * r + k)]);
-        k_poly_div_linear(d[k], len, z[k], ctx->scratch_a, s);
         if (rank < world - 1) k_add_powers(d[k], len, c, z[k], s);
     }
 }
