@@ -1208,9 +1208,10 @@ __global__ __launch_bounds__(256) void k_t_combine(const uint64_t *Y, uint64_t l
     for (int m = 0; m < M; m++) y[m] = load_fr(Y, m * len + u);
 #pragma unroll
     for (int e = 0; e < 8 - M; e++) {
-        Fr acc = ext.c[e * M] * y[0];
+        // products in pairs sharing one Montgomery reduction (fr_mul2)
+        Fr acc = M % 2 ? ext.c[e * M + M - 1] * y[M - 1] : Fr::zero();
 #pragma unroll
-        for (int m = 1; m < M; m++) acc += ext.c[e * M + m] * y[m];
+        for (int m = 0; m + 1 < M; m += 2) acc += fr_mul2(ext.c[e * M + m], y[m], ext.c[e * M + m + 1], y[m + 1]);
         y[M + e] = acc;
     }
     // DIF stage h = 4 (twiddles w^k), h = 2 (w^2k), h = 1; output bit-reversed

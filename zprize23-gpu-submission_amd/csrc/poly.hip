@@ -175,8 +175,15 @@ __global__ void k_horner_chunk(HornerSet hs, uint64_t n, uint64_t *L, uint64_t n
     const uint64_t *v = hs.v[blockIdx.y];
     const Fr z = hs.z[blockIdx.y];
     uint64_t hi = lo + CHUNK < n ? lo + CHUNK : n;
+    // two steps at a time, acc z^2 + v_(i+1) z + v_i: one reduction (fr_mul2)
+    const Fr z2 = z * z;
+    uint64_t i = hi;
     Fr acc = Fr::zero();
-    for (uint64_t i = hi; i-- > lo;) acc = acc * z + load_fr(v, i);
+    if ((hi - lo) & 1) acc = load_fr(v, --i);
+    while (i > lo) {
+        i -= 2;
+        acc = fr_mul2(acc, z2, load_fr(v, i + 1), z) + load_fr(v, i);
+    }
     store_fr(L + 4 * nc * blockIdx.y, c, acc);
 }
 // H at chunk starts is in Hc (inclusive); write H[k] for every k of the chunk
