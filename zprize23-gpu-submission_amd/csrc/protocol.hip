@@ -78,20 +78,22 @@ __global__ void k_perm_numden_(uint64_t *num, uint64_t *den, PermArgs a, Fr step
     const uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
     const uint64_t T = (uint64_t)gridDim.x * blockDim.x;
     if (t >= n) return;
-    Fr root = pow_u64(a.omega, t);
+    Fr xb = pow_u64(a.omega, t) * a.beta;  // beta x_i, stepped (no root * beta per element)
     for (uint64_t i = t; i < n; i += T) {
-        const Fr xb = root * a.beta, x2 = xb + xb, x4 = x2 + x2, x8 = x4 + x4;
+        const Fr x2 = xb + xb, x4 = x2 + x2, x8 = x4 + x4;
         const Fr xk[4] = {xb, x8 - xb, x8 + x4 + xb, x8 + x8 + xb};
-        Fr nm = Fr::one(), dn = Fr::one();
+        Fr w = load_fr(a.w[0], i);
+        Fr nm = w + xk[0] + a.gamma;  // the first factors start the products (no 1 * f)
+        Fr dn = w + load_fr(a.sigma[0], i) * a.beta + a.gamma;
 #pragma unroll
-        for (int j = 0; j < 4; j++) {
-            Fr w = load_fr(a.w[j], i);
+        for (int j = 1; j < 4; j++) {
+            w = load_fr(a.w[j], i);
             nm = nm * (w + xk[j] + a.gamma);
             dn = dn * (w + load_fr(a.sigma[j], i) * a.beta + a.gamma);
         }
         store_fr(num, i, nm);
         store_fr(den, i, dn);
-        root = root * step;
+        xb = xb * step;
     }
 }
 void k_perm_numden(uint64_t *num, uint64_t *den, const PermArgs &a, uint64_t n, hipStream_t s) {
