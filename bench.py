@@ -170,6 +170,12 @@ FQ_PRODUCTS_PER_MADD = 10
 ALG_BYTES_PER_ENTRY = 96 + 4
 MADS_PER_FQ_PRODUCT = 288
 MADD_ISSUE_CYCLES = 19761
+MADS_PER_FR_PRODUCT = 128  # 2 x 8 x 8: a b and m q of a 256-bit Montgomery product in 32-bit limbs
+# the radix-4 NTT group's ISA: 1,403 VALU per 4 butterflies, 73%
+# of them the 8-limb product's v_mad_u64_u32 / v_addc_co_u32 pairs (~4.4 cycles
+# each per wave64, profiles/r02_ubench_ops.txt), the rest ~2.2: ~3.8 on average
+NTT_VALU_PER_BUTTERFLY = 351
+NTT_CYCLES_PER_VALU = 0.73 * 4.4 + 0.27 * 2.2
 SIMDS, CLOCK_HZ = 256 * 4, 2.4e9
 HELD_CLOCK_GHZ = 2.10  # k_accumulate29 under load (DVFS), PMC clock pass, profiles/r02_pmc_clock.txt
 UBENCH_FILE = os.path.join(REPO, "profiles", "r02_ubench_ops.txt")
@@ -437,8 +443,10 @@ def drop_in(ctx, syn, steps: int, v1: bool):
         lib = ctx.lib
         ref = abi.proof_to_bytes(ctx.prove(syn.cs, device_ptrs=True))
         same = True
-        # The v1 symbol's own context is cold here, as in the reference
-        # driver's one proof per process (merkle-tree/src/main.rs:103): its
+        # The v1 symbol's own context is cold here, but NOT the process: HIP is
+        # initialised and the code objects are loaded by the v2 proofs above
+        # (the process-cold call, one proof per fresh process as the reference
+        # driver makes it, is tools/cold_call.py's v1_process_cold_s).  Its
         # first call hashes and uploads both keys and proves without the
         # optional tables, which then build in the background (context.h);
         # the next calls run beside that build.  Then the steady state of each
@@ -449,7 +457,7 @@ def drop_in(ctx, syn, steps: int, v1: bool):
             p = lib.gen_proof(cs_h, pk_h, ck_h)
             cold.append(round(time.perf_counter() - t0, 3))
             same &= abi.proof_to_bytes(p) == ref
-        out["v1_cold_calls_s"] = cold
+        out["v1_context_cold_calls_s"] = cold
         t0 = time.perf_counter()
         ctx.lib.pnp_sync(C.c_void_p(lib.pnp_v1_context()))
         out["v1_background_build_left_s"] = round(time.perf_counter() - t0, 3)
@@ -533,6 +541,17 @@ def bench_ntt(ctx, lg: int, steps: int, warmup: int, verify: bool):
     gbs = alg / (ms / 1e3) / 1e9
     per_call = ms / calls
     traffic = op_traffic(NTT_TRAFFIC_FILE, f"bytes_per_call_lg{lg}")
+    # VALU roofline (the transform is integer-VALU bound, not
+    # HBM-bound; DESIGN.md 7 "The NTT, measured"): the twiddle products done,
+    # n/2 (lg - 1) per transform (the half-size-1 level multiplies by 1 and
+    # skips the product; the iNTT's n^-1 scaling is not credited), against the
+    # textbook peak of 256-bit Montgomery products: 2 x 8 x 8 = 128 32-bit
+    # multiply-adds each at the measured v_mad_u64_u32 issue rate.  The HBM
+    # figure stays beside it (hbm_frac)
+    prods = (n // 2) * (lg - 1) * calls
+    fr_rate = prods / (ms / 1e3)
+    fr_peak = SIMDS * CLOCK_HZ * 64 / mad_cycles() / MADS_PER_FR_PRODUCT
+    bfly_rate = (n // 2) * lg * calls / (ms / 1e3)
     out = {"metric": f"NTT/iNTT 2^{lg} over BLS12-381 Fr (BASELINE config 2): HBM throughput",
            "value": round(gbs, 1), "unit": "GB/s", "n_gpus": 1, "steps": steps, "warmup": warmup,
            "ms_per_step": round(wall * 1e3 / steps, 3), "higher_is_better": True, "scaling": "weak",
@@ -541,12 +560,22 @@ def bench_ntt(ctx, lg: int, steps: int, warmup: int, verify: bool):
                                   f"per step ({batch * n * 32 / 2**30:.2f} GiB, beyond the 256 MiB MALL)",
                       "domain_log2": lg, "batch": batch, "op": "ntt"},
            "ms_per_transform": round(per_call, 4),
-           "roofline": {"bound": "hbm", "kernel": "pnp_ntt (k_ntt_pass4 passes + k_bitrev_tiles)",
-                        "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                        "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": traffic,
+           "roofline": {"bound": "valu", "kernel": "pnp_ntt (k_ntt_pass4 passes + k_bitrev_tiles)",
+                        "achieved": round(fr_rate / 1e9, 2), "peak": round(fr_peak / 1e9, 2),
+                        "unit": "G Fr-mul/s", "frac": round(fr_rate / fr_peak, 4),
+                        "traffic": traffic,
                         "traffic_over_algorithmic": round(traffic / (64 * n), 3) if traffic else None,
-                        "work": "2 x 32 B per element per transform (one read, one write: SURVEY 8(d)) / "
-                                "HIP-event time per pnp_ntt call on the library stream",
+                        "work": f"n/2 (lg - 1) twiddle products per transform / HIP-event time per pnp_ntt "
+                                f"call on the library stream; peak = {SIMDS} SIMDs x {CLOCK_HZ / 1e9} GHz x 64 "
+                                f"lanes / {mad_cycles()} cycles per v_mad_u64_u32 / {MADS_PER_FR_PRODUCT} "
+                                "multiply-adds per 256-bit Montgomery product",
+                        "butterflies_per_s": round(bfly_rate / 1e9, 2),
+                        "valu_per_butterfly_isa": NTT_VALU_PER_BUTTERFLY,
+                        "issue_model_frac": round(bfly_rate * NTT_VALU_PER_BUTTERFLY * NTT_CYCLES_PER_VALU
+                                                  / (SIMDS * CLOCK_HZ * 64), 4),
+                        "hbm_achieved_gbs": round(gbs, 1), "hbm_peak_gbs": HBM_PEAK_GBS,
+                        "hbm_frac": round(gbs / HBM_PEAK_GBS, 4),
+                        "hbm_work": "2 x 32 B per element per transform (one read, one write: SURVEY 8(d))",
                         "launches": calls}}
     if verify:
         lib = __import__("pnp_testlib").oracle()
@@ -713,6 +742,20 @@ def main():
     if world != args.gpus:
         log(f"bench: WORLD_SIZE={world} but --gpus {args.gpus}")
         return 2
+    # The v1 symbol as the reference driver calls it, one proof per fresh
+    # process (merkle-tree/src/main.rs:102-103): measured first, while this
+    # process has made no GPU call (a process that has done GPU work beside
+    # the children would share the GPU with them), by
+    # tools/cold_call.py's producer and cold children
+    cold = None
+    if (world == 1 and args.op == "proof" and args.drop_in == "v1" and not args.solo
+            and args.circuit == "merkle" and os.environ.get("PNP_BENCH_COLD", "1") != "0"):
+        sys.path.insert(0, os.path.join(REPO, "tools"))
+        try:
+            import cold_call
+            cold = cold_call.measure(args.lg, 3, seed=1, log=log)
+        except Exception as e:  # reported, never fatal to the headline
+            cold = {"v1_process_cold_error": repr(e)}
     import torch
     import torch.distributed as dist
     # PNP_BENCH_BACKEND=gloo: rehearsal of the multi-rank bench on fewer GPUs
@@ -981,6 +1024,8 @@ def main():
             log(f"proof check: {out['verified']} {chk}")
         if args.drop_in and world == 1:
             out["drop_in"] = drop_in(ctx, syn, args.steps, v1=args.drop_in == "v1")
+            if cold:
+                out["drop_in"].update(cold)
         if args.cpu_lg and world == 1:  # the CPU baseline: rank 0 at N = 1 only
             try:
                 out["cpu_baseline"] = cpu_baseline(ctx, args.cpu_lg, args.circuit, syn, proofs[0])

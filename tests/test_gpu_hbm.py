@@ -44,9 +44,14 @@ def test_plan_bounds_the_first_proof(lg):
         u0 = ctx.hbm_usage()
         plan = u0["mandatory"] + u0["lagrange"] + u0["groups"] + u0["transient"]
         # the first proof goes without the optional tables and starts their
-        # background build (context.h deferred tables); sync waits for it, the
-        # second proof uses them: the plan must cover the proof and the build
-        ctx.prove(syn.cs, device_ptrs=True)
+        # background build (context.h deferred tables); a second proof runs
+        # while that build is in flight (the proof's working set and
+        # the build's scratch live together), sync waits for the build, the
+        # third proof uses the tables: the plan must cover all of it
+        first = ctx.prove(syn.cs, device_ptrs=True)
+        during = ctx.prove(syn.cs, device_ptrs=True)
+        from pnp import abi
+        assert abi.proof_to_bytes(during) == abi.proof_to_bytes(first)
         ctx.sync()
         ctx.kernel_timing(True)
         ctx.prove(syn.cs, device_ptrs=True)
@@ -60,7 +65,7 @@ def test_plan_bounds_the_first_proof(lg):
         assert used == 1  # the groups were built and used, so the plan covered them
         assert grew <= plan, (grew, plan)
         assert plan <= 3 * grew + (256 << 20), (grew, plan)
-        # a third proof allocates nothing new
+        # a fourth proof allocates nothing new
         ctx.prove(syn.cs, device_ptrs=True)
         assert ctx.hbm_usage()["peak"] <= u1["live"] + (64 << 20)
     finally:
@@ -230,3 +235,32 @@ def test_background_build_then_key_load():
     _load(ctx, syn)
     assert abi.proof_to_bytes(ctx.prove(syn.cs, device_ptrs=True)) == p1  # starts a build
     ctx.close()  # stops it
+
+
+def test_exchange_setters_stop_the_background_build():
+    """pnp_set_msm_shard / pnp_set_exchange_v / _a2a change what
+    the background build reads (the world, the exchange) and release the table
+    it may be writing, so they stop it first.  A world-1 proof starts the
+    build, the setters run at once (set_msm_shard(None) calls all three), the
+    next proof keeps the bytes, and a later build completes and is used."""
+    import pnp
+    from pnp import abi
+    lg = 16
+    ctx = pnp.Context(0)
+    try:
+        syn = _instance(ctx, lg)
+        _load(ctx, syn)
+        p1 = abi.proof_to_bytes(ctx.prove(syn.cs, device_ptrs=True))  # starts the build
+        ctx.set_msm_shard(None)                                        # stops it
+        p2 = abi.proof_to_bytes(ctx.prove(syn.cs, device_ptrs=True))  # (may start another)
+        ctx.sync()
+        ctx.kernel_timing(True)
+        p3 = abi.proof_to_bytes(ctx.prove(syn.cs, device_ptrs=True))
+        ctx.sync()
+        p4 = abi.proof_to_bytes(ctx.prove(syn.cs, device_ptrs=True))
+        used = ctx.kernel_bytes("wire_groups_used")
+        ctx.kernel_timing(False)
+        assert p1 == p2 == p3 == p4
+        assert used >= 1, used
+    finally:
+        ctx.close()

@@ -264,7 +264,10 @@ def test_sharded_full_size_matches_golden(tmp_path, golden, world, shard):
     # table, so the 8 ranks of the Merkle case hold the
     # production default, groups on, and must really commit over them
     extra = {"PNP_WIRE_GROUPS": "0"} if world >= 4 and shard == "buckets" else {}
-    if shard == "points" and g.get("circuit") == "merkle":
+    if g.get("circuit") == "merkle" and (shard == "points" or world < 4):
+        # point ranges: each rank's slice of the group table; 2 bucket-range
+        # ranks: the whole table on each (~65 GB a rank) — both fit, and must
+        # really commit over the groups (the production default)
         extra["PNP_EXPECT_GROUPS"] = "1"
     _launch(world, ["full", prefix, str(g["lg"]), str(g["gates"]), str(g["seed"]), g.get("circuit", "arith")],
             tmp_path, 900, PNP_TEST_MSM_SHARD=shard, PNP_EXPECT_BUCKETS="1" if shard == "buckets" else "0",
@@ -296,6 +299,36 @@ def test_sharded_merkle_h13_groups_on(tmp_path, world, shard):
             PNP_TEST_MSM_SHARD=shard, PNP_EXPECT_BUCKETS="1" if shard == "buckets" else "0",
             PNP_MSM_BUCKETS_MIN_WORLD="2", PNP_EXPECT_GROUPS="1")
     for r in range(world):
+        assert open(f"{prefix}.{r}", "rb").read().hex() == g["proof_hex"], f"rank {r}"
+
+
+@pytest.mark.gpu
+def test_sharded_merkle_h14_buckets_groups_on(tmp_path):
+    """the production multi-GPU default — bucket-range
+    MSMs (from 4 ranks on) with the copy-constraint groups and z's runs ON —
+    byte-checked at the largest size 4 ranks sharing one GPU hold.  In
+    bucket-range mode every rank keeps the whole group table (5 segments x n
+    x 13 windows x 128 B), the folded SRS and the Lagrange table: ~35 GB of
+    tables a rank at HEIGHT = 14 (n = 2^21) against ~65 GB at HEIGHT = 15,
+    where 4 ranks plus build scratch would overrun the 288 GB.  Every rank
+    must commit over the groups (PNP_EXPECT_GROUPS) through bucket ranges
+    (PNP_EXPECT_BUCKETS) and equal the CPU restatement's golden proof
+    (tests/golden/merkle_h14_seed1.json, make_golden_full.py --lg 21
+    --circuit merkle); the second proof goes through the fixed slots."""
+    import json
+    path = os.path.join(HERE, "golden", "merkle_h14_seed1.json")
+    if not os.path.exists(path):
+        pytest.skip("golden merkle_h14_seed1.json not generated")
+    with open(path) as f:
+        g = json.load(f)
+    import torch
+    if torch.cuda.is_initialized():
+        torch.cuda.synchronize()
+        torch.cuda.empty_cache()
+    prefix = str(tmp_path / "h14")
+    _launch(4, ["full", prefix, str(g["lg"]), str(g["gates"]), str(g["seed"]), "merkle"], tmp_path, 900,
+            PNP_TEST_MSM_SHARD="buckets", PNP_EXPECT_BUCKETS="1", PNP_EXPECT_GROUPS="1")
+    for r in range(4):
         assert open(f"{prefix}.{r}", "rb").read().hex() == g["proof_hex"], f"rank {r}"
 
 

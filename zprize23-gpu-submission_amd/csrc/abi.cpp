@@ -8,6 +8,7 @@
 #include <dlfcn.h>
 #include <array>
 #include <atomic>
+#include <chrono>
 #include <mutex>
 #include <set>
 #include <thread>
@@ -626,6 +627,10 @@ int pnp_set_msm_shard(pnp_ctx *ctx, int rank, int world, pnp_allgather_fn allgat
                       uint64_t *d_xbuf, uint64_t xbuf_bytes) {
     if (!ctx || world < 1 || rank < 0 || rank >= world) return PNP_E_ARG;
     if (world > 1 && (!allgather || !d_xbuf)) return PNP_E_ARG;
+    // a background table build reads msm.world / rank / allgather (all_ranks_ok)
+    // and writes the tables whose point ranges these settings decide: stop it
+    // first (the next deferring proof starts a new one)
+    tables_cancel(ctx);
     ctx->msm.rank = world > 1 ? rank : 0;
     ctx->msm.world = world;
     ctx->msm.allgather = world > 1 ? allgather : nullptr;
@@ -638,6 +643,7 @@ int pnp_set_msm_shard(pnp_ctx *ctx, int rank, int world, pnp_allgather_fn allgat
 int pnp_set_exchange_a2a(pnp_ctx *ctx, pnp_alltoall_fn alltoall, void *user, uint64_t *d_a2a,
                          uint64_t a2a_bytes) {
     if (!ctx || (alltoall && !d_a2a)) return PNP_E_ARG;
+    tables_cancel(ctx);  // (as pnp_set_msm_shard)
     ctx->msm.alltoall = alltoall;
     ctx->msm.a2a_user = user;
     ctx->msm.a2a = alltoall ? d_a2a : nullptr;
@@ -648,6 +654,7 @@ int pnp_set_exchange_a2a(pnp_ctx *ctx, pnp_alltoall_fn alltoall, void *user, uin
 int pnp_set_exchange_v(pnp_ctx *ctx, pnp_alltoallv_fn alltoallv, void *user, uint64_t *d_send,
                        uint64_t *d_recv, uint64_t capacity_bytes) {
     if (!ctx || (alltoallv && (!d_send || !d_recv || capacity_bytes < 8))) return PNP_E_ARG;
+    tables_cancel(ctx);  // the builder may be writing lag_table, released below
     ctx->msm.alltoallv = alltoallv;
     ctx->msm.v_user = user;
     ctx->msm.v_send = alltoallv ? d_send : nullptr;
@@ -1442,7 +1449,15 @@ ProofC gen_proof(CircuitC circuit, ProverKeyC pk, CommitKeyC ck) {
         exit(EXIT_FAILURE);
     };
     int rc;
+    // the cold call's own stages (HIP init + context, key uploads, the hasher's
+    // tail after the proof), put before the proof's stages in
+    // pnp_last_stage_times(pnp_v1_context()) — bench.py's process-cold line
+    using clk = std::chrono::steady_clock;
+    const auto t_call = clk::now();
+    auto ms_since = [](clk::time_point a) { return std::chrono::duration<double, std::milli>(clk::now() - a).count(); };
+    const bool cold_ctx = !ctx;
     if (!ctx && (rc = pnp_ctx_create(0, &ctx)) != PNP_OK) die(rc);
+    const double ms_ctx = cold_ctx ? ms_since(t_call) : 0.0;
     uint64_t bound = circuit.n > circuit.lookup_len ? circuit.n : circuit.lookup_len;
     uint64_t D = 1;
     while (D < bound) D <<= 1;
@@ -1507,19 +1522,37 @@ ProofC gen_proof(CircuitC circuit, ProverKeyC pk, CommitKeyC ck) {
             });
             int lrc = PNP_OK;
             bool envelope = true;
+            double ms_pk = 0, ms_ck = 0, ms_prove = 0;
             try {
+                auto t = clk::now();
                 if ((lrc = pnp_load_prover_key(ctx, &pk, D, 0)) == PNP_OK) {
                     envelope = !strict || (ctx->pk_qm_zero && ctx->pk_qlookup_zero && !ctx->pk_custom_nz[0] &&
                                            !ctx->pk_custom_nz[1] && !ctx->pk_custom_nz[2] &&
                                            !ctx->pk_custom_nz[3] && key_tables_zero(ctx));
-                    if (envelope && (lrc = pnp_load_commit_key(ctx, &ck, D, 0)) == PNP_OK)
+                    ms_pk = ms_since(t);
+                    t = clk::now();
+                    if (envelope && (lrc = pnp_load_commit_key(ctx, &ck, D, 0)) == PNP_OK) {
+                        ms_ck = ms_since(t);
+                        t = clk::now();
                         lrc = pnp_prove(ctx, &circuit, 0, &out);
+                        ms_prove = ms_since(t);
+                    }
                 }
             } catch (...) {
                 hasher.join();
                 throw;
             }
+            const auto t_join = clk::now();
             hasher.join();
+            {
+                std::vector<std::pair<std::string, double>> st = {
+                    {"v1_ctx_create", ms_ctx}, {"v1_load_prover_key", ms_pk}, {"v1_load_commit_key", ms_ck},
+                    {"v1_prove", ms_prove}};
+                st.insert(st.end(), ctx->stages.begin(), ctx->stages.end());
+                st.push_back({"v1_hash_wait", ms_since(t_join)});
+                st.push_back({"v1_call", ms_since(t_call)});
+                ctx->stages.swap(st);
+            }
             have_pk = have_ck = false;
             if (lrc != PNP_OK) die(lrc);
             if (!envelope) {

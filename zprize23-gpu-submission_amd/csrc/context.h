@@ -97,7 +97,10 @@ struct pnp_ctx {
     uint64_t pk_gen = 0;                // incremented by every pnp_load_prover_key
     // the key-load HBM budget (pnp_load_prover_key) left no room for these
     // optional tables: the prover commits without them (same proof bytes)
-    bool hbm_lag_off = false, hbm_groups_off = false;
+    // (atomic: the background builder's failure paths set them while a proof
+    // on the owning thread may read them; such a proof finds the build busy and
+    // commits without the tables whatever it reads)
+    std::atomic<bool> hbm_lag_off{false}, hbm_groups_off{false};
     bool hbm_checked = false;  // the budget of the loaded keys has been checked (first proof)
     // Deferred tables: the context's first proof commits without the
     // optional tables it would have to build first (Lagrange basis, copy

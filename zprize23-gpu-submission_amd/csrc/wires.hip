@@ -356,8 +356,10 @@ void build_wire_bases(pnp_ctx *ctx, uint64_t n) {
     std::vector<DevBuf> bx(5);
     {
         DevBuf srt(n * 4), srow(n * 4), row(n * 4), head(n * 4), gid(n * 4), gstart(n * 4), part(n * 192);
-        // (at most n / (C WB_HEAVY) groups have more than WB_HEAVY pieces)
-        DevBuf heavy((n / (32 * WB_HEAVY) + 2) * 4);
+        // a group of more than WB_HEAVY pieces spans at least (WB_HEAVY - 1) C + 2
+        // positions (its first and last pieces may hold one each), so at most
+        // n / ((WB_HEAVY - 1) C) of them are queued, + the count word
+        DevBuf heavy((n / (32 * (WB_HEAVY - 1)) + 2) * 4);
         uint32_t *srt_p = static_cast<uint32_t *>(srt.p), *srow_p = static_cast<uint32_t *>(srow.p);
         uint32_t *head_p = static_cast<uint32_t *>(head.p), *gid_p = static_cast<uint32_t *>(gid.p);
         const int bits = (int)lg + 2;  // labels < 4n
