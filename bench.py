@@ -995,7 +995,29 @@ def main():
                                "callback_ms_per_proof": round(timed_cb["callback_ms"], 3),
                                "callbacks_per_proof_incl_warmup": (ex.calls + ex.a2a_calls + getattr(ex, "v_calls", 0)) / k}
         if solo:
-            out["solo"] = {"rank": solo.rank, "world": solo.world,
+            # xGMI term the loopback leaves out: one
+            # direct link per peer on a fully connected 8-GPU node, all peers
+            # in parallel, so a collective costs its bytes per peer over one
+            # link's rate plus a per-collective latency.  Stated assumptions
+            # (PNP_XGMI_LINK_GBS, PNP_XGMI_LAT_US): 64 GB/s per link and
+            # direction (MI355X quotes ~153 GB/s per link, both directions;
+            # RCCL reaches ~80% of it), 25 us per collective
+            link = float(os.environ.get("PNP_XGMI_LINK_GBS", "64")) * 1e9
+            lat = float(os.environ.get("PNP_XGMI_LAT_US", "25")) * 1e-6
+            k = args.steps + args.warmup
+            peers = max(solo.world - 1, 1)
+            per_peer = ((solo.a2a_bytes_moved + solo.v_bytes_moved) / k / peers
+                        + solo.gather_bytes / k / solo.world)  # an all-gather slot goes to every peer
+            xgmi_s = per_peer / link + timed_cb["callbacks"] * lat
+            xgmi = {"ms_per_proof": round(xgmi_s * 1e3, 3),
+                    "bytes_per_peer_per_proof": round(per_peer),
+                    "collectives_per_proof": timed_cb["callbacks"],
+                    "link_gbs_per_direction": link / 1e9, "latency_us_per_collective": lat * 1e6,
+                    "projected_rank_ms": round(per_proof * 1e3 + xgmi_s * 1e3, 2),
+                    "basis": "(all-to-all + bucket-record bytes sent / (world - 1) + all-gather slot bytes) "
+                             "/ one link's rate + collectives x latency; not overlapped with compute "
+                             "(an upper bound for the exchanges the proof waits on)"}
+            out["solo"] = {"rank": solo.rank, "world": solo.world, "xgmi_model": xgmi,
                            "allgathers_per_proof": timed_cb["allgathers"],
                            "alltoalls_per_proof": timed_cb["alltoalls"],
                            "allgather_bytes_per_proof": solo.gather_bytes / (args.steps + args.warmup),

@@ -53,6 +53,8 @@ def produce(d, lg, seed):
     ref = abi.proof_to_bytes(ctx.prove(syn.cs, device_ptrs=True))
     ctx.sync()
     # every host array once, by address; the structs refer to them by index
+    # (host_copy keys its arrays by the device address they copy)
+    byaddr = {a.ctypes.data: a for a in host.values()}
     files, index = [], {}
 
     def put(p):
@@ -60,7 +62,7 @@ def produce(d, lg, seed):
         if not addr:
             return -1
         if addr not in index:
-            arr = host[addr]
+            arr = byaddr[addr]
             k = len(files)
             arr.tofile(os.path.join(d, f"a{k}.bin"))
             files.append(arr.nbytes)
@@ -88,13 +90,18 @@ def child(d):
     t_py = time.perf_counter()
     with open(os.path.join(d, "meta.json")) as f:
         meta = json.load(f)
-    maps = []
+    maps, addrs = [], []
     for k, nb in enumerate(meta["files"]):
+        if nb == 0:  # an empty Vec (e.g. powers_of_gamma_g): any valid address
+            m = (C.c_uint64 * 8)()
+            maps.append(m)
+            addrs.append(C.addressof(m))
+            continue
         fd = os.open(os.path.join(d, f"a{k}.bin"), os.O_RDONLY)
         m = mmap.mmap(fd, nb, flags=mmap.MAP_SHARED | getattr(mmap, "MAP_POPULATE", 0), prot=mmap.PROT_READ)
         os.close(fd)
         maps.append(m)
-    addrs = [_map_address(m) for m in maps]
+        addrs.append(_map_address(m))
 
     def P(i):
         return abi.ptr(addrs[i]) if i >= 0 else abi.U64P()

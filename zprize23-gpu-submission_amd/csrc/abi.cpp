@@ -322,9 +322,11 @@ HbmPlan hbm_plan(pnp_ctx *ctx, uint64_t n) {
         const char *e = getenv("PNP_NTT29");
         return e && atoi(e) != 0;
     }();
-    const uint64_t ntt = 32 * n + 3 * 32 * N8 + (ntt29 ? 36 * n / 2 * 2 + 3 * 36 * N8 : 0);
+    // (+ the dense twiddle rows of both directions, 2 x (n - 1) entries)
+    const uint64_t ntt = 32 * n + 64 * n + 3 * 32 * N8 + (ntt29 ? 36 * n / 2 * 2 + 3 * 36 * N8 : 0);
     // (the 8n LDE twist of pnp_coset_lde8 is not a proof's: not counted as held)
-    const uint64_t ntt_held = map_bytes(ctx->ntt.fwd) + map_bytes(ctx->ntt.inv) + map_bytes(ctx->ntt.blk_twist) +
+    const uint64_t ntt_held = map_bytes(ctx->ntt.fwd) + map_bytes(ctx->ntt.inv) + map_bytes(ctx->ntt.fwd_rows) +
+                              map_bytes(ctx->ntt.inv_rows) + map_bytes(ctx->ntt.blk_twist) +
                               map_bytes(ctx->ntt.blk_twist_inv) + map_bytes(ctx->ntt.fwd29) +
                               map_bytes(ctx->ntt.inv29) + map_bytes(ctx->ntt.blk_twist29) +
                               map_bytes(ctx->ntt.blk_twist_inv29) + map_bytes(ctx->ntt.blk_twist32) +

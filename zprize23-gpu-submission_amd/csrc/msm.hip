@@ -374,6 +374,19 @@ __device__ __forceinline__ void tile_scan_wave0(uint32_t *lh, uint32_t *lofs, in
     }
 }
 
+// Tile ranking of pass A.  PNP_SORT_WAVERANK=0: one LDS atomic-with-return per
+// key on the tile's bin counters.  1: wave-level ranking —
+// each wave keeps its own 16-bit bin counters; a key's peers in its wave (same
+// bin) come from one ballot per bin bit (match-any), its rank is the popcount of
+// the peers below it (mbcnt), and the lowest peer alone adds the group to the
+// wave's counter (a plain LDS read and write: a wave's LDS operations execute in
+// order, so no atomic); the tile's bin offsets are then one scan over
+// (bin, wave) in bin-major order, which also makes the tile's order stable
+#ifndef PNP_SORT_WAVERANK
+#define PNP_SORT_WAVERANK 0
+#endif
+constexpr int SORT_NW = 16;  // waves of a 1024-lane sort workgroup
+
 // rec != nullptr: entries leave as 8-byte records entry | fine key << 32 (the
 // bucket-range exchange format) instead of the ent / fk arrays.  slot_recs > 0
 // (fixed-slot exchange): destination d's records go to its slot, rec + d
@@ -388,6 +401,15 @@ __global__ __launch_bounds__(1024) void k_coarse_scatter(const uint32_t *keys, K
     __shared__ uint32_t cur[1 << SORT_CB], lh[1 << SORT_CB], lofs[1 << SORT_CB], lim[1 << SORT_CB], wsum[16];
     __shared__ uint32_t st_e[TILE_K];
     __shared__ uint32_t st_m[TILE_K];
+#if PNP_SORT_WAVERANK
+    // per-wave bin counters (<= KPT * 64 per wave), then the (bin, wave) offsets
+    __shared__ uint16_t wh[SORT_NW][1 << SORT_CB];
+    __shared__ uint32_t tile_total;
+    const int cbits = 31 - __builtin_clz((uint32_t)NBc);
+    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const uint64_t below = (1ULL << lane) - 1;
+    for (int b = threadIdx.x; b < SORT_NW * NBc; b += blockDim.x) wh[b / NBc][b % NBc] = 0;
+#endif
     const int v = blockIdx.y, ch = blockIdx.x;
     for (int b = threadIdx.x; b < NBc; b += blockDim.x) {
         cur[b] = offs[cidx(v, gridDim.y, b, NBc, wmaj, ch, nch)];
@@ -444,6 +466,59 @@ __global__ __launch_bounds__(1024) void k_coarse_scatter(const uint32_t *keys, K
 #if PNP_SORT_PREFETCH
             if (nr < kr.rows) load_tile(nr, ntb, nxt);
 #endif
+#if PNP_SORT_WAVERANK
+#pragma unroll
+            for (int j = 0; j < KPT; j++) {
+                const bool valid = key[j] != KEY_ZERO;
+                const uint32_t bin = valid ? (key[j] & 0x7FFFFFFFu) >> fb : 0u;
+                uint64_t peers = __ballot(valid);
+                for (int b = 0; b < cbits; b++) {
+                    const bool bit = (bin >> b) & 1u;
+                    const uint64_t m = __ballot(bit);
+                    peers &= bit ? m : ~m;
+                }
+                if (valid) {
+                    const uint32_t base = wh[wv][bin];
+                    rank[j] = base + (uint32_t)__popcll(peers & below);
+                    if ((peers & below) == 0) wh[wv][bin] = (uint16_t)(base + (uint32_t)__popcll(peers));
+                }
+            }
+            __syncthreads();
+            {
+                // exclusive scan of the (bin, wave) counters in bin-major order
+                const int E = SORT_NW * NBc, per = (E + (int)blockDim.x - 1) / (int)blockDim.x;
+                const int f0 = (int)threadIdx.x * per;
+                uint32_t loc = 0;
+                for (int f = f0; f < f0 + per && f < E; f++) loc += wh[f % SORT_NW][f / SORT_NW];
+                const uint32_t x = wave_scan_incl(loc);
+                if (lane == 63) wsum[wv] = x;
+                __syncthreads();
+                const uint32_t wt = wave_scan_incl(lane < SORT_NW ? wsum[lane] : 0u);
+                const int wsrc = __builtin_amdgcn_readfirstlane(wv) - 1;
+                uint32_t run = x - loc + (wsrc >= 0 ? (uint32_t)__builtin_amdgcn_readlane((int)wt, wsrc) : 0u);
+                if (threadIdx.x == blockDim.x - 1) tile_total = run + loc;
+                for (int f = f0; f < f0 + per && f < E; f++) {
+                    const int b = f / SORT_NW, w = f % SORT_NW;
+                    const uint32_t c = wh[w][b];
+                    if (w == 0) lofs[b] = run;
+                    wh[w][b] = (uint16_t)run;
+                    run += c;
+                }
+            }
+            __syncthreads();
+#pragma unroll
+            for (int j = 0; j < KPT; j++) {
+                if (key[j] == KEY_ZERO) continue;
+                const uint64_t i = tb + 4 * (threadIdx.x + 1024 * (j / 4)) + (j & 3);
+                uint32_t mag = key[j] & 0x7FFFFFFFu, at = wh[wv][mag >> fb] + rank[j];
+                st_e[at] = (idb + (uint32_t)i) | (key[j] & 0x80000000u);
+                st_m[at] = mag;
+            }
+            __syncthreads();
+            const uint32_t total = tile_total;
+            for (int b = threadIdx.x; b < NBc; b += blockDim.x)
+                lh[b] = (b + 1 < NBc ? lofs[b + 1] : total) - lofs[b];
+#else
 #pragma unroll
             for (int j = 0; j < KPT; j++)
                 if (key[j] != KEY_ZERO) rank[j] = atomicAdd(&lh[(key[j] & 0x7FFFFFFFu) >> fb], 1u);
@@ -460,6 +535,7 @@ __global__ __launch_bounds__(1024) void k_coarse_scatter(const uint32_t *keys, K
             }
             __syncthreads();
             const uint32_t total = lofs[NBc - 1] + lh[NBc - 1];
+#endif
             for (uint32_t x = threadIdx.x; x < total; x += blockDim.x) {
                 uint32_t mag = st_m[x], bn = mag >> fb;
                 uint32_t pos = cur[bn] + x - lofs[bn];
@@ -475,6 +551,9 @@ __global__ __launch_bounds__(1024) void k_coarse_scatter(const uint32_t *keys, K
                 cur[b] += lh[b];
                 lh[b] = 0;
             }
+#if PNP_SORT_WAVERANK
+            for (int b = threadIdx.x; b < SORT_NW * NBc; b += blockDim.x) wh[b / NBc][b % NBc] = 0;
+#endif
             __syncthreads();
         }
 #if !PNP_SORT_PREFETCH

@@ -80,6 +80,50 @@ const uint64_t *ntt_twiddles(NttTables &t, uint32_t lg, bool inverse, hipStream_
     return p;
 }
 
+// Twiddle rows.  A level of a pass reads w_N^(r 2^sh),
+// r = j + mlow 2^lg_hlo, sh = lg_N - 1 - lg_hlo - l: from the plain table every
+// 2^sh-th entry, i.e. one 32-B twiddle per 128-B line once sh >= 2 (the first
+// DIF pass of a block LDE fetched ~62 B of twiddle lines per element,
+// profiles/r05_ntt_pmc_traffic.txt).  Row sh holds exactly those entries,
+// densely: rows[N - N / 2^sh + r] = w_N^(r 2^sh), so a tile's G consecutive
+// columns read G consecutive twiddles of every level.  N - 1 entries per size
+// and direction (2x the plain table).  PNP_NTT_ROWS=0: the plain table
+__global__ void k_twiddle_rows(const uint64_t *tw, uint32_t lg, uint64_t *rows) {
+    const uint64_t N = 1ULL << lg;
+    const uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;  // position in rows, < N - 1
+    if (i >= N - 1) return;
+    // row sh starts at N - N / 2^sh: sh = the number of leading ones of i in lg bits
+    uint32_t sh = 0;
+    while (i >= N - (N >> (sh + 1))) sh++;
+    const uint64_t r = i - (N - (N >> sh));
+    const uint4 *src = reinterpret_cast<const uint4 *>(tw + 4 * (r << sh));
+    uint4 *dst = reinterpret_cast<uint4 *>(rows + 4 * i);
+    dst[0] = src[0];
+    dst[1] = src[1];
+}
+
+static bool ntt_rows_enabled() {
+    static const bool on = [] {
+        const char *e = getenv("PNP_NTT_ROWS");
+        return !(e && atoi(e) == 0);
+    }();
+    return on;
+}
+
+static const uint64_t *ntt_twiddle_rows(NttTables &t, uint32_t lg, bool inverse, hipStream_t s) {
+    auto &m = inverse ? t.inv_rows : t.fwd_rows;
+    auto it = m.find(lg);
+    if (it != m.end()) return it->second.u64();
+    const uint64_t *tw = ntt_twiddles(t, lg, inverse, s);
+    const uint64_t cnt = (1ULL << lg) - 1;
+    DevBuf buf(std::max<uint64_t>(cnt, 1) * 32);
+    hipLaunchKernelGGL(k_twiddle_rows, dim3((uint32_t)((cnt + 255) / 256)), dim3(256), 0, s, tw, lg, buf.u64());
+    PNP_HIP(hipGetLastError());
+    const uint64_t *p = buf.u64();
+    m.emplace(lg, std::move(buf));
+    return p;
+}
+
 // a 2^256-form table (32-bit Montgomery Fr) -> its 2^261 form in radix 2^29
 __global__ void k_table_to_r29(const uint64_t *tab, uint64_t count, uint32_t *out) {
     const uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
@@ -283,7 +327,8 @@ template <int K, bool DIT>
 __global__ __launch_bounds__(NTT4_THREADS) void k_ntt_pass4(uint64_t *data, const uint64_t *tw,
                                                             uint32_t lg_n, uint32_t lg_hlo,
                                                             const uint64_t *src, const uint64_t *pre,
-                                                            uint64_t src_mask, const uint64_t *post) {
+                                                            uint64_t src_mask, const uint64_t *post,
+                                                            int rows = 0) {
     constexpr int G = TILE >> K;
     __shared__ uint4 lds_lo[TILE];
     __shared__ uint4 lds_hi[TILE];
@@ -306,8 +351,11 @@ __global__ __launch_bounds__(NTT4_THREADS) void k_ntt_pass4(uint64_t *data, cons
     }
     __syncthreads();
     // twiddle of a level-l butterfly whose lower element has low bits mlow
+    // (rows: the dense row of its shift, ntt_twiddle_rows)
     auto twl = [&](uint64_t j, int l, uint32_t mlow) {
-        return load_fr(tw, (j + ((uint64_t)mlow << lg_hlo)) << (lg_n - 1 - lg_hlo - l));
+        const uint32_t sh = lg_n - 1 - lg_hlo - l;
+        const uint64_t r = j + ((uint64_t)mlow << lg_hlo);
+        return rows ? load_fr(tw, (1ULL << lg_n) - (1ULL << (lg_n - sh)) + r) : load_fr(tw, r << sh);
     };
     constexpr int NPAIR = K / 2;
 #pragma unroll 1
@@ -912,15 +960,17 @@ static void ntt_core(NttTables &t, uint64_t *d, uint32_t lg, bool inverse, bool 
             continue;
         }
         if (ntt4_enabled() && k >= 2) {
+            const int rows = ntt_rows_enabled() ? 1 : 0;
+            const uint64_t *tw4 = rows ? ntt_twiddle_rows(t, lg, inverse, s) : tw;
             switch (k) {
 #define PNP_CASE4(KK)                                                                               \
     case KK:                                                                                        \
         if (dit)                                                                                    \
-            hipLaunchKernelGGL((k_ntt_pass4<KK, true>), dim3(blocks), dim3(NTT4_THREADS), 0, s, d, tw, \
-                               lg, lg_hlo, src, pre, fz.src_mask, post);                           \
+            hipLaunchKernelGGL((k_ntt_pass4<KK, true>), dim3(blocks), dim3(NTT4_THREADS), 0, s, d, tw4, \
+                               lg, lg_hlo, src, pre, fz.src_mask, post, rows);                     \
         else                                                                                        \
-            hipLaunchKernelGGL((k_ntt_pass4<KK, false>), dim3(blocks), dim3(NTT4_THREADS), 0, s, d, tw, \
-                               lg, lg_hlo, src, pre, fz.src_mask, post);                           \
+            hipLaunchKernelGGL((k_ntt_pass4<KK, false>), dim3(blocks), dim3(NTT4_THREADS), 0, s, d, tw4, \
+                               lg, lg_hlo, src, pre, fz.src_mask, post, rows);                     \
         break;
                 PNP_CASE4(2) PNP_CASE4(3) PNP_CASE4(4) PNP_CASE4(5) PNP_CASE4(6)
                 PNP_CASE4(7) PNP_CASE4(8) PNP_CASE4(9) PNP_CASE4(10)

@@ -52,6 +52,9 @@ struct DevBuf {
 struct NttTables {
     // tw[e] = w_N^e, e < N/2, for forward and inverse roots, per lg
     std::map<uint32_t, DevBuf> fwd, inv;
+    // the same twiddles as dense rows per shift (ntt.hip ntt_twiddle_rows): row
+    // sh = w_N^(i 2^sh), i < N / 2^(sh+1), at offset N - N / 2^sh
+    std::map<uint32_t, DevBuf> fwd_rows, inv_rows;
     DevBuf coset_hi, coset_lo;        // g^(4096 k), g^k
     DevBuf coset_inv_hi, coset_inv_lo;  // g^-(4096 k), g^-k
     bool coset_ready = false;
