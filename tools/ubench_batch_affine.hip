@@ -46,6 +46,25 @@ using namespace pnp;
     } while (0)
 
 constexpr uint64_t PT = 32;  // u32 per table point (x, y, padding: one 128-B line)
+// u32 per F29 in the prefix / total / scratch arrays: 64 B, so every element is
+// 16-B aligned (load29's 8-byte tail load is widened to 16 bytes by the
+// compiler on that assumption: at a 56-B stride the last element's widened load
+// crossed the end of the allocation and faulted)
+constexpr uint64_t SF = 16;
+
+// bounds of every array the batch-affine kernels index (checked per access:
+// an index out of range is counted in *bad and clamped, never dereferenced)
+struct Lim {
+    uint64_t tab_pts, pairs, pre_elems, tot_elems, out_pts;
+    uint32_t *bad;
+};
+__device__ __forceinline__ uint64_t chk(uint64_t i, uint64_t n, const Lim &lim) {
+    if (i >= n) {
+        atomicAdd(lim.bad, 1u);
+        return 0;
+    }
+    return i;
+}
 
 __device__ __forceinline__ F29 ld29(const uint32_t *p) { return load29(p); }
 __device__ __forceinline__ F29 ld29_x_half(const uint32_t *p) {
@@ -112,25 +131,25 @@ __global__ __launch_bounds__(256, PF ? 3 : 4) void k_xyzz_chain(const uint32_t *
 
 // pass 1: running products of d = x2 - x1 over the lane's K pairs
 __global__ __launch_bounds__(256) void k_ba_prefix(const uint32_t *tab, const uint2 *pairs, uint64_t L, int K,
-                                                    uint32_t *prefix, uint32_t *total) {
+                                                    uint32_t *prefix, uint32_t *total, Lim lim) {
     const uint64_t l = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
     if (l >= L) return;
     F29 acc;
-    uint2 e = pairs[l];
-    F29 nx1 = ld29_x_half(tab + PT * e.x), nx2 = ld29_x_half(tab + PT * e.y);
+    uint2 e = pairs[chk(l, lim.pairs, lim)];
+    F29 nx1 = ld29_x_half(tab + PT * chk(e.x, lim.tab_pts, lim)), nx2 = ld29_x_half(tab + PT * chk(e.y, lim.tab_pts, lim));
 #pragma unroll 1
     for (int k = 0; k < K; k++) {
         const F29 x1 = nx1, x2 = nx2;
         if (k + 1 < K) {
-            e = pairs[(uint64_t)(k + 1) * L + l];
-            nx1 = ld29_x_half(tab + PT * e.x);
-            nx2 = ld29_x_half(tab + PT * e.y);
+            e = pairs[chk((uint64_t)(k + 1) * L + l, lim.pairs, lim)];
+            nx1 = ld29_x_half(tab + PT * chk(e.x, lim.tab_pts, lim));
+            nx2 = ld29_x_half(tab + PT * chk(e.y, lim.tab_pts, lim));
         }
         const F29 d = sub29(x2, x1, F29_KB);
         acc = k ? mul29(acc, d) : d;
-        if (k + 1 < K) store_f29(prefix + 14 * ((uint64_t)k * L + l), acc);
+        if (k + 1 < K) store_f29(prefix + SF * chk((uint64_t)k * L + l, lim.pre_elems, lim), acc);
     }
-    store_f29(total + 14 * l, acc);
+    store_f29(total + SF * chk(l, lim.tot_elems, lim), acc);
 }
 
 // a^(q-2) in the Montgomery form (R = 2^406): the Montgomery form of a^-1
@@ -148,25 +167,25 @@ __device__ F29 inv29_fermat(const F29 &a) {
 
 // the lane totals (L of them) inverted: lanes of 64 totals (strided), prefix,
 // one Fermat inversion, back pass
-__global__ __launch_bounds__(256) void k_ba_inv_lvl2(uint32_t *total, uint64_t L, uint32_t *scratch) {
+__global__ __launch_bounds__(256) void k_ba_inv_lvl2(uint32_t *total, uint64_t L, uint32_t *scratch, Lim lim) {
     const uint64_t L2 = (L + 63) / 64;
     const uint64_t j = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
     if (j >= L2) return;
     F29 acc;
     int cnt = 0;
     for (uint64_t i = j; i < L; i += L2, cnt++) {
-        const F29 t = ld29(total + 14 * i);
+        const F29 t = ld29(total + SF * chk(i, lim.tot_elems, lim));
         acc = cnt ? mul29(acc, t) : t;
-        store_f29(scratch + 14 * i, acc);
+        store_f29(scratch + SF * chk(i, lim.tot_elems, lim), acc);
     }
     if (!cnt) return;
     F29 inv = inv29_fermat(acc);
     for (int c = cnt - 1; c >= 0; c--) {
         const uint64_t i = j + (uint64_t)c * L2;
-        const F29 t = ld29(total + 14 * i);
-        const F29 ti = c ? mul29(inv, ld29(scratch + 14 * (i - L2))) : inv;
+        const F29 t = ld29(total + SF * chk(i, lim.tot_elems, lim));
+        const F29 ti = c ? mul29(inv, ld29(scratch + SF * chk(i - L2, lim.tot_elems, lim))) : inv;
         if (c) inv = mul29(inv, t);
-        store_f29(total + 14 * i, ti);  // total[i] <- total[i]^-1
+        store_f29(total + SF * chk(i, lim.tot_elems, lim), ti);  // total[i] <- total[i]^-1
     }
 }
 
@@ -174,42 +193,37 @@ __global__ __launch_bounds__(256) void k_ba_inv_lvl2(uint32_t *total, uint64_t L
 template <bool PF>
 __global__ __launch_bounds__(256, PF ? 3 : 4) void k_ba_finish(const uint32_t *tab, const uint2 *pairs, uint64_t L,
                                                                 int K, const uint32_t *prefix,
-                                                                const uint32_t *total_inv, uint32_t *out) {
+                                                                const uint32_t *total_inv, uint32_t *out, Lim lim) {
     const uint64_t l = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
     if (l >= L) return;
-    F29 inv = ld29(total_inv + 14 * l);
+    F29 inv = ld29(total_inv + SF * chk(l, lim.tot_elems, lim));
     F29 nx1, ny1, nx2, ny2;
-    if (PF) {
-        const uint2 e = pairs[(uint64_t)(K - 1) * L + l];
-        const uint32_t *a = tab + PT * e.x, *b = tab + PT * e.y;
-        nx1 = ld29(a), ny1 = ld29(a + 14), nx2 = ld29(b), ny2 = ld29(b + 14);
-    }
+    auto gather = [&](int k, F29 &x1, F29 &y1, F29 &x2, F29 &y2) {
+        const uint2 e = pairs[chk((uint64_t)k * L + l, lim.pairs, lim)];
+        const uint32_t *a = tab + PT * chk(e.x, lim.tab_pts, lim), *b = tab + PT * chk(e.y, lim.tab_pts, lim);
+        x1 = ld29(a), y1 = ld29(a + 14), x2 = ld29(b), y2 = ld29(b + 14);
+    };
+    if (PF) gather(K - 1, nx1, ny1, nx2, ny2);
 #pragma unroll 1
     for (int k = K - 1; k >= 0; k--) {
-        F29 x1, y1, x2, y2, pk;
+        F29 x1, y1, x2, y2;
         if (PF) {
             x1 = nx1, y1 = ny1, x2 = nx2, y2 = ny2;
-            if (k) {
-                const uint2 e = pairs[(uint64_t)(k - 1) * L + l];
-                const uint32_t *a = tab + PT * e.x, *b = tab + PT * e.y;
-                nx1 = ld29(a), ny1 = ld29(a + 14), nx2 = ld29(b), ny2 = ld29(b + 14);
-            }
+            if (k) gather(k - 1, nx1, ny1, nx2, ny2);
         } else {
-            const uint2 e = pairs[(uint64_t)k * L + l];
-            const uint32_t *a = tab + PT * e.x, *b = tab + PT * e.y;
-            x1 = ld29(a), y1 = ld29(a + 14), x2 = ld29(b), y2 = ld29(b + 14);
+            gather(k, x1, y1, x2, y2);
         }
         const F29 d = sub29(x2, x1, F29_KB);
         F29 di = inv;
         if (k) {
-            pk = ld29(prefix + 14 * ((uint64_t)(k - 1) * L + l));
+            const F29 pk = ld29(prefix + SF * chk((uint64_t)(k - 1) * L + l, lim.pre_elems, lim));
             di = mul29(inv, pk);
             inv = mul29(inv, d);
         }
         const F29 lam = mul29(sub29(y2, y1, F29_KB), di);
         const F29 x3 = sub29(sub29(sqr29(lam), x1, F29_KA), x2, F29_KA);
         const F29 y3 = sub29(mul29(lam, sub29(x1, x3, F29_KB)), y1, F29_KA);
-        uint32_t *o = out + PT * ((uint64_t)k * L + l);
+        uint32_t *o = out + PT * chk((uint64_t)k * L + l, lim.out_pts, lim);
         store_f29(o, x3);
         store_f29(o + 14, y3);
     }
@@ -239,12 +253,15 @@ int main(int argc, char **argv) {
     std::vector<uint32_t> hi(2 * P);
     for (auto &v : hi) v = (uint32_t)(rnd() % T);
     uint32_t *tab, *idx, *pre, *tot, *scr, *out, *xo;
-    CK(hipMalloc(&tab, h.size() * 4));
-    CK(hipMalloc(&idx, hi.size() * 4));
+    CK(hipMalloc(&tab, h.size() * 4 + 256));
+    CK(hipMalloc(&idx, hi.size() * 4 + 256));
     CK(hipMemcpy(tab, h.data(), h.size() * 4, hipMemcpyHostToDevice));
     CK(hipMemcpy(idx, hi.data(), hi.size() * 4, hipMemcpyHostToDevice));
-    CK(hipMalloc(&pre, P * 56));
-    CK(hipMalloc(&out, P * 128));
+    CK(hipMalloc(&pre, P * SF * 4 + 256));
+    CK(hipMalloc(&out, P * 128 + 256));
+    uint32_t *bad;
+    CK(hipMalloc(&bad, 4));
+    CK(hipMemset(bad, 0, 4));
     hipEvent_t e0, e1, e2, e3;
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
@@ -256,7 +273,7 @@ int main(int argc, char **argv) {
     for (int K2 : {32, 64, 128})
     for (int pf = 0; pf < 2; pf++) {
         const uint64_t L2 = 2 * P / K2;
-        CK(hipMalloc(&xo, L2 * 224));
+        CK(hipMalloc(&xo, L2 * 224 + 256));
         float best = 1e30f;
         for (int rep = 0; rep < 3; rep++) {
             CK(hipEventRecord(e0));
@@ -280,23 +297,32 @@ int main(int argc, char **argv) {
     for (int K : {16, 32, 64, 128})
     for (int pf = 0; pf < 2; pf++) {
         const uint64_t L = P / K;
-        CK(hipMalloc(&tot, L * 56));
-        CK(hipMalloc(&scr, L * 56));
+        CK(hipMalloc(&tot, L * SF * 4 + 256));
+        CK(hipMalloc(&scr, L * SF * 4 + 256));
+        const Lim lim{T, P, P, L, P, bad};
         float b1 = 1e30f, b2 = 1e30f, b3 = 1e30f;
         for (int rep = 0; rep < 3; rep++) {
             CK(hipEventRecord(e0));
             hipLaunchKernelGGL(k_ba_prefix, dim3((uint32_t)((L + 255) / 256)), dim3(256), 0, 0, tab,
-                               reinterpret_cast<const uint2 *>(idx), L, K, pre, tot);
+                               reinterpret_cast<const uint2 *>(idx), L, K, pre, tot, lim);
             CK(hipEventRecord(e1));
+            if (rep == 0) {  // (the first round synchronises after every kernel: a fault names its kernel)
+                CK(hipEventSynchronize(e1));
+                fprintf(stderr, "K=%d pf=%d prefix ok\n", K, pf);
+            }
             const uint64_t L2 = (L + 63) / 64;
-            hipLaunchKernelGGL(k_ba_inv_lvl2, dim3((uint32_t)((L2 + 255) / 256)), dim3(256), 0, 0, tot, L, scr);
+            hipLaunchKernelGGL(k_ba_inv_lvl2, dim3((uint32_t)((L2 + 255) / 256)), dim3(256), 0, 0, tot, L, scr, lim);
             CK(hipEventRecord(e2));
+            if (rep == 0) {
+                CK(hipEventSynchronize(e2));
+                fprintf(stderr, "K=%d pf=%d inverse ok\n", K, pf);
+            }
             if (pf)
                 hipLaunchKernelGGL(k_ba_finish<true>, dim3((uint32_t)((L + 255) / 256)), dim3(256), 0, 0, tab,
-                                   reinterpret_cast<const uint2 *>(idx), L, K, pre, tot, out);
+                                   reinterpret_cast<const uint2 *>(idx), L, K, pre, tot, out, lim);
             else
                 hipLaunchKernelGGL(k_ba_finish<false>, dim3((uint32_t)((L + 255) / 256)), dim3(256), 0, 0, tab,
-                                   reinterpret_cast<const uint2 *>(idx), L, K, pre, tot, out);
+                                   reinterpret_cast<const uint2 *>(idx), L, K, pre, tot, out, lim);
             CK(hipEventRecord(e3));
             CK(hipEventSynchronize(e3));
             float m1, m2, m3;
@@ -306,10 +332,17 @@ int main(int argc, char **argv) {
             if (m1 + m2 + m3 < b1 + b2 + b3) b1 = m1, b2 = m2, b3 = m3;
         }
         CK(hipGetLastError());
+        uint32_t nbad = 0;
+        CK(hipMemcpy(&nbad, bad, 4, hipMemcpyDeviceToHost));
+        if (nbad) {
+            printf("batch-affine K=%d: %u out-of-range indices (clamped, not dereferenced)\n", K, nbad);
+            return 2;
+        }
         const double tot_ms = b1 + b2 + b3;
-        // algorithmic bytes per addition: pass 1: 8 B pair + 2 x 64 B x halves + 56 B prefix (K-1 of K);
-        // pass 2: 8 B + 2 x 128 B lines + 56 B prefix + 128 B out; the totals' level ~ 3 x 56 / K
-        const double bytes = 8 + 128 + 56.0 * (K - 1) / K + 8 + 256 + 56.0 * (K - 1) / K + 128 + 3 * 56.0 / K;
+        // bytes per addition as laid out here: pass 1: 8 B pair + 2 x 64 B x halves + 64 B prefix
+        // (K-1 of K); pass 2: 8 B + 2 x 128 B lines + 64 B prefix + 128 B out; the totals' level
+        // ~ 4 x 64 / K
+        const double bytes = 8 + 128 + 64.0 * (K - 1) / K + 8 + 256 + 64.0 * (K - 1) / K + 128 + 4 * 64.0 / K;
         printf("batch-affine K=%3d prefetch=%d: %8.3f ms (prefix %.3f, inverse %.3f, finish %.3f), %.1f ps per addition, "
                "%.0f B per addition (%.2f TB/s)\n",
                K, pf, tot_ms, b1, b2, b3, 1e9 * tot_ms / P, bytes, bytes * P / (tot_ms * 1e-3) / 1e12);

@@ -6,6 +6,7 @@
 //   rocprofv3 --pmc FETCH_SIZE -- ./ubench_gather
 #include <hip/hip_runtime.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <stdint.h>
 typedef __attribute__((address_space(3))) void lds_void_t;
 typedef __attribute__((address_space(1))) void glob_void_t;
@@ -31,8 +32,12 @@ __global__ __launch_bounds__(256) void k_gather(const uint32_t *table, uint64_t 
     out[blockIdx.x * 256 + threadIdx.x] = acc;
 }
 
-int main() {
-    const uint64_t nlines = 6ULL << 30 >> 7;  // 6 GiB of 128-B lines
+int main(int argc, char **argv) {
+    // table size in GiB (argv[1], default 6): the folded SRS table is 6.5 GiB,
+    // the copy-group table of HEIGHT = 15 35 GB (page-walk cost of random
+    // gathers over it)
+    const uint64_t gib = argc > 1 ? strtoull(argv[1], nullptr, 10) : 6;
+    const uint64_t nlines = gib << 30 >> 7;
     uint32_t *table, *out;
     if (hipMalloc(&table, nlines * 128) != hipSuccess) return 1;
     hipMemset(table, 1, nlines * 128);
@@ -48,7 +53,7 @@ int main() {
     hipEventSynchronize(e1);
     float ms; hipEventElapsedTime(&ms, e0, e1);
     const double lines = (double)blocks * 256 * steps;
-    printf("gathered lines per launch: %.0f  = %.3f GB at 128 B (%.3f GB used at 112 B); %.3f ms, %.1f GB/s (128 B)\n",
-           lines, lines * 128 / 1e9, lines * 112 / 1e9, ms, lines * 128 / (ms * 1e-3) / 1e9);
+    printf("table %llu GiB: gathered lines per launch: %.0f  = %.3f GB at 128 B (%.3f GB used at 112 B); %.3f ms, %.1f GB/s (128 B)\n",
+           (unsigned long long)gib, lines, lines * 128 / 1e9, lines * 112 / 1e9, ms, lines * 128 / (ms * 1e-3) / 1e9);
     return 0;
 }

@@ -36,7 +36,13 @@ std::atomic<uint64_t> g_dev_live{0}, g_dev_peak{0};
 void DevBuf::alloc(size_t b) {
     release();
     if (b == 0) b = 16;
-    hipError_t e = hipMalloc(&p, b);
+    // + 64 B past the end: the compiler widens the 8-byte tail load of an F29
+    // (ec29.cuh load29: 14 limbs read as 3 x 16 + 8 B) to 16 bytes on the
+    // assumption that the element is 16-B aligned; F29s at 56-B strides are only
+    // 8-B aligned, so the last one of an array whose end falls on a page boundary
+    // would read 8 bytes into the next page (found by tools/ubench_batch_affine
+    // faulting on exactly that, DESIGN.md 4 "Fault record")
+    hipError_t e = hipMalloc(&p, b + 64);
     if (e != hipSuccess) {
         p = nullptr;
         (void)hipGetLastError();  // clear the sticky out-of-memory status
@@ -83,6 +89,86 @@ const uint64_t *commit_table(pnp_ctx *ctx, uint64_t n) {
         ctx->ck_table_p1 = p1;
     }
     return ctx->ck_table.u64();
+}
+
+// Host -> HBM at PCIe speed from the caller's pageable buffers.  HIP's own
+// pageable copy stages through one host thread (the 19 GB prover key of
+// HEIGHT = 15 crossed in ~0.67 s, ~29 GB/s, profiles/r06_cold_calls.json);
+// here kStgThreads threads each memcpy 32-MiB chunks into two pinned staging
+// buffers of their own and DMA them on a stream of their own, so the host
+// copies and the DMAs of several chunks overlap.  Copies below 4 MiB go
+// through hipMemcpy directly.  PNP_H2D_STAGED=0: hipMemcpyAsync throughout.
+static bool h2d_staged_enabled() {
+    static const bool on = [] {
+        const char *e = getenv("PNP_H2D_STAGED");
+        return !(e && atoi(e) == 0);
+    }();
+    return on;
+}
+void h2d_batch(pnp_ctx *ctx, const std::vector<H2D> &copies) {
+    constexpr size_t CH = 32u << 20;
+    struct Chunk {
+        char *dst;
+        const char *src;
+        size_t bytes;
+    };
+    std::vector<Chunk> chunks;
+    for (const H2D &c : copies) {
+        if (!c.bytes) continue;
+        if (!h2d_staged_enabled() || c.bytes < (4u << 20)) {
+            PNP_HIP(hipMemcpyAsync(c.dst, c.src, c.bytes, hipMemcpyHostToDevice, ctx->stream));
+            continue;
+        }
+        for (size_t o = 0; o < c.bytes; o += CH)
+            chunks.push_back({static_cast<char *>(c.dst) + o, static_cast<const char *>(c.src) + o,
+                              std::min(CH, c.bytes - o)});
+    }
+    PNP_HIP(hipStreamSynchronize(ctx->stream));
+    if (chunks.empty()) return;
+    constexpr int T = pnp_ctx::kStgThreads;
+    if (!ctx->stg_buf[0]) {
+        for (int k = 0; k < 2 * T; k++) {
+            PNP_HIP(hipHostMalloc(&ctx->stg_buf[k], CH, hipHostMallocDefault));
+            PNP_HIP(hipEventCreateWithFlags(&ctx->stg_ev[k], hipEventDisableTiming));
+        }
+        for (int t = 0; t < T; t++) PNP_HIP(hipStreamCreateWithFlags(&ctx->stg_st[t], hipStreamNonBlocking));
+    }
+    std::atomic<size_t> next{0};
+    std::atomic<int> failed{0};
+    auto worker = [&](int t) {
+        try {
+            PNP_HIP(hipSetDevice(ctx->device));
+            int use = 0;
+            for (size_t j; (j = next.fetch_add(1)) < chunks.size() && !failed.load();) {
+                const int k = 2 * t + use;
+                use ^= 1;
+                PNP_HIP(hipEventSynchronize(ctx->stg_ev[k]));  // this buffer's previous DMA has landed
+                memcpy(ctx->stg_buf[k], chunks[j].src, chunks[j].bytes);
+                PNP_HIP(hipMemcpyAsync(chunks[j].dst, ctx->stg_buf[k], chunks[j].bytes, hipMemcpyHostToDevice,
+                                       ctx->stg_st[t]));
+                PNP_HIP(hipEventRecord(ctx->stg_ev[k], ctx->stg_st[t]));
+            }
+            PNP_HIP(hipStreamSynchronize(ctx->stg_st[t]));
+        } catch (...) {
+            failed.store(1);
+        }
+    };
+    std::vector<std::thread> th;
+    for (int t = 1; t < T; t++) th.emplace_back(worker, t);
+    worker(0);
+    for (auto &x : th) x.join();
+    if (failed.load()) {
+        set_error("host -> HBM staged upload failed");
+        throw Error(PNP_E_DEVICE);
+    }
+}
+static void h2d_release(pnp_ctx *ctx) {
+    for (int k = 0; k < 2 * pnp_ctx::kStgThreads; k++) {
+        if (ctx->stg_buf[k]) (void)hipHostFree(ctx->stg_buf[k]);
+        if (ctx->stg_ev[k]) (void)hipEventDestroy(ctx->stg_ev[k]);
+    }
+    for (int t = 0; t < pnp_ctx::kStgThreads; t++)
+        if (ctx->stg_st[t]) (void)hipStreamDestroy(ctx->stg_st[t]);
 }
 
 void ck_derived_reset(pnp_ctx *ctx) {
@@ -589,6 +675,7 @@ void pnp_ctx_destroy(pnp_ctx *ctx) {
         for (hipEvent_t e : {ctx->ev_fork, ctx->ev_w8, ctx->ev_z8}) (void)hipEventDestroy(e);
     }
     (void)hipStreamDestroy(ctx->stream);
+    h2d_release(ctx);
     for (hipEvent_t e : ctx->ktimer.pool) (void)hipEventDestroy(e);
     for (auto &p : ctx->ktimer.pending) {
         (void)hipEventDestroy(p.e0);
@@ -941,6 +1028,7 @@ int pnp_load_prover_key(pnp_ctx *ctx, const ProverKeyC *pk, uint64_t D, int devi
                                         : !host_all_zero(src[f], words);
             sel_nz[f] = sel_nz[f - 1] = nz;
         }
+        std::vector<H2D> up;  // host fields, uploaded together (h2d_batch)
         for (int f = 0; f < 44; f++) {
             FieldKind k = kPkKinds[f];
             dst[f] = nullptr;
@@ -959,10 +1047,11 @@ int pnp_load_prover_key(pnp_ctx *ctx, const ProverKeyC *pk, uint64_t D, int devi
             } else {
                 auto &o = ctx->pk_owned[f];
                 if (o.bytes != elems * 32) o.alloc(elems * 32);
-                PNP_HIP(hipMemcpyAsync(o.p, src[f], elems * 32, hipMemcpyHostToDevice, ctx->stream));
+                up.push_back({o.p, src[f], elems * 32});
                 dst[f] = o.u64();
             }
         }
+        h2d_batch(ctx, up);
         // key-derived constants, computed once per key instead of per proof:
         // zero-selector flags (the quotient kernel skips known-zero selectors)
         // and the sigma n-domain evaluations (gen_proof.cuh:159-165 recomputes
@@ -1156,7 +1245,7 @@ int pnp_load_commit_key(pnp_ctx *ctx, const CommitKeyC *ck, uint64_t n_points, i
             ctx->ck_hash_valid = false;
             // upload (as the reference does per call, load.cu:348-358)
             pnp::DevBuf up(n_points * 96);
-            PNP_HIP(hipMemcpyAsync(up.p, ck->powers_of_g, n_points * 96, hipMemcpyHostToDevice, ctx->stream));
+            h2d_batch(ctx, {{up.p, ck->powers_of_g, n_points * 96}});
             adopt_ck(ctx, up, n_points);
         }
     });
@@ -1427,6 +1516,30 @@ uint64_t ck_fingerprint(const CommitKeyC &ck, uint64_t D) {
 
 }  // namespace
 
+// The folded MSM table of a freshly uploaded SRS (what a context's first proof
+// builds first: ~0.19 s at 2^22) built on a stream of its own, from a thread of
+// its own (msm_build_table synchronises its stream and frees its level
+// buffers), while the caller uploads the prover key over PCIe — the v1 cold
+// call.  The first proof finds it (commit_table); if it could not be built
+// (e.g. out of HBM) the proof builds it as before.  One GPU: the whole table.
+static std::thread table_prebuild(pnp_ctx *ctx, uint64_t n) {
+    return std::thread([ctx, n] {
+        hipStream_t s = nullptr;
+        try {
+            PNP_HIP(hipSetDevice(ctx->device));
+            PNP_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+            ctx->ck_table_n = 0;
+            msm_build_table(ctx->ck_table, ctx->ck_dev, n, ctx->msm.fold_c, s);
+            ctx->ck_table_p0 = 0;
+            ctx->ck_table_p1 = n;
+            ctx->ck_table_n = n;
+        } catch (...) {
+            ctx->ck_table_n = 0;
+        }
+        if (s) (void)hipStreamDestroy(s);
+    });
+}
+
 extern "C" {
 
 // v1: lib/hello.cu:4-6.  Same contract as the reference (structs by value,
@@ -1509,9 +1622,11 @@ ProofC gen_proof(CircuitC circuit, ProverKeyC pk, CommitKeyC ck) {
             // both keys are uploaded whatever their hashes (a cold call: the
             // reference driver's one proof per process): hash them on the
             // other cores beside the uploads and the proof, for the next call
+            // (leaving this thread and the upload's copy threads their cores)
             unsigned T = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
             if (const char *e = getenv("OMP_NUM_THREADS")) T = std::max(1, std::min(atoi(e), 64));
-            const unsigned cap = T > 1 ? T - 1 : 1;
+            const unsigned busy = 1 + pnp_ctx::kStgThreads;
+            const unsigned cap = T > busy + 1 ? T - busy : 1;
             bool hash_ok = true;
             std::array<uint64_t, 2> ahp{}, ahc{};
             std::thread hasher([&] {
@@ -1525,22 +1640,29 @@ ProofC gen_proof(CircuitC circuit, ProverKeyC pk, CommitKeyC ck) {
             int lrc = PNP_OK;
             bool envelope = true;
             double ms_pk = 0, ms_ck = 0, ms_prove = 0;
+            std::thread tb;
             try {
+                // the SRS first: its folded table builds on the GPU (table_prebuild)
+                // while the prover key crosses PCIe
                 auto t = clk::now();
-                if ((lrc = pnp_load_prover_key(ctx, &pk, D, 0)) == PNP_OK) {
-                    envelope = !strict || (ctx->pk_qm_zero && ctx->pk_qlookup_zero && !ctx->pk_custom_nz[0] &&
-                                           !ctx->pk_custom_nz[1] && !ctx->pk_custom_nz[2] &&
-                                           !ctx->pk_custom_nz[3] && key_tables_zero(ctx));
-                    ms_pk = ms_since(t);
+                if ((lrc = pnp_load_commit_key(ctx, &ck, D, 0)) == PNP_OK) {
+                    ms_ck = ms_since(t);
+                    if (ctx->msm.world <= 1 && ctx->ck_table_n != D) tb = table_prebuild(ctx, D);
                     t = clk::now();
-                    if (envelope && (lrc = pnp_load_commit_key(ctx, &ck, D, 0)) == PNP_OK) {
-                        ms_ck = ms_since(t);
+                    lrc = pnp_load_prover_key(ctx, &pk, D, 0);
+                    if (tb.joinable()) tb.join();
+                    if (lrc == PNP_OK) {
+                        envelope = !strict || (ctx->pk_qm_zero && ctx->pk_qlookup_zero && !ctx->pk_custom_nz[0] &&
+                                               !ctx->pk_custom_nz[1] && !ctx->pk_custom_nz[2] &&
+                                               !ctx->pk_custom_nz[3] && key_tables_zero(ctx));
+                        ms_pk = ms_since(t);
                         t = clk::now();
-                        lrc = pnp_prove(ctx, &circuit, 0, &out);
+                        if (envelope) lrc = pnp_prove(ctx, &circuit, 0, &out);
                         ms_prove = ms_since(t);
                     }
                 }
             } catch (...) {
+                if (tb.joinable()) tb.join();
                 hasher.join();
                 throw;
             }

@@ -19,6 +19,12 @@ struct pnp_ctx {
     pnp::NttTables ntt;
     pnp::MsmWork msm;
     pnp::DevBuf scratch_a, scratch_b;
+    // pinned staging of the host -> HBM uploads (abi.cpp h2d_batch): per copy
+    // thread two chunks, a stream and an event per chunk; made on first use
+    static constexpr int kStgThreads = 4;
+    void *stg_buf[2 * kStgThreads] = {};
+    hipStream_t stg_st[kStgThreads] = {};
+    hipEvent_t stg_ev[2 * kStgThreads] = {};
 
     // ---- resident prover key (ProverKeyC mirrored in HBM) ----
     bool pk_loaded = false;
@@ -155,6 +161,14 @@ Fr fr_from_u64(uint64_t x);
 void ck_derived_reset(pnp_ctx *ctx);
 // commitments over the resident SRS (folded MSM)
 const uint64_t *commit_table(pnp_ctx *ctx, uint64_t n);
+// host -> HBM copies of caller buffers (pageable memory) through pinned
+// staging chunks, several copy threads at once; returns when they have landed
+struct H2D {
+    void *dst;
+    const void *src;
+    size_t bytes;
+};
+void h2d_batch(pnp_ctx *ctx, const std::vector<H2D> &copies);
 // the folded table of the Lagrange-basis SRS of size n (this rank's point
 // range), nullptr when it is unavailable (PNP_LAGRANGE=0, n not a power of
 // two or above the key, degenerate key)

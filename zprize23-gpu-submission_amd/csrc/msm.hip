@@ -1038,7 +1038,7 @@ __global__ __launch_bounds__(256, PNP_ACC_WAVES) void k_accumulate29(const uint3
                                                       uint32_t *buckets, uint32_t *head,
                                                       uint32_t *tail, uint32_t *tailb, uint32_t *redo,
                                                       uint32_t *nredo, uint32_t *tlist) {
-#if PNP_ACC_GLDS
+#if PNP_ACC_GLDS == 1
     // per wave: the staged point (7 x 64 x 16 B) and the staged next index
     // (64 x 4 B); both arrive by LDS-DMA, so no ordinary global load result is
     // consumed inside the loop (that would make the compiler drain the DMA)
@@ -1064,11 +1064,16 @@ __global__ __launch_bounds__(256, PNP_ACC_WAVES) void k_accumulate29(const uint3
     uint32_t next = offs[cur + 1];
     bool ok = true, fresh = true;
     Xyzz29 acc;
-#if PNP_ACC_GLDS
+#if PNP_ACC_GLDS == 1
     uint32_t e = sorted[lo];
     stage_point(pts29 + PT29 * (e & 0x7FFFFFFFu), wave_base);
     if (lo + 1 < hi)
         __builtin_amdgcn_global_load_lds((glob_void_t *)(sorted + lo + 1), (lds_void_t *)idx_base, 4, 0, 0);
+#elif PNP_ACC_GLDS == 2
+    // (2: the next point prefetched into registers, the index after it too)
+    uint32_t e = sorted[lo];
+    F29 nx = load29(pts29 + PT29 * (e & 0x7FFFFFFFu)), ny = load29(pts29 + PT29 * (e & 0x7FFFFFFFu) + 14);
+    uint32_t en = lo + 1 < hi ? sorted[lo + 1] : 0u;
 #endif
     for (uint32_t k = lo; k < hi; k++) {
         if (k == next) {
@@ -1077,7 +1082,18 @@ __global__ __launch_bounds__(256, PNP_ACC_WAVES) void k_accumulate29(const uint3
             fresh = true;
             cur = next_bucket(offs, 1, U, cur + 1, k, next);
         }
-#if PNP_ACC_GLDS
+#if PNP_ACC_GLDS == 2
+        F29 x = nx, y = ny;
+        const uint32_t ecur = e;
+        if (k + 1 < hi) {
+            const uint32_t *p = pts29 + PT29 * (en & 0x7FFFFFFFu);
+            nx = load29(p);
+            ny = load29(p + 14);
+            e = en;
+            if (k + 2 < hi) en = sorted[k + 2];
+        }
+        if (ecur >> 31) y = neg29(y, F29_KA);
+#elif PNP_ACC_GLDS
         F29 x, y;
         __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): point k and index k+1 have landed
         unstage_point(wave_base + ln, x, y);

@@ -252,15 +252,18 @@ int prove_impl(pnp_ctx *ctx, const CircuitC *cs, int device_ptrs, ProofC *out, c
     // ---------------- inputs: padded witness evaluations (pad_poly)
     uint64_t *wsc[4], *wpoly[4];
     const uint64_t *wsrc[4] = {cs->w_l, cs->w_r, cs->w_o, cs->w_4};
-    const hipMemcpyKind kind = device_ptrs ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
+    std::vector<H2D> up;  // a host witness: staged uploads (abi.cpp h2d_batch)
     for (int j = 0; j < 4; j++) {
         wsc[j] = ctx->buf("wsc" + std::to_string(j), n);
         wpoly[j] = ctx->buf("wpoly" + std::to_string(j), n);
-        PNP_HIP(hipMemcpyAsync(wsc[j], wsrc[j], 32 * ng, kind, s));
+        if (device_ptrs) PNP_HIP(hipMemcpyAsync(wsc[j], wsrc[j], 32 * ng, hipMemcpyDeviceToDevice, s));
+        else up.push_back({wsc[j], wsrc[j], 32 * ng});
         if (n > ng) PNP_HIP(hipMemsetAsync(wsc[j] + 4 * ng, 0, 32 * (n - ng), s));
     }
     uint64_t *qlk = ctx->buf("qlk", n);
-    PNP_HIP(hipMemcpyAsync(qlk, cs->q_lookup, 32 * ng, kind, s));
+    if (device_ptrs) PNP_HIP(hipMemcpyAsync(qlk, cs->q_lookup, 32 * ng, hipMemcpyDeviceToDevice, s));
+    else up.push_back({qlk, cs->q_lookup, 32 * ng});
+    if (!up.empty()) h2d_batch(ctx, up);
     alg(4.0 * (2 * ng + (n - ng)) + 2.0 * ng);
     tm.mark("inputs");
 
