@@ -193,7 +193,7 @@ def mad_cycles():
     return 4.1  # DESIGN.md 4 (round 1 measurement)
 
 
-PMC_FILE = os.path.join(REPO, "profiles", "r05_accumulate_traffic.json")
+PMC_FILE = os.path.join(REPO, "profiles", "r06_accumulate_traffic.json")
 def parallelism_label(world: int) -> str:
     """what the multi-rank proof shards: the MSMs by bucket ranges from
     PNP_MSM_BUCKETS_MIN_WORLD (4) ranks on, else by point ranges (msm.hip);

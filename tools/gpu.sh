@@ -53,7 +53,10 @@ run_step() {
     pmc*)
       local c=${arg:-SQ_WAVES+SQ_INSTS_VALU+SQ_WAVE_CYCLES+SQ_WAIT_ANY+SQ_WAIT_INST_ANY+SQ_ACTIVE_INST_ANY+SQ_ACTIVE_INST_VALU+SQ_INSTS_SALU}
       local d=$OUT/pmc_$(echo "$c" | tr '+' '_' | cut -c1-40)
-      (cd /tmp && export TMPDIR=/tmp && timeout -s KILL 200 rocprofv3 --pmc ${c//+/ } --kernel-include-regex "$RX" -f csv \
+      # the one profiled proof is the process's first: without PNP_DEFER_TABLES=0
+      # it defers the Lagrange / copy-group tables and commits the wires and z
+      # densely — not the steady-state proof the bench times
+      (cd /tmp && export TMPDIR=/tmp && export PNP_DEFER_TABLES=${PNP_DEFER_TABLES:-0} && timeout -s KILL 200 rocprofv3 --pmc ${c//+/ } --kernel-include-regex "$RX" -f csv \
           -d "$d" -o run -- python3 "$R/bench.py" --steps 1 --warmup 0 --cpu-lg 0 --drop-in "" --no-verify \
           ${PMC_BENCH_ARGS:-} > "$d.log" 2>&1) ;;
     traffic)

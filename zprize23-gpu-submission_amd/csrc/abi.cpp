@@ -94,10 +94,12 @@ const uint64_t *commit_table(pnp_ctx *ctx, uint64_t n) {
 // Host -> HBM at PCIe speed from the caller's pageable buffers.  HIP's own
 // pageable copy stages through one host thread (the 19 GB prover key of
 // HEIGHT = 15 crossed in ~0.67 s, ~29 GB/s, profiles/r06_cold_calls.json);
-// here kStgThreads threads each memcpy 32-MiB chunks into two pinned staging
+// here kStgThreads threads each memcpy 8-MiB chunks into two pinned staging
 // buffers of their own and DMA them on a stream of their own, so the host
-// copies and the DMAs of several chunks overlap.  Copies below 4 MiB go
-// through hipMemcpy directly.  PNP_H2D_STAGED=0: hipMemcpyAsync throughout.
+// copies and the DMAs of several chunks overlap (small chunks: pinning the
+// staging memory is the fixed cost of a cold call, ~0.4 ms per MiB).  Copies
+// below 4 MiB go through hipMemcpy directly.  PNP_H2D_STAGED=0:
+// hipMemcpyAsync throughout.
 static bool h2d_staged_enabled() {
     static const bool on = [] {
         const char *e = getenv("PNP_H2D_STAGED");
@@ -106,7 +108,7 @@ static bool h2d_staged_enabled() {
     return on;
 }
 void h2d_batch(pnp_ctx *ctx, const std::vector<H2D> &copies) {
-    constexpr size_t CH = 32u << 20;
+    constexpr size_t CH = 8u << 20;
     struct Chunk {
         char *dst;
         const char *src;

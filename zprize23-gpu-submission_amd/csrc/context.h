@@ -21,7 +21,7 @@ struct pnp_ctx {
     pnp::DevBuf scratch_a, scratch_b;
     // pinned staging of the host -> HBM uploads (abi.cpp h2d_batch): per copy
     // thread two chunks, a stream and an event per chunk; made on first use
-    static constexpr int kStgThreads = 4;
+    static constexpr int kStgThreads = 6;
     void *stg_buf[2 * kStgThreads] = {};
     hipStream_t stg_st[kStgThreads] = {};
     hipEvent_t stg_ev[2 * kStgThreads] = {};
