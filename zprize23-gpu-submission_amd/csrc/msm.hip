@@ -1034,7 +1034,7 @@ __device__ __forceinline__ void unstage_point(const uint4 *st, F29 &x, F29 &y) {
 }
 
 __global__ __launch_bounds__(256, PNP_ACC_WAVES) void k_accumulate29(const uint32_t *pts29, const uint32_t *sorted,
-                                                      const uint32_t *offs, uint64_t U, uint32_t S,
+                                                      const uint32_t *offs, uint64_t U, uint64_t nthr, uint32_t S,
                                                       uint32_t *buckets, uint32_t *head,
                                                       uint32_t *tail, uint32_t *tailb, uint32_t *redo,
                                                       uint32_t *nredo, uint32_t *tlist) {
@@ -1050,6 +1050,7 @@ __global__ __launch_bounds__(256, PNP_ACC_WAVES) void k_accumulate29(const uint3
 #endif
     uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
     const uint32_t total = offs[U];
+    S = acc_seg(offs, U, nthr, S);
     const uint64_t lo64 = t * S;
     if (lo64 >= total) return;
     const uint32_t lo = (uint32_t)lo64;
@@ -1152,8 +1153,9 @@ __global__ __launch_bounds__(256, PNP_ACC_WAVES) void k_accumulate29(const uint3
 // the ~2M-bucket launch takes microseconds, not the ~0.3 ms one contended
 // counter cost); the host sums them.
 constexpr int WCTR_SLOTS = 64;
-__global__ __launch_bounds__(1024) void k_count_pieces(const uint32_t *offs, uint64_t WB, uint32_t S,
+__global__ __launch_bounds__(1024) void k_count_pieces(const uint32_t *offs, uint64_t WB, uint64_t nthr, uint32_t S,
                                                        unsigned long long *ctr) {
+    S = acc_seg(offs, WB, nthr, S);
     __shared__ uint32_t part[16];
     const uint64_t b = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
     bool fresh = false;
@@ -1178,7 +1180,7 @@ __global__ __launch_bounds__(1024) void k_count_pieces(const uint32_t *offs, uin
 
 // exact 32-bit recomputation of the segments k_accumulate29 flagged
 __global__ __launch_bounds__(64) void k_accumulate_redo(const uint32_t *pts29, const uint32_t *sorted,
-                                                        const uint32_t *offs, uint64_t U, uint32_t S,
+                                                        const uint32_t *offs, uint64_t U, uint64_t nthr, uint32_t S,
                                                         uint32_t *buckets, uint32_t *head,
                                                         uint32_t *tail, const uint32_t *redo,
                                                         const uint32_t *nredo) {
@@ -1196,6 +1198,7 @@ __global__ __launch_bounds__(64) void k_accumulate_redo(const uint32_t *pts29, c
         store_f29(d + 42, from_fq32(p.zzz));
     };
     const uint32_t cnt = *nredo;
+    S = acc_seg(offs, U, nthr, S);
     for (uint32_t r = blockIdx.x * blockDim.x + threadIdx.x; r < cnt; r += gridDim.x * blockDim.x)
         segment32(redo[r], ld, st, sorted, offs, 1, U, S);
 }
@@ -1458,13 +1461,13 @@ static void accumulate_group(MsmWork &wk, MsmGroup &gb, const GroupPlan &gp, con
         PNP_HIP(hipMemsetAsync(nredo, 0, 4, s));
         const uint32_t *t29 = reinterpret_cast<const uint32_t *>(table);
         const uint32_t blocks = (uint32_t)((nthr + 255) / 256);
-        hipLaunchKernelGGL(k_accumulate29, dim3(blocks), dim3(256), 0, s, t29, sorted, bstart, WB, S, bk29,
+        hipLaunchKernelGGL(k_accumulate29, dim3(blocks), dim3(256), 0, s, t29, sorted, bstart, WB, nthr, S, bk29,
                            head, tail, tailb, redo, nredo, tlist);
         PNP_HIP(hipGetLastError());
         // equal / opposite points or infinity inside a piece: exact recomputation
         // of the flagged lanes (the count stays on the device: no host sync)
         hipLaunchKernelGGL(k_accumulate_redo, dim3((uint32_t)std::min<uint64_t>((nthr + 63) / 64, 1024)), dim3(64), 0, s, t29,
-                           sorted, bstart, WB, S, bk29, head, tail, redo, nredo);
+                           sorted, bstart, WB, nthr, S, bk29, head, tail, redo, nredo);
         PNP_HIP(hipGetLastError());
         // split buckets into bk29 (in place, F29; empty ones stay unwritten), reduced by msm_reduce29
         need(gb.exc, 16);
@@ -1492,7 +1495,7 @@ static void accumulate_group(MsmWork &wk, MsmGroup &gb, const GroupPlan &gp, con
         if (table) {  // the real work, counted on the device (k_count_pieces)
             need(gb.wctr, 8 * (1 + WCTR_SLOTS));
             PNP_HIP(hipMemsetAsync(gb.wctr.p, 0, 8 * (1 + WCTR_SLOTS), s));
-            hipLaunchKernelGGL(k_count_pieces, dim3((uint32_t)((WB + 1023) / 1024)), dim3(1024), 0, s, bstart, WB, S,
+            hipLaunchKernelGGL(k_count_pieces, dim3((uint32_t)((WB + 1023) / 1024)), dim3(1024), 0, s, bstart, WB, nthr, S,
                                static_cast<unsigned long long *>(gb.wctr.p));
             PNP_HIP(hipGetLastError());
             gb.wctr_live = true;
@@ -1534,7 +1537,7 @@ static const uint64_t *reduce_group_exact(MsmGroup &gb, const GroupPlan &gp, con
     uint64_t *bk = gb.buckets.u64();
     const uint32_t *bk29 = static_cast<const uint32_t *>(gb.seg.p);
     const uint32_t *head = bk29 + 56 * WB, *tail = head + 56 * gb.nthr;
-    msm_merge_pieces29_exact(static_cast<const uint32_t *>(gb.offsets.p), WB, gb.S, gb.pieces, bk29, head, tail,
+    msm_merge_pieces29_exact(static_cast<const uint32_t *>(gb.offsets.p), WB, gb.S, gb.nthr, gb.pieces, bk29, head, tail,
                              bk, s);
     return msm_reduce(bk, (uint64_t)gp.nv, g.NB, bk + WB * 24, s);
 }

@@ -59,11 +59,36 @@ void msm_merge_pieces(const uint32_t *offs, int nch, uint64_t U, uint32_t S, uin
 // msm_reduce29.)  `heavy`: U + 1 u32 of scratch (count, then the queued
 // buckets of > 64 pieces).
 constexpr uint32_t NO_TAIL = 0xFFFFFFFFu;
+
+// Segment length of an accumulation launch.  The host sizes the launch (nthr
+// lanes of S entries, whole rounds of the chip's wave slots) from an upper
+// bound of the sorted entries — MSMs x windows x points, or the fixed slots'
+// capacity — before the sort has counted them; zero digits, copy groups and
+// padding rows drop out, so a launch can hold far fewer (round 1's wires: 82 M
+// of 218 M), and lanes of S entries then leave part of the chip idle (a round
+// 0.74 full at rank 0 of 8).  PNP_ACC_DEVSEG=1: every kernel that walks the
+// segments takes S = ceil(total / nthr) from the device count instead (never
+// above the host's S, at least 16), so the launch's lanes share the real
+// entries evenly; all of them compute the same S from offs[U]
+#ifndef PNP_ACC_DEVSEG
+#define PNP_ACC_DEVSEG 1
+#endif
+__device__ __forceinline__ uint32_t acc_seg(const uint32_t *offs, uint64_t U, uint64_t nthr, uint32_t S) {
+#if PNP_ACC_DEVSEG
+    const uint64_t total = offs[U];
+    uint64_t d = (total + nthr - 1) / nthr;
+    d = d < 16 ? 16 : d;
+    return d < S ? (uint32_t)d : S;
+#else
+    (void)offs, (void)U, (void)nthr;
+    return S;
+#endif
+}
 void msm_merge_pieces29(const uint32_t *offs, uint64_t U, uint32_t S, uint64_t nthr, const uint32_t *tailb,
                         const uint32_t *tlist, uint32_t *bk29, const uint32_t *head, const uint32_t *tail, uint32_t *exc,
                         uint32_t *heavy, hipStream_t s);
 // exact fallback: the same pieces summed in 32-bit Fq into bk (R384)
-void msm_merge_pieces29_exact(const uint32_t *offs, uint64_t U, uint32_t S, uint32_t pieces,
+void msm_merge_pieces29_exact(const uint32_t *offs, uint64_t U, uint32_t S, uint64_t nthr, uint32_t pieces,
                               const uint32_t *bk29, const uint32_t *head, const uint32_t *tail, uint64_t *bk,
                               hipStream_t s);
 

@@ -147,12 +147,13 @@ constexpr uint32_t MERGE_HEAVY = PNP_MERGE_HEAVY;
 // One merge lane per listed tail (tlist: the accumulation lanes that left
 // one, compacted by k_accumulate29): a wave is 64 merges, where one lane per
 // accumulation lane ran ~1 in 3 of its lanes (a segment of ~3 buckets splits one)
-__global__ __launch_bounds__(256) void k_merge_tails29(const uint32_t *offs, uint32_t S, const uint32_t *tailb,
-                                                       const uint32_t *tlist, uint32_t *bk29, const uint32_t *head,
-                                                       const uint32_t *tail, uint32_t *exc, uint32_t *heavy,
-                                                       uint32_t *nheavy) {
+__global__ __launch_bounds__(256) void k_merge_tails29(const uint32_t *offs, uint64_t U, uint64_t nthr, uint32_t S,
+                                                       const uint32_t *tailb, const uint32_t *tlist, uint32_t *bk29,
+                                                       const uint32_t *head, const uint32_t *tail, uint32_t *exc,
+                                                       uint32_t *heavy, uint32_t *nheavy) {
     const uint64_t q = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
     if (q >= tlist[0]) return;
+    S = acc_seg(offs, U, nthr, S);
     const uint64_t t = tlist[1 + q];
     const uint32_t u = tailb[t];
     const uint32_t t1 = (offs[u + 1] - 1) / S;
@@ -169,11 +170,12 @@ __global__ __launch_bounds__(256) void k_merge_tails29(const uint32_t *offs, uin
 // the queued heavy buckets, one workgroup each (grid-stride over the queue):
 // 256 lanes sum every 256th piece, then an LDS tree of log2 of the lanes that
 // hold a piece (8 levels from 128 pieces on, 4 for a bucket of 16)
-__global__ __launch_bounds__(256) void k_merge_heavy29(const uint32_t *offs, uint32_t S, uint32_t *bk29,
-                                                       const uint32_t *head, const uint32_t *tail, uint32_t *exc,
-                                                       const uint32_t *heavy, const uint32_t *nheavy) {
+__global__ __launch_bounds__(256) void k_merge_heavy29(const uint32_t *offs, uint64_t U, uint64_t nthr, uint32_t S,
+                                                       uint32_t *bk29, const uint32_t *head, const uint32_t *tail,
+                                                       uint32_t *exc, const uint32_t *heavy, const uint32_t *nheavy) {
     __shared__ uint32_t lds[256 * 56];
     const uint32_t cnt = *nheavy;
+    S = acc_seg(offs, U, nthr, S);
     uint32_t *mine = lds + 56 * threadIdx.x;
     for (uint32_t q = blockIdx.x; q < cnt; q += gridDim.x) {
         const uint32_t g = heavy[q];
@@ -200,16 +202,15 @@ __global__ __launch_bounds__(256) void k_merge_heavy29(const uint32_t *offs, uin
 void msm_merge_pieces29(const uint32_t *offs, uint64_t U, uint32_t S, uint64_t nthr, const uint32_t *tailb,
                         const uint32_t *tlist, uint32_t *bk29, const uint32_t *head, const uint32_t *tail,
                         uint32_t *exc, uint32_t *heavy, hipStream_t s) {
-    (void)U;
     uint32_t *nheavy = heavy, *list = heavy + 1;
     PNP_HIP(hipMemsetAsync(nheavy, 0, 4, s));
     // (the count stays on the device: a grid for every accumulation lane, the
     // waves past the count exit at once)
-    hipLaunchKernelGGL(k_merge_tails29, dim3((uint32_t)((nthr + 255) / 256)), dim3(256), 0, s, offs, S, tailb, tlist,
-                       bk29, head, tail, exc, list, nheavy);
+    hipLaunchKernelGGL(k_merge_tails29, dim3((uint32_t)((nthr + 255) / 256)), dim3(256), 0, s, offs, U, nthr, S,
+                       tailb, tlist, bk29, head, tail, exc, list, nheavy);
     PNP_HIP(hipGetLastError());
     // a small grid: it exits at once when nothing was queued
-    hipLaunchKernelGGL(k_merge_heavy29, dim3(256), dim3(256), 0, s, offs, S, bk29, head, tail, exc, list,
+    hipLaunchKernelGGL(k_merge_heavy29, dim3(256), dim3(256), 0, s, offs, U, nthr, S, bk29, head, tail, exc, list,
                        nheavy);
     PNP_HIP(hipGetLastError());
 }
@@ -220,11 +221,12 @@ void msm_merge_pieces29(const uint32_t *offs, uint64_t U, uint32_t S, uint64_t n
 // (the F29 merge writes only split and empty buckets).  Writes bk (R384) for
 // the 32-bit msm_reduce.
 __device__ __forceinline__ Xyzz piece29(const uint32_t *p) { return to32(load_xyzz29(p)); }
-__global__ __launch_bounds__(256) void k_merge_pieces29_exact(const uint32_t *offs, uint64_t U, uint32_t S,
-                                                              int G, const uint32_t *bk29,
+__global__ __launch_bounds__(256) void k_merge_pieces29_exact(const uint32_t *offs, uint64_t U, uint64_t nthr,
+                                                              uint32_t S, int G, const uint32_t *bk29,
                                                               const uint32_t *head, const uint32_t *tail,
                                                               uint64_t *bk) {
     __shared__ uint64_t lds[256 * 24];
+    S = acc_seg(offs, U, nthr, S);
     const uint64_t g = (blockIdx.x * (uint64_t)blockDim.x + threadIdx.x) / G;
     const int j = threadIdx.x % G;
     bool live = false;
@@ -255,13 +257,13 @@ __global__ __launch_bounds__(256) void k_merge_pieces29_exact(const uint32_t *of
     if (live && j == 0) store_xyzz(bk + 24 * g, acc);
 }
 
-void msm_merge_pieces29_exact(const uint32_t *offs, uint64_t U, uint32_t S, uint32_t pieces,
+void msm_merge_pieces29_exact(const uint32_t *offs, uint64_t U, uint32_t S, uint64_t nthr, uint32_t pieces,
                               const uint32_t *bk29, const uint32_t *head, const uint32_t *tail, uint64_t *bk,
                               hipStream_t s) {
     int G = 1;
     while (G < 8 && (uint32_t)G * 8 <= pieces) G *= 2;
     const uint64_t blocks = (U * G + 255) / 256;
-    hipLaunchKernelGGL(k_merge_pieces29_exact, dim3((uint32_t)blocks), dim3(256), 0, s, offs, U, S, G, bk29,
+    hipLaunchKernelGGL(k_merge_pieces29_exact, dim3((uint32_t)blocks), dim3(256), 0, s, offs, U, nthr, S, G, bk29,
                        head, tail, bk);
     PNP_HIP(hipGetLastError());
 }
