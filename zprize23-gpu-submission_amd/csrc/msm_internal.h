@@ -69,9 +69,12 @@ constexpr uint32_t NO_TAIL = 0xFFFFFFFFu;
 // 0.74 full at rank 0 of 8).  PNP_ACC_DEVSEG=1: every kernel that walks the
 // segments takes S = ceil(total / nthr) from the device count instead (never
 // above the host's S, at least 16), so the launch's lanes share the real
-// entries evenly; all of them compute the same S from offs[U]
+// entries evenly; all of them compute the same S from offs[U].  Measured
+// (same box, 3 interleaved rounds, profiles/r06_ab_devseg_leaf.txt): one GPU
+// 0.1284 -> 0.1299 s (the shorter segments split more buckets: more pieces
+// to store and merge), rank 0 of 8 neutral (28.5 vs 28.6 ms) — off
 #ifndef PNP_ACC_DEVSEG
-#define PNP_ACC_DEVSEG 1
+#define PNP_ACC_DEVSEG 0
 #endif
 __device__ __forceinline__ uint32_t acc_seg(const uint32_t *offs, uint64_t U, uint64_t nthr, uint32_t S) {
 #if PNP_ACC_DEVSEG

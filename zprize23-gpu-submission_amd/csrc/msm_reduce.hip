@@ -341,8 +341,16 @@ __global__ void k_tree_roots29(const uint32_t *in, uint64_t n, uint64_t *out) {
 
 const uint64_t *msm_reduce29(const uint32_t *bk29, const uint32_t *offs, uint64_t nwin, int NB,
                              uint32_t *scratch, uint32_t *exc, hipStream_t s) {
-    // leaves of PNP_LEAF_W buckets (pairs for the small windows of small MSMs)
-    const int LW = NB >= 2 * PNP_LEAF_W ? PNP_LEAF_W : 2;
+    // leaves of PNP_LEAF_W buckets (pairs for the small windows of small MSMs);
+    // 4 for the bucket ranges of 8 ranks (NB <= 2^16 a window): there the
+    // leaves are latency-bound, a leaf's running sum costs 2 dependent
+    // additions per bucket and a tree level 2, so narrower leaves and one more
+    // level are shorter — rank 0 of 8 28.6 -> 28.2 ms, one GPU unaffected
+    // (its 2^19-bucket windows keep 8; profiles/r06_ab_devseg_leaf.txt)
+#ifndef PNP_LEAF_SMALL4
+#define PNP_LEAF_SMALL4 1
+#endif
+    const int LW = NB >= 2 * PNP_LEAF_W ? (PNP_LEAF_SMALL4 && NB <= (1 << 16) && PNP_LEAF_W > 4 ? 4 : PNP_LEAF_W) : 2;
     if (NB < 2 * LW) {
         set_error("msm_reduce29: %d buckets per window", NB);
         throw Error(PNP_E_ARG);
@@ -353,6 +361,8 @@ const uint64_t *msm_reduce29(const uint32_t *bk29, const uint32_t *offs, uint64_
     const dim3 lgrid((uint32_t)((m + 255) / 256));
     if (LW == 2)
         hipLaunchKernelGGL(k_tree_leafw29<2>, lgrid, dim3(256), 0, s, bk29, offs, m, a, exc);
+    else if (LW == 4)
+        hipLaunchKernelGGL(k_tree_leafw29<4>, lgrid, dim3(256), 0, s, bk29, offs, m, a, exc);
     else
         hipLaunchKernelGGL(k_tree_leafw29<PNP_LEAF_W>, lgrid, dim3(256), 0, s, bk29, offs, m, a, exc);
     PNP_HIP(hipGetLastError());
