@@ -363,6 +363,26 @@ def test_hbm_short_rank_fails_every_load(tmp_path, world):
         assert open(f"{prefix}.{r}").read() == "ok", f"rank {r}"
 
 
+@pytest.mark.gpu
+def test_v1_one_proof_per_fresh_process():
+    """The v1 symbol as the reference driver calls it (merkle-tree/src/main.rs:
+    102-103: one gen_proof per process, keys in host memory), through
+    tools/cold_call.py: a producer process writes a HEIGHT=9 Merkle instance's
+    host arrays, two fresh processes (no torch) each dlopen the library and
+    make ONE v1 call — the SRS table built beside the prover-key upload, the
+    8n key arrays (16 MiB each at 2^16) crossing through the staged chunks —
+    and each proof equals the producer's v2 proof.  With the multi-process
+    tests: the parent has made no GPU call."""
+    sys.path.insert(0, os.path.join(os.path.dirname(HERE), "tools"))
+    import cold_call
+    res = cold_call.measure(16, 2, seed=3)
+    assert "v1_process_cold_error" not in res, res.get("v1_process_cold_error")
+    assert res["v1_process_cold_equals_v2"], res
+    for run in res["v1_process_cold_runs"]:
+        st = run["stages_ms"]
+        assert st["v1_call"] > 0 and "v1_load_prover_key" in st and "r1_commit" in st, st
+
+
 def test_bystander_guard(tmp_path, monkeypatch):
     """4+ ranks beside a pytest process that has loaded the library fail at
     once with the reason (the shard-test crawl), instead of
