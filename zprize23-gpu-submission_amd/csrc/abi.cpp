@@ -153,6 +153,7 @@ void h2d_batch(pnp_ctx *ctx, const std::vector<H2D> &copies) {
             PNP_HIP(hipStreamSynchronize(ctx->stg_st[t]));
         } catch (...) {
             failed.store(1);
+            (void)hipStreamSynchronize(ctx->stg_st[t]);  // no DMA of this thread outlives the call
         }
     };
     std::vector<std::thread> th;
