@@ -644,7 +644,8 @@ def bench_msm(ctx, lg: int, steps: int, warmup: int, verify: bool, world: int, r
     ctx.kernel_timing(False)
     if world > 1:
         import torch.distributed as dist
-        t = torch.tensor([wall, ms], dtype=torch.float64, device="cuda")
+        dev = "cuda" if os.environ.get("PNP_BENCH_BACKEND", "nccl") == "nccl" else "cpu"  # (gloo rehearsal)
+        t = torch.tensor([wall, ms], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         wall, ms = (float(v) for v in t.tolist())
     per = ms / calls
