@@ -91,21 +91,34 @@ const uint64_t *commit_table(pnp_ctx *ctx, uint64_t n) {
     return ctx->ck_table.u64();
 }
 
-// Host -> HBM at PCIe speed from the caller's pageable buffers.  HIP's own
-// pageable copy stages through one host thread (the 19 GB prover key of
-// HEIGHT = 15 crossed in ~0.67 s, ~29 GB/s, profiles/r06_cold_calls.json);
-// here kStgThreads threads each memcpy 8-MiB chunks into two pinned staging
-// buffers of their own and DMA them on a stream of their own, so the host
-// copies and the DMAs of several chunks overlap (small chunks: pinning the
-// staging memory is the fixed cost of a cold call, ~0.4 ms per MiB).  Copies
-// below 4 MiB go through hipMemcpy directly.  PNP_H2D_STAGED=0:
-// hipMemcpyAsync throughout.
+// Host -> HBM from the caller's pageable buffers: kStgThreads threads each
+// memcpy 8-MiB chunks into two pinned staging buffers of their own and DMA them
+// on a stream of their own, so the host copies and the DMAs of several chunks
+// overlap (small chunks: pinning the staging memory is a fixed cost of a cold
+// call, ~0.4 ms per MiB).  Copies below 4 MiB go through hipMemcpyAsync
+// directly.  Measured against HIP's pageable copy (~29-32 GB/s for the 19.5 GB
+// prover key of HEIGHT = 15 either way): level on one box, ahead on another
+// when the SRS table builds beside the upload (the v1 call one
+// proof per process).  PNP_H2D_STAGED=0: hipMemcpyAsync throughout; also the
+// fallback when the staging memory cannot be pinned.
 static bool h2d_staged_enabled() {
     static const bool on = [] {
         const char *e = getenv("PNP_H2D_STAGED");
         return !(e && atoi(e) == 0);
     }();
     return on;
+}
+static void h2d_release(pnp_ctx *ctx) {
+    for (int k = 0; k < 2 * pnp_ctx::kStgThreads; k++) {
+        if (ctx->stg_buf[k]) (void)hipHostFree(ctx->stg_buf[k]);
+        if (ctx->stg_ev[k]) (void)hipEventDestroy(ctx->stg_ev[k]);
+        ctx->stg_buf[k] = nullptr;
+        ctx->stg_ev[k] = nullptr;
+    }
+    for (int t = 0; t < pnp_ctx::kStgThreads; t++) {
+        if (ctx->stg_st[t]) (void)hipStreamDestroy(ctx->stg_st[t]);
+        ctx->stg_st[t] = nullptr;
+    }
 }
 void h2d_batch(pnp_ctx *ctx, const std::vector<H2D> &copies) {
     constexpr size_t CH = 8u << 20;
@@ -128,12 +141,21 @@ void h2d_batch(pnp_ctx *ctx, const std::vector<H2D> &copies) {
     PNP_HIP(hipStreamSynchronize(ctx->stream));
     if (chunks.empty()) return;
     constexpr int T = pnp_ctx::kStgThreads;
-    if (!ctx->stg_buf[0]) {
-        for (int k = 0; k < 2 * T; k++) {
-            PNP_HIP(hipHostMalloc(&ctx->stg_buf[k], CH, hipHostMallocDefault));
-            PNP_HIP(hipEventCreateWithFlags(&ctx->stg_ev[k], hipEventDisableTiming));
+    if (!ctx->stg_st[T - 1]) {  // the pool, all of it or none (the last member is made last)
+        bool ok = true;
+        for (int k = 0; k < 2 * T && ok; k++)
+            ok = hipHostMalloc(&ctx->stg_buf[k], CH, hipHostMallocDefault) == hipSuccess &&
+                 hipEventCreateWithFlags(&ctx->stg_ev[k], hipEventDisableTiming) == hipSuccess;
+        for (int t = 0; t < T && ok; t++)
+            ok = hipStreamCreateWithFlags(&ctx->stg_st[t], hipStreamNonBlocking) == hipSuccess;
+        if (!ok) {
+            (void)hipGetLastError();
+            h2d_release(ctx);
+            for (const Chunk &c : chunks)
+                PNP_HIP(hipMemcpyAsync(c.dst, c.src, c.bytes, hipMemcpyHostToDevice, ctx->stream));
+            PNP_HIP(hipStreamSynchronize(ctx->stream));
+            return;
         }
-        for (int t = 0; t < T; t++) PNP_HIP(hipStreamCreateWithFlags(&ctx->stg_st[t], hipStreamNonBlocking));
     }
     std::atomic<size_t> next{0};
     std::atomic<int> failed{0};
@@ -164,14 +186,6 @@ void h2d_batch(pnp_ctx *ctx, const std::vector<H2D> &copies) {
         set_error("host -> HBM staged upload failed");
         throw Error(PNP_E_DEVICE);
     }
-}
-static void h2d_release(pnp_ctx *ctx) {
-    for (int k = 0; k < 2 * pnp_ctx::kStgThreads; k++) {
-        if (ctx->stg_buf[k]) (void)hipHostFree(ctx->stg_buf[k]);
-        if (ctx->stg_ev[k]) (void)hipEventDestroy(ctx->stg_ev[k]);
-    }
-    for (int t = 0; t < pnp_ctx::kStgThreads; t++)
-        if (ctx->stg_st[t]) (void)hipStreamDestroy(ctx->stg_st[t]);
 }
 
 void ck_derived_reset(pnp_ctx *ctx) {
