@@ -211,7 +211,7 @@ def test_sharded_gen_proof_parity(tmp_path, world, shard):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("world", [2, 4, 8])
 def test_sharded_slot_overflow_redone(tmp_path, world):
     """The fixed-slot bucket exchange with slots far too small
     (PNP_TEST_SLOT_CAP=64 records): every batch of the second proof overflows,
