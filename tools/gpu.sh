@@ -34,7 +34,7 @@ run_step() {
   [ "$arg" = "$step" ] && arg=""
   case "$step" in
     tests*)
-      timeout -k 10 1100 python -u -m pytest tests -m gpu -x -v --timeout ${TEST_TIMEOUT:-400} --timeout-method thread \
+      timeout -k 10 1100 python -u -m pytest tests -m gpu -x -v -rs --timeout ${TEST_TIMEOUT:-400} --timeout-method thread \
           ${arg:+-k "${arg//+/ }"} > "$OUT/pytest_gpu.log" 2>&1 ;;
     smoke)
       timeout -k 10 180 python -u -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 ;;
