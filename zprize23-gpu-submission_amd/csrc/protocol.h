@@ -20,6 +20,7 @@ struct PermArgs {
     const uint64_t *sigma[4];  // sigma evaluations on the n-domain
     Fr bk[4];                  // beta * k_j, k = 1, 7, 13, 17
     Fr beta, gamma, omega;
+    const uint64_t *tw;  // w^e, e < max(n/2, 1): the NTT's forward twiddles (ntt_twiddles)
 };
 
 // nullptr arrays are known-zero and not read, except z28: nullptr means the

@@ -69,37 +69,37 @@ void k_query_f(uint64_t *out, const uint64_t *ql, uint64_t n_gates, const uint64
 }
 
 // num_i = prod_j (w_j + beta k_j w^i + gamma), den_i = prod_j (w_j + beta sigma_j + gamma)
-static constexpr int PCHUNK = 16;
-// Grid-stride over the domain (element i = t + k T, T = total lanes): loads
-// coalesced across the wave (one lane per 16 consecutive elements strided
-// every load by 512 B, 1.3 ms at 2^22); x = w^i stepped by w^T; x beta k_j by
+// One element a lane, x_i = w^i read from the NTT's forward twiddle table
+// (w^e for e < n/2; w^(e + n/2) = -w^e).  The earlier form — 16 elements a
+// lane on n/16 lanes, a per-lane power of w and a stepped chain — held one
+// wave a SIMD and ran latency-bound (1.1-1.2 ms at 2^22, ~5x its VALU and
+// HBM floors); the table read is 32 B an element of ~350.  x beta k_j by
 // doublings from x beta (k = 1, 7, 13, 17, as the quotient).
-__global__ void k_perm_numden_(uint64_t *num, uint64_t *den, PermArgs a, Fr step, uint64_t n) {
-    const uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
-    const uint64_t T = (uint64_t)gridDim.x * blockDim.x;
-    if (t >= n) return;
-    Fr xb = pow_u64(a.omega, t) * a.beta;  // beta x_i, stepped (no root * beta per element)
-    for (uint64_t i = t; i < n; i += T) {
-        const Fr x2 = xb + xb, x4 = x2 + x2, x8 = x4 + x4;
-        const Fr xk[4] = {xb, x8 - xb, x8 + x4 + xb, x8 + x8 + xb};
-        Fr w = load_fr(a.w[0], i);
-        Fr nm = w + xk[0] + a.gamma;  // the first factors start the products (no 1 * f)
-        Fr dn = w + load_fr(a.sigma[0], i) * a.beta + a.gamma;
+__global__ __launch_bounds__(256) void k_perm_numden_(uint64_t *num, uint64_t *den, PermArgs a, uint64_t n) {
+    const uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint64_t half = n > 1 ? n >> 1 : 1;
+    const Fr xb = i < half ? load_fr(a.tw, i) * a.beta : load_fr(a.tw, i - half) * neg(a.beta);
+    const Fr x2 = xb + xb, x4 = x2 + x2, x8 = x4 + x4;
+    const Fr xk[4] = {xb, x8 - xb, x8 + x4 + xb, x8 + x8 + xb};
+    Fr w = load_fr(a.w[0], i);
+    Fr nm = w + xk[0] + a.gamma;  // the first factors start the products (no 1 * f)
+    Fr dn = w + load_fr(a.sigma[0], i) * a.beta + a.gamma;
 #pragma unroll
-        for (int j = 1; j < 4; j++) {
-            w = load_fr(a.w[j], i);
-            nm = nm * (w + xk[j] + a.gamma);
-            dn = dn * (w + load_fr(a.sigma[j], i) * a.beta + a.gamma);
-        }
-        store_fr(num, i, nm);
-        store_fr(den, i, dn);
-        xb = xb * step;
+    for (int j = 1; j < 4; j++) {
+        w = load_fr(a.w[j], i);
+        nm = nm * (w + xk[j] + a.gamma);
+        dn = dn * (w + load_fr(a.sigma[j], i) * a.beta + a.gamma);
     }
+    store_fr(num, i, nm);
+    store_fr(den, i, dn);
 }
 void k_perm_numden(uint64_t *num, uint64_t *den, const PermArgs &a, uint64_t n, hipStream_t s) {
-    const uint64_t blocks = nblk((n + PCHUNK - 1) / PCHUNK);
-    const Fr step = pow_u64(a.omega, blocks * 256);
-    hipLaunchKernelGGL(k_perm_numden_, dim3((uint32_t)blocks), dim3(256), 0, s, num, den, a, step, n);
+    if (!a.tw) {
+        set_error("k_perm_numden: twiddle table missing");
+        throw Error(PNP_E_ARG);
+    }
+    hipLaunchKernelGGL(k_perm_numden_, dim3(nblk(n)), dim3(256), 0, s, num, den, a, n);
     PNP_HIP(hipGetLastError());
 }
 

@@ -50,15 +50,55 @@ Fr root_of_unity(uint32_t lg) {
 
 namespace {
 
+// Stage times.  By default a mark waits for the main stream and reads the
+// host clock; PNP_STAGE_SYNC=0 records an event instead (no host wait) and
+// the stage is the stream time between consecutive marks, read back once the
+// proof has returned its last commitment (the waits between the quotient, its
+// inverse transforms and the round-6 divisions and their MSMs go; A/B in
+// DESIGN.md 7).
 struct Timer {
     pnp_ctx *ctx;
     std::chrono::steady_clock::time_point t0;
-    explicit Timer(pnp_ctx *c) : ctx(c), t0(std::chrono::steady_clock::now()) { ctx->stages.clear(); }
+    std::vector<const char *> names;
+    static bool sync_marks() {
+        static const bool v = [] {
+            const char *e = getenv("PNP_STAGE_SYNC");
+            return !e || atoi(e) != 0;
+        }();
+        return v;
+    }
+    hipEvent_t event(size_t k) {
+        while (ctx->stage_ev.size() <= k) {
+            hipEvent_t e;
+            PNP_HIP(hipEventCreate(&e));
+            ctx->stage_ev.push_back(e);
+        }
+        return ctx->stage_ev[k];
+    }
+    explicit Timer(pnp_ctx *c) : ctx(c), t0(std::chrono::steady_clock::now()) {
+        ctx->stages.clear();
+        if (!sync_marks()) PNP_HIP(hipEventRecord(event(0), ctx->stream));
+    }
     void mark(const char *name) {
+        if (!sync_marks()) {
+            names.push_back(name);
+            PNP_HIP(hipEventRecord(event(names.size()), ctx->stream));
+            return;
+        }
         PNP_HIP(hipStreamSynchronize(ctx->stream));
         auto t1 = std::chrono::steady_clock::now();
         ctx->stages.emplace_back(name, std::chrono::duration<double, std::milli>(t1 - t0).count());
         t0 = t1;
+    }
+    // after the last mark (every exit: a failed proof reports what completed)
+    ~Timer() {
+        if (sync_marks() || names.empty()) return;
+        if (hipEventSynchronize(ctx->stage_ev[names.size()]) != hipSuccess) return;
+        for (size_t k = 0; k < names.size(); k++) {
+            float ms = 0.f;
+            if (hipEventElapsedTime(&ms, ctx->stage_ev[k], ctx->stage_ev[k + 1]) != hipSuccess) return;
+            ctx->stages.emplace_back(names[k], (double)ms);
+        }
     }
 };
 
@@ -397,6 +437,7 @@ int prove_impl(pnp_ctx *ctx, const CircuitC *cs, int device_ptrs, ProofC *out, c
     pa.beta = beta;
     pa.gamma = gamma;
     pa.omega = root_of_unity(lg);
+    pa.tw = ntt_twiddles(nt, lg, false, s);  // built by ntt_warm above
     uint64_t *num = ctx->buf("num", n), *den = ctx->buf("den", n);
     uint64_t *z_poly = ctx->buf("z_poly", n);
     k_perm_numden(num, den, pa, n, s);
@@ -668,7 +709,6 @@ int prove_impl(pnp_ctx *ctx, const CircuitC *cs, int device_ptrs, ProofC *out, c
             alg((double)NBq * (nread + 1));
         }
         tm.mark("r4_quotient");
-        ctx->ktimer.collect();
         // Intt_coset of the coset values: per block an unscaled size-n inverse
         // transform and a twist, then per coefficient index an inverse DFT (8
         // blocks, ntt.hip t_combine) or Vandermonde solve (6 / 7 blocks,
@@ -759,6 +799,7 @@ int prove_impl(pnp_ctx *ctx, const CircuitC *cs, int device_ptrs, ProofC *out, c
         const char *tl[8] = {"t_1", "t_2", "t_3", "t_4", "t_5", "t_6", "t_7", "t_8"};
         for (int k = 0; k < 8; k++) append_comm(tr, tl[k], *tcm[k]);
         tm.mark("r4_commit");
+        ctx->ktimer.collect();  // the quotient's events (the commitments' read-back drained the stream)
 
         // ---------------- round 5: linearisation (linearisation.cu:73-306)
         Fr zc = tr.challenge_scalar("z");
