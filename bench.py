@@ -174,11 +174,40 @@ MADS_PER_FR_PRODUCT = 128  # 2 x 8 x 8: a b and m q of a 256-bit Montgomery prod
 # the radix-4 NTT group's ISA: 1,403 VALU per 4 butterflies, 73%
 # of them the 8-limb product's v_mad_u64_u32 / v_addc_co_u32 pairs (~4.4 cycles
 # each per wave64, profiles/r02_ubench_ops.txt), the rest ~2.2: ~3.8 on average
+# k_quotient29_ on the Merkle path (no q_m, one closed-form PI): issue cycles
+# per wave of 64 coset points, tools/isa_model.py on protocol.hip with the
+# q_m and pi8 branches removed (4,832 v_mad_u64_u32 of 8,709 VALU)
+QUOT29_CYCLES_PER_WAVE = 32434
 NTT_VALU_PER_BUTTERFLY = 351
 NTT_CYCLES_PER_VALU = 0.73 * 4.4 + 0.27 * 2.2
 SIMDS, CLOCK_HZ = 256 * 4, 2.4e9
 HELD_CLOCK_GHZ = 2.10  # k_accumulate29 under load (DVFS), PMC clock pass, profiles/r02_pmc_clock.txt
 UBENCH_FILE = os.path.join(REPO, "profiles", "r02_ubench_ops.txt")
+
+
+def quotient_roofline(q_ms, q_n, q_gbs, points, prods, merkle):
+    """The quotient kernel's line: VALU-bound (VERDICT r05 asked the same of the
+    NTT): ~35 Fr products per coset point against 26-36 B of each of ~26 arrays
+    — at 8 TB/s the reads take ~40% of the time the products do.  Fr products
+    credited by the prover per launch (the path taken), against the textbook
+    256-bit Montgomery peak; the compiled kernel's issue model (Merkle path)
+    and the HBM figure beside it."""
+    out = {"bound": "valu", "launch_ms": round(q_ms / max(q_n, 1), 3),
+           "hbm_achieved_gbs": round(q_gbs, 1), "hbm_peak_gbs": HBM_PEAK_GBS,
+           "hbm_frac": round(q_gbs / HBM_PEAK_GBS, 4)}
+    if q_ms <= 0 or not prods:  # the generic (non radix-2^29) quotient: no count
+        out.update({"achieved": None, "peak": None, "frac": None})
+        return out
+    s = q_ms / 1e3
+    fr_peak = SIMDS * CLOCK_HZ * 64 / mad_cycles() / MADS_PER_FR_PRODUCT
+    out.update({"achieved": round(prods / s / 1e9, 2), "peak": round(fr_peak / 1e9, 2),
+                "unit": "G Fr-mul/s", "frac": round(prods / s / fr_peak, 4),
+                "work": "Fr products per coset point on the launched path (34, + 2 with q_m, + 1 with "
+                        "the closed-form PI: prover.cpp) x points / HIP-event launch time",
+                "points_per_launch": round(points / max(q_n, 1))})
+    if merkle:
+        out["issue_model_frac"] = round(points / s / 64 * QUOT29_CYCLES_PER_WAVE / (SIMDS * CLOCK_HZ), 4)
+    return out
 
 
 def mad_cycles():
@@ -853,6 +882,7 @@ def main():
     dense = ctx.kernel_bytes("msm_entries_dense")      # the dense bound (MSMs x windows x points)
     q_ms, q_n = ctx.kernel_stats("quotient")
     q_bytes = ctx.kernel_bytes("quotient")
+    q_points, q_prods = ctx.kernel_bytes("quotient_points"), ctx.kernel_bytes("quotient_fr_products")
     redo_lanes = ctx.kernel_bytes("msm_redo_lanes")
     exact_fallbacks = ctx.kernel_bytes("msm_exact_fallback")
     # bucket-range exchange (world > 1 or --solo): batches moved through the
@@ -968,9 +998,8 @@ def main():
                                  "survey_bytes_per_launch": round(dense / max(acc_n, 1) / msm_windows(args.lg) * 128),
                                  "traffic_over_survey": (round(traffic / (dense / max(acc_n, 1) / msm_windows(args.lg) * 128), 2)
                                                          if traffic and dense else None)},
-                         "quotient": {"bound": "hbm", "achieved": round(q_gbs, 1),
-                                      "peak": HBM_PEAK_GBS, "frac": round(q_gbs / HBM_PEAK_GBS, 4),
-                                      "launch_ms": round(q_ms / max(q_n, 1), 3)}},
+                         "quotient": quotient_roofline(q_ms, q_n, q_gbs, q_points, q_prods,
+                                                       args.circuit == "merkle")},
             "stages_ms": {k: round(v, 2) for k, v in stages},
             "hbm_gbs": round(proof_bytes / per_proof / 1e9, 1),
             "hbm_whole_proof": {"bytes_per_proof": round(proof_bytes), "achieved_gbs": round(proof_bytes / per_proof / 1e9, 1),

@@ -694,7 +694,6 @@ void pnp_ctx_destroy(pnp_ctx *ctx) {
     (void)hipStreamDestroy(ctx->stream);
     h2d_release(ctx);
     for (hipEvent_t e : ctx->ktimer.pool) (void)hipEventDestroy(e);
-    for (hipEvent_t e : ctx->stage_ev) (void)hipEventDestroy(e);
     for (auto &p : ctx->ktimer.pending) {
         (void)hipEventDestroy(p.e0);
         (void)hipEventDestroy(p.e1);

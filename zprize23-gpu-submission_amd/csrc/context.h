@@ -136,7 +136,6 @@ struct pnp_ctx {
 
     // ---- stage timing of the last proof ----
     std::vector<std::pair<std::string, double>> stages;
-    std::vector<hipEvent_t> stage_ev;  // prover.cpp Timer: one timing event per stage mark
 };
 
 namespace pnp {

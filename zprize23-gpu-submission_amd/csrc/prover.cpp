@@ -50,55 +50,15 @@ Fr root_of_unity(uint32_t lg) {
 
 namespace {
 
-// Stage times.  By default a mark waits for the main stream and reads the
-// host clock; PNP_STAGE_SYNC=0 records an event instead (no host wait) and
-// the stage is the stream time between consecutive marks, read back once the
-// proof has returned its last commitment (the waits between the quotient, its
-// inverse transforms and the round-6 divisions and their MSMs go; A/B in
-// DESIGN.md 7).
 struct Timer {
     pnp_ctx *ctx;
     std::chrono::steady_clock::time_point t0;
-    std::vector<const char *> names;
-    static bool sync_marks() {
-        static const bool v = [] {
-            const char *e = getenv("PNP_STAGE_SYNC");
-            return !e || atoi(e) != 0;
-        }();
-        return v;
-    }
-    hipEvent_t event(size_t k) {
-        while (ctx->stage_ev.size() <= k) {
-            hipEvent_t e;
-            PNP_HIP(hipEventCreate(&e));
-            ctx->stage_ev.push_back(e);
-        }
-        return ctx->stage_ev[k];
-    }
-    explicit Timer(pnp_ctx *c) : ctx(c), t0(std::chrono::steady_clock::now()) {
-        ctx->stages.clear();
-        if (!sync_marks()) PNP_HIP(hipEventRecord(event(0), ctx->stream));
-    }
+    explicit Timer(pnp_ctx *c) : ctx(c), t0(std::chrono::steady_clock::now()) { ctx->stages.clear(); }
     void mark(const char *name) {
-        if (!sync_marks()) {
-            names.push_back(name);
-            PNP_HIP(hipEventRecord(event(names.size()), ctx->stream));
-            return;
-        }
         PNP_HIP(hipStreamSynchronize(ctx->stream));
         auto t1 = std::chrono::steady_clock::now();
         ctx->stages.emplace_back(name, std::chrono::duration<double, std::milli>(t1 - t0).count());
         t0 = t1;
-    }
-    // after the last mark (every exit: a failed proof reports what completed)
-    ~Timer() {
-        if (sync_marks() || names.empty()) return;
-        if (hipEventSynchronize(ctx->stage_ev[names.size()]) != hipSuccess) return;
-        for (size_t k = 0; k < names.size(); k++) {
-            float ms = 0.f;
-            if (hipEventElapsedTime(&ms, ctx->stage_ev[k], ctx->stage_ev[k + 1]) != hipSuccess) return;
-            ctx->stages.emplace_back(names[k], (double)ms);
-        }
     }
 };
 
@@ -670,6 +630,13 @@ int prove_impl(pnp_ctx *ctx, const CircuitC *cs, int device_ptrs, ProofC *out, c
                 return PNP_E_ARG;
             }
             k_quotient29(q2, NBq, t_blk, s);
+            // VALU work for bench.py's roofline: Fr products per point on the
+            // path this launch takes (protocol.hip k_quotient29_: 5 paired
+            // products = 10, three fifth powers = 9, 14 more; + 2 with q_m, + 1
+            // with the closed-form PI)
+            ctx->ktimer.credit("quotient_points", (double)NBq);
+            ctx->ktimer.credit("quotient_fr_products",
+                               (double)NBq * (34 + (q2.q_m ? 2 : 0) + (q2.pinv ? 1 : 0)));
             // (the byte accounting below counts the arrays this kernel read)
             q.q_m = q2.q_m, q.q_l = q2.q_l, q.q_r = q2.q_r, q.q_o = q2.q_o, q.q_4 = q2.q_4, q.q_c = q2.q_c;
             q.q_hl = q2.q_hl, q.q_hr = q2.q_hr, q.q_h4 = q2.q_h4, q.q_arith = q2.q_arith, q.lin = q2.lin;
