@@ -226,8 +226,8 @@ def test_madd_chain(seed):
     assert Y * pow(ZZZ, -1, Q) % Q == ref[1]
 
 
-# ---- general XYZZ addition / doubling in radix 2^29 (groundwork for the
-# bucket merge and tree in F29; not yet used by a kernel)
+# ---- general XYZZ addition / doubling in radix 2^29 (ec29.cuh: the bucket
+# merge and the reduction tree)
 def add29n(a, b):
     """a + b with carries normalised (limbs < 2^29)."""
     r, c = [0] * 14, 0
@@ -335,5 +335,71 @@ def test_xadd_xdbl_chain(seed):
             ref[i] = _dbl_aff(ref[i])
         else:
             X[i] = xadd29(X[i], X[j])
+            ref[i] = aff_add(ref[i], ref[j])
+        assert _aff(X[i]) == ref[i]
+
+
+# ---- the quad-lane forms of the tree's top levels (msm_reduce.hip xadd29w /
+# xdbl29w): the same products issued four at a time, squares as mul29, and
+# Y3 as two products summed instead of one two-product reduction
+def xadd29w(p, q):
+    KA, KB = C["F29_KA"], C["F29_KB"]
+    X1, Y1, ZZ1, ZZZ1 = p
+    X2, Y2, ZZ2, ZZZ2 = q
+    for v in (X1, Y1, X2, Y2):
+        assert val(v) < 2**389
+    for v in (ZZ1, ZZZ1, ZZ2, ZZZ2):
+        assert val(v) < 2**382
+    u1, u2, s1, s2 = mul29(X1, ZZ2), mul29(X2, ZZ1), mul29(Y1, ZZZ2), mul29(Y2, ZZZ1)
+    P, R = sub29(u2, u1, KB), sub29(s2, s1, KB)
+    assert val(P) < 2**391 and val(R) < 2**391
+    pp, rr, zz12, zzz12 = mul29(P, P), mul29(R, R), mul29(ZZ1, ZZ2), mul29(ZZZ1, ZZZ2)
+    ppp, q_, zz3 = mul29(P, pp), mul29(u1, pp), mul29(zz12, pp)
+    x3 = sub29(sub29(sub29(rr, ppp, KA), q_, KA), q_, KA)
+    assert val(x3) < 2**389
+    t, nppp = sub29(q_, x3, KB), sub29([0] * 14, ppp, KA)
+    assert val(t) < 2**391 and val(nppp) < 2**391
+    y3 = add29n(mul29(R, t), mul29(s1, nppp))
+    assert val(y3) < 2**383 and all(x < 2**29 for x in y3[:13])
+    return x3, y3, zz3, mul29(zzz12, ppp)
+
+
+def xdbl29w(p):
+    KA, KB = C["F29_KA"], C["F29_KB"]
+    X, Y, ZZ, ZZZ = p
+    assert val(X) < 2**389 and val(Y) < 2**389
+    assert val(ZZ) < 2**382 and val(ZZZ) < 2**382
+    U = add29n(Y, Y)
+    assert val(U) < 2**391
+    V, xx = mul29(U, U), mul29(X, X)
+    M = add29n(add29n(xx, xx), xx)
+    assert val(M) < 2**391
+    W, S, mm, zz3 = mul29(U, V), mul29(X, V), mul29(M, M), mul29(V, ZZ)
+    x3 = sub29(sub29(mm, S, KA), S, KA)
+    assert val(x3) < 2**389
+    t, ny = sub29(S, x3, KB), sub29([0] * 14, Y, KB)
+    assert val(t) < 2**391 and val(ny) < 2**391
+    y3 = add29n(mul29(M, t), mul29(W, ny))
+    assert val(y3) < 2**383
+    return x3, y3, zz3, mul29(W, ZZZ)
+
+
+@pytest.mark.parametrize("seed", [21, 22])
+def test_quad_forms_chain(seed):
+    """The reduction tree's operation mix through the quad-lane forms, fed
+    with the serial forms' outputs and their own (both Y bounds), every bound
+    asserted, against affine arithmetic."""
+    rnd = random.Random(seed)
+    pts = [_mulg(rnd.randrange(1, 2**64)) for _ in range(6)]
+    X = [(to_m(x), to_m(y), to_m(1), to_m(1)) for x, y in pts]
+    ref = list(pts)
+    for step in range(48):
+        i, j = rnd.randrange(len(X)), rnd.randrange(len(X))
+        wide = step % 3 != 0
+        if i == j or rnd.random() < 0.3:
+            X[i] = (xdbl29w if wide else xdbl29)(X[i])
+            ref[i] = _dbl_aff(ref[i])
+        else:
+            X[i] = (xadd29w if wide else xadd29)(X[i], X[j])
             ref[i] = aff_add(ref[i], ref[j])
         assert _aff(X[i]) == ref[i]

@@ -330,6 +330,113 @@ __global__ __launch_bounds__(256) void k_tree_level29(const uint32_t *in, uint64
     store_xyzz29(out + 168 * t + 56 * c, r);
 }
 
+// ---- the tree's top levels, four lanes per point operation.
+// Below ~2^14 nodes a level is latency-bound: 3 lanes a node, a few waves on
+// the whole chip, each lane running two dependent additions of ~14 serial
+// Montgomery products (~16 us each).  Here the four lanes of a quad share one
+// operation: every round each lane does ONE product (lane-selected operands)
+// and the quad exchanges the four results (__shfl within width 4), so an
+// addition is 4 product rounds deep and a doubling 3, instead of 14 and 8.
+// Same formulas as ec29.cuh xadd29 / xdbl29 (squares as mul29: the same
+// limbs, tests/test_field29.py), except Y3 = R (Q - X3) + S1 (K - PPP) as
+// two products summed (< 2^383) instead of one two-product reduction;
+// tests/test_field29.py models both (xadd29w / xdbl29w).
+// (masks, not a conditional chain: LLVM turns that into a private array
+// indexed by r — 1.3 KB of scratch a lane)
+__device__ __forceinline__ F29 qsel(int r, const F29 &a0, const F29 &a1, const F29 &a2, const F29 &a3) {
+    const uint32_t m0 = 0u - (uint32_t)(r == 0), m1 = 0u - (uint32_t)(r == 1), m2 = 0u - (uint32_t)(r == 2),
+                   m3 = 0u - (uint32_t)(r == 3);
+    F29 v;
+#pragma unroll
+    for (int i = 0; i < 14; i++) v.l[i] = (a0.l[i] & m0) | (a1.l[i] & m1) | (a2.l[i] & m2) | (a3.l[i] & m3);
+    return v;
+}
+// lane `src`'s value to every lane of the quad
+__device__ __forceinline__ F29 qget(const F29 &v, int src) {
+    F29 r;
+#pragma unroll
+    for (int i = 0; i < 14; i++) r.l[i] = (uint32_t)__shfl((int)v.l[i], src, 4);
+    return r;
+}
+__device__ __forceinline__ F29 add29n(const F29 &a, const F29 &b) {
+    F29 r;
+    uint32_t c = 0;
+#pragma unroll
+    for (int i = 0; i < 13; i++) {
+        const uint32_t t = a.l[i] + b.l[i] + c;
+        r.l[i] = t & F29_M;
+        c = t >> 29;
+    }
+    r.l[13] = a.l[13] + b.l[13] + c;
+    return r;
+}
+// p + q on a quad (every lane holds both operands); no exceptional cases
+__device__ __forceinline__ Xyzz29 xadd29w(const Xyzz29 &p, const Xyzz29 &q, int r) {
+    const F29 m1 = mul29(qsel(r, p.x, q.x, p.y, q.y), qsel(r, q.zz, p.zz, q.zzz, p.zzz));
+    const F29 u1 = qget(m1, 0), s1 = qget(m1, 2);
+    const F29 P = sub29(qget(m1, 1), u1, F29_KB), R = sub29(qget(m1, 3), s1, F29_KB);
+    const F29 m2 = mul29(qsel(r, P, R, p.zz, p.zzz), qsel(r, P, R, q.zz, q.zzz));
+    const F29 pp = qget(m2, 0), zzz12 = qget(m2, 3);
+    const F29 m3 = mul29(qsel(r, P, u1, qget(m2, 2), P), pp);
+    const F29 ppp = qget(m3, 0), qq = qget(m3, 1);
+    Xyzz29 o;
+    o.zz = qget(m3, 2);
+    o.x = sub29(sub29(sub29(qget(m2, 1), ppp, F29_KA), qq, F29_KA), qq, F29_KA);
+    const F29 m4 = mul29(qsel(r, zzz12, R, s1, zzz12),
+                         qsel(r, ppp, sub29(qq, o.x, F29_KB), neg29(ppp, F29_KA), ppp));
+    o.zzz = qget(m4, 0);
+    o.y = add29n(qget(m4, 1), qget(m4, 2));
+    return o;
+}
+// 2 p on a quad (dbl-2008-s-1, a = 0)
+__device__ __forceinline__ Xyzz29 xdbl29w(const Xyzz29 &p, int r) {
+    const F29 U = add29n(p.y, p.y);
+    const F29 a1 = qsel(r, U, p.x, U, p.x);
+    const F29 m1 = mul29(a1, a1);
+    const F29 V = qget(m1, 0), xx = qget(m1, 1);
+    const F29 M = add29n(add29n(xx, xx), xx);
+    const F29 m2 = mul29(qsel(r, U, p.x, M, V), qsel(r, V, V, M, p.zz));
+    const F29 W = qget(m2, 0), S = qget(m2, 1);
+    Xyzz29 o;
+    o.zz = qget(m2, 3);
+    o.x = sub29(sub29(qget(m2, 2), S, F29_KA), S, F29_KA);
+    const F29 m3 = mul29(qsel(r, W, M, W, W), qsel(r, p.zzz, sub29(S, o.x, F29_KB), neg29(p.y, F29_KB), p.zzz));
+    o.zzz = qget(m3, 0);
+    o.y = add29n(qget(m3, 1), qget(m3, 2));
+    return o;
+}
+// the *_inf forms of ec29.cuh; the tests on the operands are the same on the
+// four lanes of a quad, so a quad never diverges inside an operation
+__device__ __forceinline__ Xyzz29 xadd29w_inf(const Xyzz29 &p, const Xyzz29 &q, int r, uint32_t *exc) {
+    if (zero29(p.zz)) return q;
+    if (zero29(q.zz)) return p;
+    Xyzz29 o = xadd29w(p, q, r);
+    if (zero29(o.zz)) *exc = 1u;
+    return o;
+}
+__device__ __forceinline__ Xyzz29 xdbl29w_inf(const Xyzz29 &p, int r) {
+    if (zero29(p.zz)) return p;
+    return xdbl29w(p, r);
+}
+// k_tree_level29 with a quad per (node, component); lane r stores coordinate r
+__global__ __launch_bounds__(256) void k_tree_level29w(const uint32_t *in, uint64_t nout, uint32_t *out,
+                                                       uint32_t *exc) {
+    const uint64_t t = (blockIdx.x * (uint64_t)blockDim.x + threadIdx.x) >> 2;
+    if (t >= nout) return;  // whole quads
+    const int c = (int)blockIdx.y, r = (int)(threadIdx.x & 3);
+    const uint32_t *L = in + 336 * t, *R = L + 168;
+    Xyzz29 v;
+    if (c == 0) {
+        v = xadd29w_inf(load_xyzz29(L), load_xyzz29(R), r, exc);
+    } else if (c == 1) {
+        v = xadd29w_inf(xadd29w_inf(load_xyzz29(L + 56), load_xyzz29(R + 56), r, exc), load_xyzz29(R + 112), r,
+                        exc);
+    } else {
+        v = xdbl29w_inf(xadd29w_inf(load_xyzz29(L + 112), load_xyzz29(R + 112), r, exc), r);
+    }
+    store_f29(out + 168 * t + 56 * c + 14 * r, qsel(r, v.x, v.y, v.zz, v.zzz));
+}
+
 // the roots' T in R384 (the host's 24-u64 XYZZ), then their S (a window's
 // plain bucket sum: a bucket-range shard adds lo * S, msm.hip)
 __global__ void k_tree_roots29(const uint32_t *in, uint64_t n, uint64_t *out) {
@@ -366,9 +473,18 @@ const uint64_t *msm_reduce29(const uint32_t *bk29, const uint32_t *offs, uint64_
     else
         hipLaunchKernelGGL(k_tree_leafw29<PNP_LEAF_W>, lgrid, dim3(256), 0, s, bk29, offs, m, a, exc);
     PNP_HIP(hipGetLastError());
+    // levels of at most PNP_TREE_WIDE nodes (latency-bound) on quads
+    static const uint64_t wide_max = [] {
+        const char *e = getenv("PNP_TREE_WIDE");
+        return (uint64_t)(e ? atoll(e) : 16384);
+    }();
     while (m > nwin) {
         m /= 2;
-        hipLaunchKernelGGL(k_tree_level29, dim3((uint32_t)((m + 255) / 256), 3), dim3(256), 0, s, a, m, b, exc);
+        if (m <= wide_max)
+            hipLaunchKernelGGL(k_tree_level29w, dim3((uint32_t)((4 * m + 255) / 256), 3), dim3(256), 0, s, a, m, b,
+                               exc);
+        else
+            hipLaunchKernelGGL(k_tree_level29, dim3((uint32_t)((m + 255) / 256), 3), dim3(256), 0, s, a, m, b, exc);
         PNP_HIP(hipGetLastError());
         std::swap(a, b);
     }
