@@ -335,7 +335,7 @@ __global__ __launch_bounds__(256) void k_tree_level29(const uint32_t *in, uint64
 // the whole chip, each lane running two dependent additions of ~14 serial
 // Montgomery products (~16 us each).  Here the four lanes of a quad share one
 // operation: every round each lane does ONE product (lane-selected operands)
-// and the quad exchanges the four results (__shfl within width 4), so an
+// and the quad exchanges the four results (DPP quad broadcasts), so an
 // addition is 4 product rounds deep and a doubling 3, instead of 14 and 8.
 // Same formulas as ec29.cuh xadd29 / xdbl29 (squares as mul29: the same
 // limbs, tests/test_field29.py), except Y3 = R (Q - X3) + S1 (K - PPP) as
@@ -351,11 +351,13 @@ __device__ __forceinline__ F29 qsel(int r, const F29 &a0, const F29 &a1, const F
     for (int i = 0; i < 14; i++) v.l[i] = (a0.l[i] & m0) | (a1.l[i] & m1) | (a2.l[i] & m2) | (a3.l[i] & m3);
     return v;
 }
-// lane `src`'s value to every lane of the quad
-__device__ __forceinline__ F29 qget(const F29 &v, int src) {
+// lane S's value to every lane of the quad: a DPP quad_perm broadcast
+// [S, S, S, S] (a VALU move; ds_bpermute went through the LDS crossbar)
+template <int S>
+__device__ __forceinline__ F29 qget(const F29 &v) {
     F29 r;
 #pragma unroll
-    for (int i = 0; i < 14; i++) r.l[i] = (uint32_t)__shfl((int)v.l[i], src, 4);
+    for (int i = 0; i < 14; i++) r.l[i] = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v.l[i], S * 0x55, 0xF, 0xF, false);
     return r;
 }
 __device__ __forceinline__ F29 add29n(const F29 &a, const F29 &b) {
@@ -373,19 +375,19 @@ __device__ __forceinline__ F29 add29n(const F29 &a, const F29 &b) {
 // p + q on a quad (every lane holds both operands); no exceptional cases
 __device__ __forceinline__ Xyzz29 xadd29w(const Xyzz29 &p, const Xyzz29 &q, int r) {
     const F29 m1 = mul29(qsel(r, p.x, q.x, p.y, q.y), qsel(r, q.zz, p.zz, q.zzz, p.zzz));
-    const F29 u1 = qget(m1, 0), s1 = qget(m1, 2);
-    const F29 P = sub29(qget(m1, 1), u1, F29_KB), R = sub29(qget(m1, 3), s1, F29_KB);
+    const F29 u1 = qget<0>(m1), s1 = qget<2>(m1);
+    const F29 P = sub29(qget<1>(m1), u1, F29_KB), R = sub29(qget<3>(m1), s1, F29_KB);
     const F29 m2 = mul29(qsel(r, P, R, p.zz, p.zzz), qsel(r, P, R, q.zz, q.zzz));
-    const F29 pp = qget(m2, 0), zzz12 = qget(m2, 3);
-    const F29 m3 = mul29(qsel(r, P, u1, qget(m2, 2), P), pp);
-    const F29 ppp = qget(m3, 0), qq = qget(m3, 1);
+    const F29 pp = qget<0>(m2), zzz12 = qget<3>(m2);
+    const F29 m3 = mul29(qsel(r, P, u1, qget<2>(m2), P), pp);
+    const F29 ppp = qget<0>(m3), qq = qget<1>(m3);
     Xyzz29 o;
-    o.zz = qget(m3, 2);
-    o.x = sub29(sub29(sub29(qget(m2, 1), ppp, F29_KA), qq, F29_KA), qq, F29_KA);
+    o.zz = qget<2>(m3);
+    o.x = sub29(sub29(sub29(qget<1>(m2), ppp, F29_KA), qq, F29_KA), qq, F29_KA);
     const F29 m4 = mul29(qsel(r, zzz12, R, s1, zzz12),
                          qsel(r, ppp, sub29(qq, o.x, F29_KB), neg29(ppp, F29_KA), ppp));
-    o.zzz = qget(m4, 0);
-    o.y = add29n(qget(m4, 1), qget(m4, 2));
+    o.zzz = qget<0>(m4);
+    o.y = add29n(qget<1>(m4), qget<2>(m4));
     return o;
 }
 // 2 p on a quad (dbl-2008-s-1, a = 0)
@@ -393,16 +395,16 @@ __device__ __forceinline__ Xyzz29 xdbl29w(const Xyzz29 &p, int r) {
     const F29 U = add29n(p.y, p.y);
     const F29 a1 = qsel(r, U, p.x, U, p.x);
     const F29 m1 = mul29(a1, a1);
-    const F29 V = qget(m1, 0), xx = qget(m1, 1);
+    const F29 V = qget<0>(m1), xx = qget<1>(m1);
     const F29 M = add29n(add29n(xx, xx), xx);
     const F29 m2 = mul29(qsel(r, U, p.x, M, V), qsel(r, V, V, M, p.zz));
-    const F29 W = qget(m2, 0), S = qget(m2, 1);
+    const F29 W = qget<0>(m2), S = qget<1>(m2);
     Xyzz29 o;
-    o.zz = qget(m2, 3);
-    o.x = sub29(sub29(qget(m2, 2), S, F29_KA), S, F29_KA);
+    o.zz = qget<3>(m2);
+    o.x = sub29(sub29(qget<2>(m2), S, F29_KA), S, F29_KA);
     const F29 m3 = mul29(qsel(r, W, M, W, W), qsel(r, p.zzz, sub29(S, o.x, F29_KB), neg29(p.y, F29_KB), p.zzz));
-    o.zzz = qget(m3, 0);
-    o.y = add29n(qget(m3, 1), qget(m3, 2));
+    o.zzz = qget<0>(m3);
+    o.y = add29n(qget<1>(m3), qget<2>(m3));
     return o;
 }
 // the *_inf forms of ec29.cuh; the tests on the operands are the same on the
@@ -444,6 +446,15 @@ __global__ void k_tree_roots29(const uint32_t *in, uint64_t n, uint64_t *out) {
     if (t >= n) return;
     store_xyzz(out + 24 * t, to32(load_xyzz29(in + 168 * t + 56)));
     store_xyzz(out + 24 * (n + t), to32(load_xyzz29(in + 168 * t)));
+}
+
+// k_tree_roots29 with a quad per root: lane r converts coordinate r
+__global__ void k_tree_roots29w(const uint32_t *in, uint64_t n, uint64_t *out) {
+    const uint64_t t = (blockIdx.x * (uint64_t)blockDim.x + threadIdx.x) >> 2;
+    if (t >= n) return;
+    const int r = (int)(threadIdx.x & 3);
+    store_fq(out + 24 * t + 6 * r, to_fq32(load29(in + 168 * t + 56 + 14 * r)));
+    store_fq(out + 24 * (n + t) + 6 * r, to_fq32(load29(in + 168 * t + 14 * r)));
 }
 
 const uint64_t *msm_reduce29(const uint32_t *bk29, const uint32_t *offs, uint64_t nwin, int NB,
@@ -488,7 +499,7 @@ const uint64_t *msm_reduce29(const uint32_t *bk29, const uint32_t *offs, uint64_
         PNP_HIP(hipGetLastError());
         std::swap(a, b);
     }
-    hipLaunchKernelGGL(k_tree_roots29, dim3((uint32_t)((nwin + 255) / 256)), dim3(256), 0, s, a, nwin, roots);
+    hipLaunchKernelGGL(k_tree_roots29w, dim3((uint32_t)((4 * nwin + 255) / 256)), dim3(256), 0, s, a, nwin, roots);
     PNP_HIP(hipGetLastError());
     return roots;
 }
