@@ -439,6 +439,41 @@ __global__ __launch_bounds__(256) void k_tree_level29w(const uint32_t *in, uint6
     store_f29(out + 168 * t + 56 * c + 14 * r, qsel(r, v.x, v.y, v.zz, v.zzz));
 }
 
+// k_tree_leafw29 with a quad per leaf (the same running sums and T == S
+// tracking; every branch depends on the leaf's buckets only, so a quad stays
+// converged): for the small leaf launches of the 8-rank bucket ranges, where
+// one lane per leaf is a few waves on the chip
+template <int LW>
+__global__ __launch_bounds__(256) void k_tree_leafw29w(const uint32_t *bk, const uint32_t *offs, uint64_t nout,
+                                                       uint32_t *out, uint32_t *exc) {
+    const uint64_t t = (blockIdx.x * (uint64_t)blockDim.x + threadIdx.x) >> 2;
+    if (t >= nout) return;  // whole quads
+    const int r = (int)(threadIdx.x & 3);
+    const uint64_t u0 = (uint64_t)LW * t;
+    Xyzz29 S = bucket29(bk, offs, u0 + LW - 1), T = S;
+    bool tis = true;
+#pragma unroll 1
+    for (int k = LW - 2; k >= 0; k--) {
+        const bool empty = offs[u0 + k] == offs[u0 + k + 1];
+        if (empty) {
+            T = tis ? xdbl29w_inf(T, r) : xadd29w_inf(T, S, r, exc);
+            tis = tis && zero29(T.zz);
+        } else {
+            S = xadd29w_inf(S, load_xyzz29(bk + 56 * (u0 + k)), r, exc);
+            const bool tinf = zero29(T.zz);
+            T = xadd29w_inf(T, S, r, exc);
+            tis = tinf;
+        }
+    }
+    uint32_t *o = out + 168 * t;
+    store_f29(o + 14 * r, qsel(r, S.x, S.y, S.zz, S.zzz));
+    store_f29(o + 56 + 14 * r, qsel(r, T.x, T.y, T.zz, T.zzz));
+    Xyzz29 D = S;
+#pragma unroll 1
+    for (int k = 1; k < LW; k *= 2) D = xdbl29w_inf(D, r);
+    store_f29(o + 112 + 14 * r, qsel(r, D.x, D.y, D.zz, D.zzz));
+}
+
 // the roots' T in R384 (the host's 24-u64 XYZZ), then their S (a window's
 // plain bucket sum: a bucket-range shard adds lo * S, msm.hip)
 __global__ void k_tree_roots29(const uint32_t *in, uint64_t n, uint64_t *out) {
@@ -477,7 +512,15 @@ const uint64_t *msm_reduce29(const uint32_t *bk29, const uint32_t *offs, uint64_
     uint32_t *a = scratch, *b = scratch + 168 * m;
     uint64_t *roots = reinterpret_cast<uint64_t *>(scratch + 252 * m);
     const dim3 lgrid((uint32_t)((m + 255) / 256));
-    if (LW == 2)
+    // small leaf launches (the 8-rank ranges' one- and two-MSM batches) on quads
+    static const uint64_t leaf_wide = [] {
+        const char *e = getenv("PNP_LEAF_WIDE");
+        return (uint64_t)(e ? atoll(e) : 32768);
+    }();
+    const dim3 wgrid((uint32_t)((4 * m + 255) / 256));
+    if (LW == 4 && m <= leaf_wide)
+        hipLaunchKernelGGL(k_tree_leafw29w<4>, wgrid, dim3(256), 0, s, bk29, offs, m, a, exc);
+    else if (LW == 2)
         hipLaunchKernelGGL(k_tree_leafw29<2>, lgrid, dim3(256), 0, s, bk29, offs, m, a, exc);
     else if (LW == 4)
         hipLaunchKernelGGL(k_tree_leafw29<4>, lgrid, dim3(256), 0, s, bk29, offs, m, a, exc);
